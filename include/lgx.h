@@ -1,0 +1,256 @@
+/*
+ * lgx.h — C-ABI of the MI355X-native legged-robot rollout engine (liblgx.so).
+ *
+ * This is the drop-in boundary that replaces the Isaac Gym tensor API used by the
+ * reference's LeggedRobot.  Each entry point cites the reference
+ * call(s) it replaces.  Conventions:
+ *   - plain C types only; every buffer is a *device* pointer owned by the caller
+ *     (the Python host allocates them as torch tensors and binds them once with
+ *     lgx_sim_create); the library owns only its constant tables and scratch;
+ *   - every call returns 0 on success and a negative LGX_E* code on failure;
+ *     lgx_last_error() returns a thread-local message; no C++ exception crosses the ABI;
+ *   - every launch is stream-ordered on the `stream` argument (a hipStream_t), no
+ *     host synchronisation happens inside any call (graph-capturable);
+ *   - one lgx_sim per GPU / rank; an instance is not thread-safe.
+ *
+ * Layouts (row-major, N = num_envs, units SI, quaternions xyzw as in the reference):
+ *   root_states [N,13]   pos3 quat4 linvel3 angvel3, world frame   (legged_robot.py:518)
+ *   dof_state   [N,12,2] (pos, vel) interleaved per DOF             (legged_robot.py:519-521)
+ *   contact_forces [N,B,3] net ground contact force per body         (legged_robot.py:524)
+ *   torques     [N,12]   applied joint drive torque                  (legged_robot.py:536)
+ */
+#ifndef LGX_H
+#define LGX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LGX_NUM_LEGS 4
+#define LGX_NUM_DOF 12
+#define LGX_NUM_DYN 13          /* base + 4 legs x (hip, thigh, shank+foot) */
+#define LGX_MAX_BODIES 17       /* reporting bodies in the contact-force tensor */
+#define LGX_MAX_POINTS 128      /* contact primitives (sphere centres / box corners) */
+#define LGX_MAX_OBS 256
+#define LGX_MAX_HEIGHT_POINTS 192
+#define LGX_MAX_TERMS 24
+
+/* error codes */
+#define LGX_OK 0
+#define LGX_EINVAL -1
+#define LGX_EHIP -2
+#define LGX_ENOMEM -3
+
+/* reward term ids: one per reference `_reward_<name>` (legged_robot.py:857-966) */
+enum lgx_reward_term {
+  LGX_R_LIN_VEL_Z = 0, LGX_R_ANG_VEL_XY, LGX_R_ORIENTATION, LGX_R_BASE_HEIGHT, LGX_R_TORQUES,
+  LGX_R_ENERGY, LGX_R_DOF_VEL, LGX_R_DOF_ACC, LGX_R_ACTION_RATE, LGX_R_COLLISION,
+  LGX_R_TERMINATION, LGX_R_DOF_POS_LIMITS, LGX_R_DOF_VEL_LIMITS, LGX_R_TORQUE_LIMITS,
+  LGX_R_TRACKING_LIN_VEL, LGX_R_TRACKING_ANG_VEL, LGX_R_FEET_AIR_TIME, LGX_R_STUMBLE,
+  LGX_R_STAND_STILL, LGX_R_FEET_CONTACT_FORCES, LGX_R_HIP_MOTION, LGX_R_COUNT
+};
+
+/* control paths: position drive (the reference step path, legged_robot.py:93-96) or
+ * the explicit-torque `_compute_torques` variants (legged_robot.py:370-392) */
+enum lgx_control { LGX_CTRL_POS_DRIVE = 0, LGX_CTRL_P = 1, LGX_CTRL_V = 2, LGX_CTRL_T = 3 };
+
+/* Per-env uniform draws: slot layout of one env's row (stride LGX_DRAW_NOISE + num_obs).
+ * In production the draws come from an in-kernel Philox4x32-10 stream keyed by
+ * (seed, env, step counter); for golden parity the caller injects them (lgx_set_draws). */
+#define LGX_DRAW_CMD 0          /* 3: periodic command resample (legged_robot.py:342,360-365) */
+#define LGX_DRAW_PUSH 3         /* 2: push velocity xy (legged_robot.py:440) */
+#define LGX_DRAW_RESET_DOF 5    /* 12: dof factor U[0.5,1.5] (legged_robot.py:407) */
+#define LGX_DRAW_RESET_XY 17    /* 2: origin offset U[-1,1] (legged_robot.py:425) */
+#define LGX_DRAW_RESET_VEL 19   /* 6: root vel U[-.5,.5] (legged_robot.py:430) */
+#define LGX_DRAW_RESET_CMD 25   /* 3: command resample on reset (legged_robot.py:173) */
+#define LGX_DRAW_CURRIC 28      /* 1: randint level on curriculum wrap (legged_robot.py:461) */
+#define LGX_DRAW_NOISE 32       /* num_obs: obs noise U[0,1) (legged_robot.py:231) */
+
+typedef struct lgx_model {
+  /* kinematic tree: 4 legs x 3 revolute joints; joint j = 3*leg + k, its parent is the
+   * base (k == 0) or dyn body 1 + 3*leg + k-1.  Joint frame = parent frame * (rot, pos);
+   * child body frame = joint frame * Rot(axis, q_j). */
+  float joint_rot[LGX_NUM_DOF][9];
+  float joint_pos[LGX_NUM_DOF][3];
+  float joint_axis[LGX_NUM_DOF][3];
+  float dof_lower[LGX_NUM_DOF];     /* hard limits (URDF); lower >= upper => unlimited */
+  float dof_upper[LGX_NUM_DOF];
+  float dof_vel_limit[LGX_NUM_DOF]; /* URDF velocity, PhysX maxJointVelocity */
+  float dof_effort[LGX_NUM_DOF];    /* URDF effort = drive force limit */
+  float kp[LGX_NUM_DOF];            /* drive stiffness (legged_robot.py:692-699) */
+  float kd[LGX_NUM_DOF];            /* drive damping */
+  /* dynamic bodies: nominal inertial data in body frame (inertia about COM: xx yy zz xy xz yz) */
+  float body_mass[LGX_NUM_DYN];
+  float body_com[LGX_NUM_DYN][3];
+  float body_inertia[LGX_NUM_DYN][6];
+  /* contact primitives: sphere (radius > 0) or corner (radius 0) in dyn-body frame */
+  int32_t num_points;
+  int32_t num_report_bodies;
+  float point_pos[LGX_MAX_POINTS][3];
+  float point_radius[LGX_MAX_POINTS];
+  int32_t point_dyn[LGX_MAX_POINTS];
+  int32_t point_report[LGX_MAX_POINTS];
+  /* lgx contact / limit model */
+  float contact_k, contact_c, friction_c, limit_k, limit_c;
+  float ground_friction;            /* terrain static_friction, combined by averaging */
+  float gravity[3];
+  float sim_dt;                     /* float32(sim.dt) */
+} lgx_model;
+
+typedef struct lgx_env_params {
+  int32_t num_envs;
+  int32_t num_obs;                  /* 48 or 48 + num_height_points */
+  int32_t decimation;
+  int32_t control_type;             /* enum lgx_control */
+  float action_scale, clip_actions, clip_obs;
+  float dt;                         /* decimation * sim_dt (legged_robot.py:770) */
+  float default_dof_pos[LGX_NUM_DOF];
+  float soft_lower[LGX_NUM_DOF], soft_upper[LGX_NUM_DOF];   /* legged_robot.py:306-309 */
+  float dof_vel_limits[LGX_NUM_DOF], torque_limits[LGX_NUM_DOF];
+  float p_gains[LGX_NUM_DOF], d_gains[LGX_NUM_DOF];
+  float soft_dof_vel_limit, soft_torque_limit;
+  float max_episode_length;         /* ceil(episode_length_s / dt) = 1001 (legged_robot.py:777) */
+  float max_episode_length_s;
+  int32_t resample_interval;        /* int(resampling_time / dt) = 500 (legged_robot.py:342) */
+  int32_t push_robots;
+  int32_t push_interval;            /* ceil(push_interval_s / dt) = 751 (legged_robot.py:779) */
+  float max_push_vel_xy;
+  int32_t heading_command;
+  float cmd_ranges[4][2];           /* lin_vel_x, lin_vel_y, ang_vel_yaw, heading */
+  float obs_scale_lin_vel, obs_scale_ang_vel, obs_scale_dof_pos, obs_scale_dof_vel, obs_scale_height;
+  int32_t add_noise;
+  float noise_scale_vec[LGX_MAX_OBS];   /* _get_noise_scale_vec (legged_robot.py:477-500) */
+  /* terrain */
+  int32_t terrain_kind;             /* 0 plane/none, 1 heightfield/trimesh (sampled heightfield) */
+  int32_t measure_heights;
+  int32_t num_height_points;
+  float height_points[LGX_MAX_HEIGHT_POINTS][2];  /* base-frame xy (legged_robot.py:802-816) */
+  float border_size, horizontal_scale, vertical_scale;
+  int32_t curriculum;               /* terrain curriculum (legged_robot.py:443-463) */
+  int32_t custom_origins;
+  int32_t max_terrain_level;        /* num_rows */
+  int32_t terrain_num_cols;
+  float terrain_env_length;
+  float base_init_state[13];
+  /* rewards, in reference evaluation order (alphabetical, non-zero scale, x dt) */
+  int32_t num_terms;
+  int32_t term_ids[LGX_MAX_TERMS];
+  float term_scales[LGX_MAX_TERMS];
+  int32_t termination_slot;         /* episode_sums row of "termination" or -1 */
+  float termination_scale;
+  int32_t only_positive_rewards;
+  float tracking_sigma, base_height_target, max_contact_force;
+  int32_t num_feet, feet_indices[4];
+  int32_t num_penalised, penalised_indices[16];
+  int32_t num_termination_bodies, termination_indices[8];
+  int32_t send_timeouts;
+  /* Go1 actuator-net history (go1.py:50-53,79-107); enabled if use_actuator_history */
+  int32_t use_actuator_history;
+  float act_pos_err_mean[LGX_NUM_DOF], act_pos_err_std[LGX_NUM_DOF];
+  float act_vel_mean[LGX_NUM_DOF], act_vel_std[LGX_NUM_DOF];
+  uint64_t seed;
+} lgx_env_params;
+
+typedef struct lgx_buffers {
+  float* root_states;        /* [N,13] */
+  float* dof_state;          /* [N,12,2] */
+  float* dof_targets;        /* [N,12] target_poses (legged_robot.py:94) */
+  float* torques;            /* [N,12] */
+  float* contact_forces;     /* [N,B,3] */
+  float* actions;            /* [N,12] clipped actions (input written by host, clipped in place) */
+  float* last_actions;       /* [N,12] */
+  float* last_dof_vel;       /* [N,12] */
+  float* last_root_vel;      /* [N,6] */
+  float* commands;           /* [N,4] */
+  float* base_lin_vel;       /* [N,3] */
+  float* base_ang_vel;       /* [N,3] */
+  float* projected_gravity;  /* [N,3] */
+  float* feet_air_time;      /* [N,4] */
+  float* obs;                /* [N,num_obs] */
+  float* rew;                /* [N] */
+  uint8_t* reset;            /* [N] bool */
+  uint8_t* time_out;         /* [N] bool */
+  int64_t* episode_length;   /* [N] */
+  float* episode_sums;       /* [T,N]  T = num_terms (+1 if termination) */
+  float* measured_heights;   /* [N,P] */
+  float* env_origins;        /* [N,3] */
+  int64_t* terrain_levels;   /* [N] */
+  int64_t* terrain_types;    /* [N] */
+  float* terrain_origins;    /* [rows, cols, 3] */
+  const int16_t* height_samples; /* [hf_rows, hf_cols] */
+  int32_t hf_rows, hf_cols;
+  float* body_mass_scale;    /* [N,13] per-env mass / nominal mass (domain randomisation) */
+  float* friction;           /* [N] per-env shape friction */
+  float* act_hist;           /* [N,12,2,5] actuator-net history (pos_err, vel) oldest..newest */
+  float* model_ins;          /* [decimation,N,120] actuator-net inputs per substep */
+  const float* act_net_w;    /* packed transposed actuator-MLP weights (lgx_actuator_mlp) or NULL */
+  const float* act_net_scale;/* [3] output scale (vel_std per leg joint) */
+  float* act_dvel;           /* [decimation,N,12] actuator-net outputs (dVel, go1.py:100-105) */
+  float* extras;             /* [T + 2]: episode means per term, terrain_level, reset count */
+  uint8_t* extras_time_outs; /* [N] time_outs as last published (stale semantics) */
+  float* scratch;            /* [lgx_scratch_floats(N)] reduction partials */
+} lgx_buffers;
+
+typedef struct lgx_sim lgx_sim;
+
+const char* lgx_last_error(void);
+int lgx_version(void);
+
+/* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers): lets bindings verify layout */
+void lgx_struct_sizes(int64_t out[3]);
+
+/* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
+int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
+
+/* Replaces gym.create_sim + create_actor loop + prepare_sim + acquire_*_tensor
+ * (legged_robot.py:233-249,645-740; base_task.py:85; legged_robot.py:507-524). */
+int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const lgx_buffers* bufs,
+                   int device, lgx_sim** out);
+int lgx_sim_destroy(lgx_sim* sim);
+
+/* Full env step: clip actions, `decimation` x (targets -> physics substep), then the fused
+ * post-physics step.  Replaces LeggedRobot.step (legged_robot.py:79-107) including
+ * set_dof_position_target_tensor / simulate / refresh_* and post_physics_step.
+ * `common_step_counter` is the host counter value AFTER this step's increment. */
+int lgx_step(lgx_sim* sim, int64_t common_step_counter, void* stream);
+
+/* Physics only: `n` substeps with the currently bound dof_targets (gym.simulate x n). */
+int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
+
+/* post_physics_step only (legged_robot.py:109-141) on the current state buffers. */
+int lgx_post_physics(lgx_sim* sim, int64_t common_step_counter, void* stream);
+
+/* reset_idx for the listed envs (legged_robot.py:150-193): dof/root reset, commands,
+ * buffers, episode extras.  env_ids: device int32[n]. */
+int lgx_reset_idx(lgx_sim* sim, const int32_t* env_ids, int32_t n, int64_t common_step_counter,
+                  int32_t init_done, void* stream);
+
+/* Draw injection for parity tests: device float[N, LGX_DRAW_NOISE + num_obs] or NULL to
+ * return to the in-kernel Philox stream. */
+int lgx_set_draws(lgx_sim* sim, const float* draws);
+
+/* Go1 actuator MLP (UniNet, go1.py:22-35,100-105): rows of 30 inputs -> 3 outputs,
+ * 30-128-128-128-3 tanh MLP on f32 MFMA.  w: packed [W0t b0 W1t b1 W2t b2 W3t b3] with
+ * W_lt = transposed torch Linear weight ([in x out]).  out = net(in) * out_scale[col]
+ * (dVel *= vel_std). */
+int lgx_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
+                     void* stream);
+
+/* ANYmal SEA LSTM (anymal.py:62-78): 2-layer LSTM(2->8), Linear(8->1), in/out scale;
+ * x [M,2], h/c [2,M,8] updated in place, tau [M].  w: packed torch layout. */
+int lgx_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m, const float* w,
+                      void* stream);
+
+/* Fused MLP forward (ActorCritic, rsl_rl; legged_robot_config.py:216-220): y = MLP(x) on
+ * f32 MFMA, hidden activation ELU (act=1) or tanh (act=2), last layer linear.
+ * dims[0..nl] layer widths (<= 512); weights[l]: transposed [in x out] row-major,
+ * biases[l]: [out].  `dims`, `weights`, `biases` are HOST arrays of device pointers. */
+int lgx_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
+                    const float* const* weights, const float* const* biases, int32_t act, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LGX_H */

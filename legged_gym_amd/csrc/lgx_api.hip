@@ -1,0 +1,204 @@
+// C-ABI implementation (include/lgx.h): validation, device-resident model/params, launch
+// sequencing.  No host synchronisation in any step-path call; errors are reported through
+// return codes + a thread-local message, never by exceptions across the ABI.
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+#include <string>
+
+#include "lgx_internal.h"
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char* msg) {
+  g_err = msg;
+  return code;
+}
+static int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  char buf[256];
+  snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+  g_err = buf;
+  return LGX_EHIP;
+}
+static int launch_check(int rc, const char* what) {
+  if (rc == 0) return 0;
+  if (rc == -1) return fail(LGX_EINVAL, what);
+  return hip_check(hipGetLastError(), what);
+}
+
+struct lgx_sim {
+  int device;
+  lgx_env_params params;  // host copy
+  lgx_buffers bufs;
+  lgx_dev_model* d_model;
+  lgx_env_params* d_params;
+  const float* draws;
+  int32_t n_term_rows;
+};
+
+extern "C" {
+
+const char* lgx_last_error(void) { return g_err.c_str(); }
+int lgx_version(void) { return 1; }
+
+void lgx_struct_sizes(int64_t out[3]) {
+  out[0] = (int64_t)sizeof(lgx_model);
+  out[1] = (int64_t)sizeof(lgx_env_params);
+  out[2] = (int64_t)sizeof(lgx_buffers);
+}
+
+int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms) {
+  (void)num_terms;
+  int64_t blocks = (num_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
+  return blocks * LGX_PARTIAL_STRIDE + 64;
+}
+
+int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const lgx_buffers* bufs, int device,
+                   lgx_sim** out) {
+  if (!model || !params || !bufs || !out) return fail(LGX_EINVAL, "lgx_sim_create: null argument");
+  if (params->num_envs <= 0) return fail(LGX_EINVAL, "lgx_sim_create: num_envs must be > 0");
+  if (params->num_obs <= 0 || params->num_obs > LGX_MAX_OBS) return fail(LGX_EINVAL, "lgx_sim_create: bad num_obs");
+  if (params->measure_heights && (params->num_height_points <= 0 || params->num_height_points > LGX_MAX_HEIGHT_POINTS ||
+                                  48 + params->num_height_points != params->num_obs))
+    return fail(LGX_EINVAL, "lgx_sim_create: num_obs must be 48 + num_height_points when measuring heights");
+  if (!params->measure_heights && params->num_obs != 48)
+    return fail(LGX_EINVAL, "lgx_sim_create: num_obs must be 48 without height measurements");
+  if (params->num_terms < 0 || params->num_terms + 1 > LGX_MAX_TERMS) return fail(LGX_EINVAL, "lgx_sim_create: too many reward terms");
+  if (params->decimation <= 0) return fail(LGX_EINVAL, "lgx_sim_create: decimation must be > 0");
+  if (params->resample_interval <= 0) return fail(LGX_EINVAL, "lgx_sim_create: resample_interval must be > 0");
+  if (params->push_robots && params->push_interval <= 0) return fail(LGX_EINVAL, "lgx_sim_create: push_interval must be > 0");
+  if (model->num_points < 0 || model->num_points > LGX_MAX_POINTS) return fail(LGX_EINVAL, "lgx_sim_create: bad num_points");
+  if (params->terrain_kind != 0 && (!bufs->height_samples || bufs->hf_rows < 2 || bufs->hf_cols < 2))
+    return fail(LGX_EINVAL, "lgx_sim_create: terrain requires height_samples");
+  const void* required[] = {bufs->root_states, bufs->dof_state, bufs->dof_targets, bufs->torques, bufs->contact_forces,
+                            bufs->actions, bufs->last_actions, bufs->last_dof_vel, bufs->last_root_vel, bufs->commands,
+                            bufs->base_lin_vel, bufs->base_ang_vel, bufs->projected_gravity, bufs->feet_air_time,
+                            bufs->obs, bufs->rew, bufs->reset, bufs->time_out, bufs->episode_length,
+                            bufs->episode_sums, bufs->env_origins, bufs->body_mass_scale, bufs->extras,
+                            bufs->extras_time_outs, bufs->scratch};
+  for (const void* p : required)
+    if (!p) return fail(LGX_EINVAL, "lgx_sim_create: a required buffer is null");
+  if (params->measure_heights && !bufs->measured_heights) return fail(LGX_EINVAL, "lgx_sim_create: measured_heights is null");
+  if (params->use_actuator_history && (!bufs->act_hist || !bufs->model_ins))
+    return fail(LGX_EINVAL, "lgx_sim_create: actuator history buffers are null");
+  if (params->curriculum && (!bufs->terrain_levels || !bufs->terrain_types || !bufs->terrain_origins))
+    return fail(LGX_EINVAL, "lgx_sim_create: curriculum buffers are null");
+
+  // per-lane contact candidate tables: leg points to their leg's lane, base points round-robin
+  lgx_dev_model dm;
+  memset(&dm, 0, sizeof dm);
+  dm.m = *model;
+  int rr = 0;
+  for (int i = 0; i < model->num_points; ++i) {
+    int d = model->point_dyn[i];
+    int rep = model->point_report[i];
+    if (d < 0 || d >= LGX_NUM_DYN) return fail(LGX_EINVAL, "lgx_sim_create: bad point_dyn");
+    int lane;
+    if (d == 0) {
+      if (rep != 0) return fail(LGX_EINVAL, "lgx_sim_create: base points must report on body 0");
+      lane = rr++ & 3;
+    } else {
+      lane = (d - 1) / 3;
+      if (rep < 1 + 4 * lane || rep > 4 + 4 * lane) return fail(LGX_EINVAL, "lgx_sim_create: leg point reports on a foreign body");
+    }
+    if (dm.lane_npts[lane] >= LGX_MAX_LANE_PTS) return fail(LGX_EINVAL, "lgx_sim_create: too many contact points per leg");
+    dm.lane_pts[lane][dm.lane_npts[lane]++] = i;
+  }
+  for (int l = 0; l < 4; ++l) dm.max_lane_npts = dm.lane_npts[l] > dm.max_lane_npts ? dm.lane_npts[l] : dm.max_lane_npts;
+
+  int rc = hip_check(hipSetDevice(device), "hipSetDevice");
+  if (rc) return rc;
+  lgx_sim* s = new (std::nothrow) lgx_sim();
+  if (!s) return fail(LGX_ENOMEM, "lgx_sim_create: out of host memory");
+  s->device = device;
+  s->params = *params;
+  s->bufs = *bufs;
+  s->draws = nullptr;
+  s->n_term_rows = params->num_terms + (params->termination_slot >= 0 ? 1 : 0);
+  if ((rc = hip_check(hipMalloc(&s->d_model, sizeof(lgx_dev_model)), "hipMalloc(model)"))) { delete s; return rc; }
+  if ((rc = hip_check(hipMalloc(&s->d_params, sizeof(lgx_env_params)), "hipMalloc(params)"))) {
+    (void)hipFree(s->d_model); delete s; return rc;
+  }
+  rc = hip_check(hipMemcpy(s->d_model, &dm, sizeof dm, hipMemcpyHostToDevice), "hipMemcpy(model)");
+  if (!rc) rc = hip_check(hipMemcpy(s->d_params, params, sizeof *params, hipMemcpyHostToDevice), "hipMemcpy(params)");
+  if (rc) { (void)hipFree(s->d_model); (void)hipFree(s->d_params); delete s; return rc; }
+  *out = s;
+  return 0;
+}
+
+int lgx_sim_destroy(lgx_sim* s) {
+  if (!s) return 0;
+  (void)hipFree(s->d_model);
+  (void)hipFree(s->d_params);
+  delete s;
+  return 0;
+}
+
+int lgx_set_draws(lgx_sim* s, const float* draws) {
+  if (!s) return fail(LGX_EINVAL, "lgx_set_draws: null sim");
+  s->draws = draws;
+  return 0;
+}
+
+int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
+  if (!s || n < 0) return fail(LGX_EINVAL, "lgx_simulate: bad arguments");
+  if (n == 0) return 0;
+  return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, n, 0, (hipStream_t)stream),
+                      "lgx_simulate: physics launch");
+}
+
+int lgx_post_physics(lgx_sim* s, int64_t step, void* stream) {
+  if (!s) return fail(LGX_EINVAL, "lgx_post_physics: null sim");
+  return launch_check(lgx_launch_post_physics(s->d_params, s->bufs, s->params.num_envs, s->params.num_obs, s->n_term_rows,
+                                              s->params.measure_heights, step, s->draws, (hipStream_t)stream),
+                      "lgx_post_physics: launch");
+}
+
+int lgx_step(lgx_sim* s, int64_t step, void* stream) {
+  if (!s) return fail(LGX_EINVAL, "lgx_step: null sim");
+  hipStream_t st = (hipStream_t)stream;
+  const lgx_env_params& p = s->params;
+  int rc = launch_check(lgx_launch_clip_actions(s->bufs.actions, (int64_t)p.num_envs * 12, p.clip_actions, st),
+                        "lgx_step: clip launch");
+  if (rc) return rc;
+  rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, st),
+                    "lgx_step: physics launch");
+  if (rc) return rc;
+  if (p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel) {
+    // UniNet on every (substep, env, leg) row of this step's model_ins; result = dVel
+    rc = launch_check(lgx_launch_actuator_mlp(s->bufs.model_ins, s->bufs.act_dvel, (int64_t)p.decimation * p.num_envs * 4,
+                                              s->bufs.act_net_w, s->bufs.act_net_scale, st),
+                      "lgx_step: actuator mlp launch");
+    if (rc) return rc;
+  }
+  return lgx_post_physics(s, step, stream);
+}
+
+int lgx_reset_idx(lgx_sim* s, const int32_t* env_ids, int32_t n, int64_t step, int32_t init_done, void* stream) {
+  if (!s || n < 0 || (n > 0 && !env_ids)) return fail(LGX_EINVAL, "lgx_reset_idx: bad arguments");
+  if (n > s->params.num_envs) return fail(LGX_EINVAL, "lgx_reset_idx: more ids than envs");
+  return launch_check(lgx_launch_reset_idx(s->d_params, s->bufs, s->params.num_envs, s->n_term_rows, env_ids, n, step,
+                                           init_done, s->draws, (hipStream_t)stream),
+                      "lgx_reset_idx: launch");
+}
+
+int lgx_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale, void* stream) {
+  if (!in || !out || !w || rows < 0) return fail(LGX_EINVAL, "lgx_actuator_mlp: bad arguments");
+  return launch_check(lgx_launch_actuator_mlp(in, out, rows, w, out_scale, (hipStream_t)stream), "lgx_actuator_mlp: launch");
+}
+
+int lgx_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m, const float* w, void* stream) {
+  if (!x || !h || !c || !tau || !w || m < 0) return fail(LGX_EINVAL, "lgx_actuator_lstm: bad arguments");
+  return launch_check(lgx_launch_actuator_lstm(x, h, c, tau, m, w, (hipStream_t)stream), "lgx_actuator_lstm: launch");
+}
+
+int lgx_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims, const float* const* weights,
+                    const float* const* biases, int32_t act, void* stream) {
+  if (!x || !y || !dims || !weights || !biases || rows < 0) return fail(LGX_EINVAL, "lgx_mlp_forward: bad arguments");
+  return launch_check(lgx_launch_mlp_forward(x, y, rows, nl, dims, weights, biases, act, (hipStream_t)stream),
+                      "lgx_mlp_forward: launch (widths must be 1..512, layers 1..6)");
+}
+
+}  // extern "C"

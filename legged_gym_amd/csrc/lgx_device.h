@@ -1,0 +1,111 @@
+// Device helpers shared by the lgx HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/lgx.h"
+
+#define LGX_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- Philox4x32-10 uniforms
+// Same stream as the oracle's lgxo_uniform: counter (env, slot/4, step, tag), key = seed.
+LGX_DEV float lgx_uniform(uint64_t seed, int32_t env, int32_t slot, int64_t step, uint32_t tag) {
+  uint32_t c0 = (uint32_t)env, c1 = (uint32_t)(slot >> 2), c2 = (uint32_t)step;
+  uint32_t c3 = tag ^ ((uint32_t)((uint64_t)step >> 32) << 8);
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  uint32_t sel = (slot & 3) == 0 ? c0 : (slot & 3) == 1 ? c1 : (slot & 3) == 2 ? c2 : c3;
+  return (float)(sel >> 8) * (1.0f / 16777216.0f);
+}
+
+// ---------------------------------------------------------------- small vector math
+struct f3 { float x, y, z; };
+LGX_DEV f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+LGX_DEV f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+LGX_DEV f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+LGX_DEV f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+LGX_DEV float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+LGX_DEV f3 cross(f3 a, f3 b) { return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+
+struct m33 { float a[9]; };
+LGX_DEV f3 mul(const m33& R, f3 v) {
+  return f3{R.a[0] * v.x + R.a[1] * v.y + R.a[2] * v.z, R.a[3] * v.x + R.a[4] * v.y + R.a[5] * v.z,
+            R.a[6] * v.x + R.a[7] * v.y + R.a[8] * v.z};
+}
+LGX_DEV m33 mul(const m33& A, const m33& B) {
+  m33 C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) C.a[3 * i + j] = A.a[3 * i] * B.a[j] + A.a[3 * i + 1] * B.a[3 + j] + A.a[3 * i + 2] * B.a[6 + j];
+  return C;
+}
+LGX_DEV m33 quat_to_mat(float x, float y, float z, float w) {
+  m33 R;
+  R.a[0] = 1 - 2 * (y * y + z * z); R.a[1] = 2 * (x * y - z * w);     R.a[2] = 2 * (x * z + y * w);
+  R.a[3] = 2 * (x * y + z * w);     R.a[4] = 1 - 2 * (x * x + z * z); R.a[5] = 2 * (y * z - x * w);
+  R.a[6] = 2 * (x * z - y * w);     R.a[7] = 2 * (y * z + x * w);     R.a[8] = 1 - 2 * (x * x + y * y);
+  return R;
+}
+LGX_DEV m33 axis_angle(f3 a, float th) {
+  float s, c;
+  sincosf(th, &s, &c);
+  float t = 1 - c;
+  m33 R;
+  R.a[0] = t * a.x * a.x + c;       R.a[1] = t * a.x * a.y - s * a.z; R.a[2] = t * a.x * a.z + s * a.y;
+  R.a[3] = t * a.x * a.y + s * a.z; R.a[4] = t * a.y * a.y + c;       R.a[5] = t * a.y * a.z - s * a.x;
+  R.a[6] = t * a.x * a.z - s * a.y; R.a[7] = t * a.y * a.z + s * a.x; R.a[8] = t * a.z * a.z + c;
+  return R;
+}
+
+// isaacgym.torch_utils semantics, xyzw
+LGX_DEV f3 quat_rotate_inverse(float qx, float qy, float qz, float qw, f3 v) {
+  f3 q = mk3(qx, qy, qz);
+  float a = 2.0f * qw * qw - 1.0f;
+  f3 c = cross(q, v);
+  float d = dot(q, v);
+  return f3{v.x * a - c.x * qw * 2.0f + q.x * d * 2.0f, v.y * a - c.y * qw * 2.0f + q.y * d * 2.0f,
+            v.z * a - c.z * qw * 2.0f + q.z * d * 2.0f};
+}
+LGX_DEV f3 quat_apply(float qx, float qy, float qz, float qw, f3 v) {
+  f3 q = mk3(qx, qy, qz);
+  f3 t = 2.0f * cross(q, v);
+  f3 u = cross(q, t);
+  return f3{v.x + qw * t.x + u.x, v.y + qw * t.y + u.y, v.z + qw * t.z + u.z};
+}
+
+LGX_DEV float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+
+// quad (4-lane) all-reduce: lanes 4e..4e+3 own one env
+LGX_DEV float quad_sum(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  return v;
+}
+
+// triangulated heightfield (diagonal (i,j)-(i+1,j+1), isaacgym terrain_utils trimesh)
+LGX_DEV float ground_height(const lgx_env_params* __restrict__ P, const int16_t* __restrict__ H, int rows, int cols,
+                            float x, float y, f3* n) {
+  if (P->terrain_kind == 0 || H == nullptr) { *n = mk3(0.f, 0.f, 1.f); return 0.0f; }
+  float hs = P->horizontal_scale, vs = P->vertical_scale;
+  float u = (x + P->border_size) / hs, v = (y + P->border_size) / hs;
+  int i = (int)floorf(u), j = (int)floorf(v);
+  i = min(max(i, 0), rows - 2);
+  j = min(max(j, 0), cols - 2);
+  float fu = clampf(u - (float)i, 0.f, 1.f), fv = clampf(v - (float)j, 0.f, 1.f);
+  float h00 = H[i * cols + j] * vs, h10 = H[(i + 1) * cols + j] * vs;
+  float h01 = H[i * cols + j + 1] * vs, h11 = H[(i + 1) * cols + j + 1] * vs;
+  float gx, gy, h;
+  if (fu >= fv) { gx = (h10 - h00) / hs; gy = (h11 - h10) / hs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
+  else          { gx = (h11 - h01) / hs; gy = (h01 - h00) / hs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
+  float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
+  *n = mk3(-gx * inv, -gy * inv, inv);
+  return h;
+}

@@ -1,0 +1,416 @@
+// lgx post-physics kernel: the fused LeggedRobot.post_physics_step (legged_robot.py:109-141)
+// — base-frame transforms, command resampling / heading, height scan, pushes, termination,
+// the reward terms in reference order, reset_idx, observations + noise + clip, last_* copies —
+// with no host synchronisation (the reference's reset_buf.nonzero() and per-term launches
+// are replaced by per-env predication and a deterministic two-stage reduction for extras).
+//
+// Block = 256 threads owns 64 envs.  Phases:
+//   A  (all 256 lanes) height scan: (env, point) pairs, coalesced int16 gathers
+//   B  (lanes 0..63)   one env per lane: scalar logic, rewards, reset
+//   C  (all 256 lanes) observation rows: (env, obs index) pairs, coalesced stores
+// Extras (episode means over reset envs) are reduced per block in LDS, then by a one-block
+// finalize kernel in fixed order (bitwise reproducible).
+#include "lgx_device.h"
+#include "lgx_internal.h"
+
+#define ENV_THREADS 256
+
+namespace {
+
+struct Draws {
+  const lgx_env_params* P;
+  const float* inj;  // injected [N, stride] or null
+  int32_t stride;
+  LGX_DEV float operator()(int e, int slot, int64_t step, uint32_t tag) const {
+    return inj ? inj[(int64_t)e * stride + slot] : lgx_uniform(P->seed, e, slot, step, tag);
+  }
+};
+
+LGX_DEV float wrap_to_pi(float a) {  // utils/math.py:45-48 (torch remainder semantics)
+  const float tp = (float)(2.0 * 3.14159265358979323846);
+  float r = fmodf(a, tp);
+  if (r != 0.0f && r < 0.0f) r += tp;
+  if (r > (float)3.14159265358979323846) r -= tp;
+  return r;
+}
+
+LGX_DEV void resample_cmd(const lgx_env_params* __restrict__ P, const Draws& D, int e, int slot, int64_t step,
+                          uint32_t tag, float* c) {  // legged_robot.py:354-368
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    float lo = P->cmd_ranges[k][0], hi = P->cmd_ranges[k][1];
+    c[k] = (hi - lo) * D(e, slot + k, step, tag) + lo;
+  }
+  int k3 = P->heading_command ? 3 : 2;
+  float lo = P->cmd_ranges[k3][0], hi = P->cmd_ranges[k3][1];
+  float v = (hi - lo) * D(e, slot + 2, step, tag) + lo;
+  if (k3 == 3) c[3] = v; else c[2] = v;
+  float keep = sqrtf(c[0] * c[0] + c[1] * c[1]) > 0.2f ? 1.0f : 0.0f;
+  c[0] *= keep; c[1] *= keep;
+}
+
+LGX_DEV float norm3p(const float* f) { return sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]); }
+
+struct EnvView {
+  f3 blv, bav, pg;
+  float cmd[4];
+  const float* ds;   // dof_state row (pre-reset)
+  const float* tq;
+  const float* cf;
+  const float* act;
+  const float* la;
+  const float* ldv;
+  float* fat;
+  float rootz;
+  const float* mh;
+  bool reset, time_out;
+};
+
+LGX_DEV float reward_term(const lgx_env_params* __restrict__ P, const EnvView& v, int id) {  // :857-966
+  float s = 0.f;
+  switch (id) {
+    case LGX_R_LIN_VEL_Z: return v.blv.z * v.blv.z;
+    case LGX_R_ANG_VEL_XY: return v.bav.x * v.bav.x + v.bav.y * v.bav.y;
+    case LGX_R_ORIENTATION: return v.pg.x * v.pg.x + v.pg.y * v.pg.y;
+    case LGX_R_BASE_HEIGHT: {
+      float acc;
+      if (P->measure_heights) {
+        acc = 0.f;
+        for (int i = 0; i < P->num_height_points; ++i) acc += v.rootz - v.mh[i];
+        acc /= (float)P->num_height_points;
+      } else acc = v.rootz;
+      float d = acc - P->base_height_target;
+      return d * d;
+    }
+    case LGX_R_TORQUES: for (int j = 0; j < 12; ++j) s += v.tq[j] * v.tq[j]; return s;
+    case LGX_R_ENERGY: for (int j = 0; j < 12; ++j) { float x = v.tq[j] * v.ds[2 * j + 1]; s += x * x; } return s;
+    case LGX_R_DOF_VEL: for (int j = 0; j < 12; ++j) s += v.ds[2 * j + 1] * v.ds[2 * j + 1]; return s;
+    case LGX_R_DOF_ACC:
+      for (int j = 0; j < 12; ++j) { float x = (v.ldv[j] - v.ds[2 * j + 1]) / P->dt; s += x * x; }
+      return s;
+    case LGX_R_ACTION_RATE: for (int j = 0; j < 12; ++j) { float x = v.la[j] - v.act[j]; s += x * x; } return s;
+    case LGX_R_COLLISION:
+      for (int i = 0; i < P->num_penalised; ++i) s += norm3p(v.cf + 3 * P->penalised_indices[i]) > 0.1f ? 1.f : 0.f;
+      return s;
+    case LGX_R_TERMINATION: return (v.reset && !v.time_out) ? 1.f : 0.f;
+    case LGX_R_DOF_POS_LIMITS:
+      for (int j = 0; j < 12; ++j) {
+        float lo = v.ds[2 * j] - P->soft_lower[j], hi = v.ds[2 * j] - P->soft_upper[j];
+        s += -(lo < 0.f ? lo : 0.f) + (hi > 0.f ? hi : 0.f);
+      }
+      return s;
+    case LGX_R_DOF_VEL_LIMITS:
+      for (int j = 0; j < 12; ++j)
+        s += clampf(fabsf(v.ds[2 * j + 1]) - P->dof_vel_limits[j] * P->soft_dof_vel_limit, 0.f, 1.f);
+      return s;
+    case LGX_R_TORQUE_LIMITS:
+      for (int j = 0; j < 12; ++j) s += fmaxf(fabsf(v.tq[j]) - P->torque_limits[j] * P->soft_torque_limit, 0.f);
+      return s;
+    case LGX_R_TRACKING_LIN_VEL: {
+      float ex = v.cmd[0] - v.blv.x, ey = v.cmd[1] - v.blv.y;
+      return expf(-(ex * ex + ey * ey) / P->tracking_sigma);
+    }
+    case LGX_R_TRACKING_ANG_VEL: { float ez = v.cmd[2] - v.bav.z; return expf(-(ez * ez) / P->tracking_sigma); }
+    case LGX_R_FEET_AIR_TIME: {  // mutates feet_air_time (:941-949)
+      for (int f = 0; f < P->num_feet; ++f) {
+        bool contact = v.cf[3 * P->feet_indices[f] + 2] > 1.0f;
+        float first = (v.fat[f] > 0.f && contact) ? 1.f : 0.f;
+        v.fat[f] += P->dt;
+        s += (v.fat[f] - 0.5f) * first;
+      }
+      s *= (sqrtf(v.cmd[0] * v.cmd[0] + v.cmd[1] * v.cmd[1]) > 0.1f) ? 1.f : 0.f;
+      for (int f = 0; f < P->num_feet; ++f)
+        if (v.cf[3 * P->feet_indices[f] + 2] > 1.0f) v.fat[f] = 0.f;
+      return s;
+    }
+    case LGX_R_STUMBLE:
+      for (int f = 0; f < P->num_feet; ++f) {
+        const float* F = v.cf + 3 * P->feet_indices[f];
+        if (sqrtf(F[0] * F[0] + F[1] * F[1]) > 5.f * fabsf(F[2])) return 1.f;
+      }
+      return 0.f;
+    case LGX_R_STAND_STILL:
+      for (int j = 0; j < 12; ++j) s += fabsf(v.ds[2 * j] - P->default_dof_pos[j]);
+      return s * ((sqrtf(v.cmd[0] * v.cmd[0] + v.cmd[1] * v.cmd[1]) < 0.1f) ? 1.f : 0.f);
+    case LGX_R_FEET_CONTACT_FORCES:
+      for (int f = 0; f < P->num_feet; ++f) s += fmaxf(norm3p(v.cf + 3 * P->feet_indices[f]) - P->max_contact_force, 0.f);
+      return s;
+    case LGX_R_HIP_MOTION:
+      for (int j = 0; j < 12; j += 3) s += fabsf(v.ds[2 * j] - P->default_dof_pos[j]);
+      return s;
+  }
+  return 0.f;
+}
+
+// reset one env (legged_robot.py:150-180, per env); cmd is the env's command row in registers
+LGX_DEV void reset_env(const lgx_env_params* __restrict__ P, const lgx_buffers& B, const Draws& D, int e,
+                       int64_t step, uint32_t tag, bool init_done, float* cmd) {
+  float* org = B.env_origins + (int64_t)e * 3;
+  float* rs = B.root_states + (int64_t)e * 13;
+  if (P->curriculum && init_done) {  // _update_terrain_curriculum :443-463
+    float dx = rs[0] - org[0], dy = rs[1] - org[1];
+    float dist = sqrtf(dx * dx + dy * dy);
+    bool up = dist > P->terrain_env_length / 2.0f;
+    bool down = (dist < sqrtf(cmd[0] * cmd[0] + cmd[1] * cmd[1]) * P->max_episode_length_s * 0.5f) && !up;
+    int64_t lvl = B.terrain_levels[e] + (up ? 1 : 0) - (down ? 1 : 0);
+    if (lvl >= P->max_terrain_level) {
+      int64_t r = (int64_t)(D(e, LGX_DRAW_CURRIC, step, tag) * (float)P->max_terrain_level);
+      lvl = r >= P->max_terrain_level ? P->max_terrain_level - 1 : r;
+    } else if (lvl < 0) lvl = 0;
+    B.terrain_levels[e] = lvl;
+    const float* to = B.terrain_origins + (lvl * P->terrain_num_cols + B.terrain_types[e]) * 3;
+    org[0] = to[0]; org[1] = to[1]; org[2] = to[2];
+  }
+  float* ds = B.dof_state + (int64_t)e * 24;
+  for (int j = 0; j < 12; ++j) {
+    ds[2 * j] = P->default_dof_pos[j] * ((1.5f - 0.5f) * D(e, LGX_DRAW_RESET_DOF + j, step, tag) + 0.5f);
+    ds[2 * j + 1] = 0.f;
+  }
+  for (int i = 0; i < 13; ++i) rs[i] = P->base_init_state[i];
+  for (int i = 0; i < 3; ++i) rs[i] += org[i];
+  if (P->custom_origins)
+    for (int i = 0; i < 2; ++i) rs[i] += (1.0f - -1.0f) * D(e, LGX_DRAW_RESET_XY + i, step, tag) + -1.0f;
+  for (int i = 0; i < 6; ++i) rs[7 + i] = (0.5f - -0.5f) * D(e, LGX_DRAW_RESET_VEL + i, step, tag) + -0.5f;
+  resample_cmd(P, D, e, LGX_DRAW_RESET_CMD, step, tag, cmd);
+  for (int j = 0; j < 12; ++j) { B.last_actions[(int64_t)e * 12 + j] = 0.f; B.last_dof_vel[(int64_t)e * 12 + j] = 0.f; }
+  for (int f = 0; f < 4; ++f) B.feet_air_time[(int64_t)e * 4 + f] = 0.f;
+  B.episode_length[e] = 0;
+  B.reset[e] = 1;
+}
+
+// per-block deterministic partial sums of the episode sums of reset envs (+ reset count)
+LGX_DEV void block_partials(float (*lds)[LGX_PARTIAL_STRIDE], int nrows, float* partial_out) {
+  __syncthreads();
+  int t = threadIdx.x;
+  if (t < nrows + 1) {
+    float s = 0.f;
+    for (int i = 0; i < LGX_ENV_BLOCK; ++i) s += lds[i][t];
+    partial_out[t] = s;
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(ENV_THREADS)
+lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int64_t step, const float* draws) {
+  const int N = P->num_envs;
+  const int nobs = P->num_obs;
+  const int e0 = blockIdx.x * LGX_ENV_BLOCK;
+  const int tid = threadIdx.x;
+  const Draws D{P, draws, LGX_DRAW_NOISE + nobs};
+  const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
+  __shared__ float part[LGX_ENV_BLOCK][LGX_PARTIAL_STRIDE];
+
+  // ---- phase A: height scan (legged_robot.py:818-854), pre-reset base pose
+  if (P->measure_heights) {
+    const int np = P->num_height_points;
+    const int total = LGX_ENV_BLOCK * np;
+    for (int idx = tid; idx < total; idx += ENV_THREADS) {
+      int le = idx / np, i = idx - le * np;
+      int e = e0 + le;
+      if (e >= N) break;
+      float* mh = B.measured_heights + (int64_t)e * np + i;
+      if (P->terrain_kind == 0) { *mh = 0.f; continue; }
+      const float* rs = B.root_states + (int64_t)e * 13;
+      float z = rs[5], w = rs[6];
+      float nrm = fmaxf(sqrtf(z * z + w * w), 1e-9f);
+      f3 o = quat_apply(0.f, 0.f, z / nrm, w / nrm, mk3(P->height_points[i][0], P->height_points[i][1], 0.f));
+      float x = o.x + rs[0] + P->border_size, y = o.y + rs[1] + P->border_size;
+      int64_t px = (int64_t)(x / P->horizontal_scale), py = (int64_t)(y / P->horizontal_scale);
+      px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
+      py = py < 0 ? 0 : (py > B.hf_cols - 2 ? B.hf_cols - 2 : py);
+      const int16_t* H = B.height_samples;
+      int h1 = H[px * B.hf_cols + py], h2 = H[(px + 1) * B.hf_cols + py], h3 = H[px * B.hf_cols + py + 1];
+      *mh = (float)min(min(h1, h2), h3) * P->vertical_scale;
+    }
+    __syncthreads();
+  }
+
+  // ---- phase B: one env per lane
+  if (tid < LGX_ENV_BLOCK) {
+    const int e = e0 + tid;
+    for (int t = 0; t < LGX_PARTIAL_STRIDE; ++t) part[tid][t] = 0.f;
+    if (e < N) {
+      int64_t ep = B.episode_length[e] + 1;  // :118
+      B.episode_length[e] = ep;
+      float* rs = B.root_states + (int64_t)e * 13;
+      const float qx = rs[3], qy = rs[4], qz = rs[5], qw = rs[6];
+      EnvView v;
+      v.blv = quat_rotate_inverse(qx, qy, qz, qw, mk3(rs[7], rs[8], rs[9]));     // :122-125
+      v.bav = quat_rotate_inverse(qx, qy, qz, qw, mk3(rs[10], rs[11], rs[12]));
+      v.pg = quat_rotate_inverse(qx, qy, qz, qw, mk3(0.f, 0.f, -1.f));
+      float* cmd_g = B.commands + (int64_t)e * 4;
+      for (int k = 0; k < 4; ++k) v.cmd[k] = cmd_g[k];
+      if (ep % P->resample_interval == 0) resample_cmd(P, D, e, LGX_DRAW_CMD, step, 0u, v.cmd);  // :342-343
+      if (P->heading_command) {  // :344-347
+        f3 f = quat_apply(qx, qy, qz, qw, mk3(1.f, 0.f, 0.f));
+        float heading = atan2f(f.y, f.x);
+        v.cmd[2] = clampf(0.5f * wrap_to_pi(v.cmd[3] - heading), -1.f, 1.f);
+      }
+      if (P->push_robots && step % P->push_interval == 0) {  // :351-352, 436-441
+        float mv = P->max_push_vel_xy;
+        rs[7] = (mv - -mv) * D(e, LGX_DRAW_PUSH, step, 0u) + -mv;
+        rs[8] = (mv - -mv) * D(e, LGX_DRAW_PUSH + 1, step, 0u) + -mv;
+      }
+      v.ds = B.dof_state + (int64_t)e * 24;
+      v.tq = B.torques + (int64_t)e * 12;
+      v.cf = B.contact_forces + (int64_t)e * LGX_MAX_BODIES * 3;
+      v.act = B.actions + (int64_t)e * 12;
+      v.la = B.last_actions + (int64_t)e * 12;
+      v.ldv = B.last_dof_vel + (int64_t)e * 12;
+      v.fat = B.feet_air_time + (int64_t)e * 4;
+      v.rootz = rs[2];
+      v.mh = B.measured_heights ? B.measured_heights + (int64_t)e * P->num_height_points : nullptr;
+      // check_termination :143-148
+      bool r = false;
+      for (int i = 0; i < P->num_termination_bodies; ++i) r |= norm3p(v.cf + 3 * P->termination_indices[i]) > 1.f;
+      v.time_out = (float)ep > P->max_episode_length;
+      v.reset = r || v.time_out;
+      // compute_reward :195-212
+      float rew = 0.f;
+      for (int t = 0; t < P->num_terms; ++t) {
+        float rr = reward_term(P, v, P->term_ids[t]) * P->term_scales[t];
+        rew += rr;
+        B.episode_sums[(int64_t)t * N + e] += rr;
+      }
+      if (P->only_positive_rewards) rew = fmaxf(rew, 0.f);
+      if (P->termination_slot >= 0) {
+        float rr = reward_term(P, v, LGX_R_TERMINATION) * P->termination_scale;
+        rew += rr;
+        B.episode_sums[(int64_t)P->termination_slot * N + e] += rr;
+      }
+      B.rew[e] = rew;
+      B.time_out[e] = v.time_out ? 1 : 0;
+      B.reset[e] = v.reset ? 1 : 0;
+      if (v.reset) {  // reset_idx :150-193
+        for (int t = 0; t < T; ++t) {
+          part[tid][t] = B.episode_sums[(int64_t)t * N + e];
+          B.episode_sums[(int64_t)t * N + e] = 0.f;
+        }
+        part[tid][T] = 1.f;
+        reset_env(P, B, D, e, step, 0u, true, v.cmd);
+      }
+      for (int k = 0; k < 4; ++k) cmd_g[k] = v.cmd[k];
+      float* o3 = B.base_lin_vel + (int64_t)e * 3;
+      o3[0] = v.blv.x; o3[1] = v.blv.y; o3[2] = v.blv.z;
+      o3 = B.base_ang_vel + (int64_t)e * 3;
+      o3[0] = v.bav.x; o3[1] = v.bav.y; o3[2] = v.bav.z;
+      o3 = B.projected_gravity + (int64_t)e * 3;
+      o3[0] = v.pg.x; o3[1] = v.pg.y; o3[2] = v.pg.z;
+    }
+  }
+  block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
+  __syncthreads();
+
+  // ---- phase C: observations (:214-231) + noise + clip (:103-104)
+  const int total = LGX_ENV_BLOCK * nobs;
+  for (int idx = tid; idx < total; idx += ENV_THREADS) {
+    int le = idx / nobs, i = idx - le * nobs;
+    int e = e0 + le;
+    if (e >= N) break;
+    float o;
+    if (i < 3) o = B.base_lin_vel[(int64_t)e * 3 + i] * P->obs_scale_lin_vel;
+    else if (i < 6) o = B.base_ang_vel[(int64_t)e * 3 + i - 3] * P->obs_scale_ang_vel;
+    else if (i < 9) o = B.projected_gravity[(int64_t)e * 3 + i - 6];
+    else if (i < 12) o = B.commands[(int64_t)e * 4 + i - 9] * (i < 11 ? P->obs_scale_lin_vel : P->obs_scale_ang_vel);
+    else if (i < 24) o = (B.dof_state[(int64_t)e * 24 + 2 * (i - 12)] - P->default_dof_pos[i - 12]) * P->obs_scale_dof_pos;
+    else if (i < 36) o = B.dof_state[(int64_t)e * 24 + 2 * (i - 24) + 1] * P->obs_scale_dof_vel;
+    else if (i < 48) o = B.actions[(int64_t)e * 12 + i - 36];
+    else o = clampf(B.root_states[(int64_t)e * 13 + 2] - 0.5f - B.measured_heights[(int64_t)e * P->num_height_points + i - 48],
+                    -1.f, 1.f) * P->obs_scale_height;
+    if (P->add_noise) o += (2.f * D(e, LGX_DRAW_NOISE + i, step, 0u) - 1.f) * P->noise_scale_vec[i];
+    B.obs[(int64_t)e * nobs + i] = clampf(o, -P->clip_obs, P->clip_obs);
+  }
+  // ---- last_* copies (:136-138), post-reset values
+  for (int idx = tid; idx < LGX_ENV_BLOCK * 12; idx += ENV_THREADS) {
+    int e = e0 + idx / 12, j = idx % 12;
+    if (e >= N) break;
+    B.last_actions[(int64_t)e * 12 + j] = B.actions[(int64_t)e * 12 + j];
+    B.last_dof_vel[(int64_t)e * 12 + j] = B.dof_state[(int64_t)e * 24 + 2 * j + 1];
+  }
+  if (tid < LGX_ENV_BLOCK && e0 + tid < N) {
+    int e = e0 + tid;
+    for (int i = 0; i < 6; ++i) B.last_root_vel[(int64_t)e * 6 + i] = B.root_states[(int64_t)e * 13 + 7 + i];
+  }
+}
+
+// reset_idx on an explicit env list (BaseTask.reset, base_task.py:111-115)
+__global__ void __launch_bounds__(LGX_ENV_BLOCK)
+lgx_reset_idx_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, const int32_t* ids, int32_t n, int64_t step,
+                     int32_t init_done, const float* draws) {
+  const int N = P->num_envs;
+  const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
+  const Draws D{P, draws, LGX_DRAW_NOISE + P->num_obs};
+  __shared__ float part[LGX_ENV_BLOCK][LGX_PARTIAL_STRIDE];
+  int tid = threadIdx.x;
+  int k = blockIdx.x * LGX_ENV_BLOCK + tid;
+  for (int t = 0; t < LGX_PARTIAL_STRIDE; ++t) part[tid][t] = 0.f;
+  if (k < n) {
+    int e = ids[k];
+    float cmd[4];
+    for (int c = 0; c < 4; ++c) cmd[c] = B.commands[(int64_t)e * 4 + c];
+    for (int t = 0; t < T; ++t) {
+      part[tid][t] = B.episode_sums[(int64_t)t * N + e];
+      B.episode_sums[(int64_t)t * N + e] = 0.f;
+    }
+    part[tid][T] = 1.f;
+    reset_env(P, B, D, e, step, 1u, init_done != 0, cmd);
+    for (int c = 0; c < 4; ++c) B.commands[(int64_t)e * 4 + c] = cmd[c];
+  }
+  block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
+}
+
+// extras finalize: deterministic sum of block partials; publish only if >= 1 env reset
+__global__ void __launch_bounds__(256)
+lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks) {
+  const int N = P->num_envs;
+  const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
+  __shared__ float red[256];
+  __shared__ float sums[LGX_PARTIAL_STRIDE];
+  int t = threadIdx.x;
+  if (t <= T) {
+    float s = 0.f;
+    for (int b = 0; b < nblocks; ++b) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + t];
+    sums[t] = s;
+  }
+  float lv = 0.f;
+  if (P->curriculum)
+    for (int e = t; e < N; e += 256) lv += (float)B.terrain_levels[e];
+  red[t] = lv;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  float count = sums[T];
+  if (count <= 0.f) return;  // reference keeps stale extras (legged_robot.py:160-161)
+  if (t < T) B.extras[t] = (sums[t] / count) / P->max_episode_length_s;
+  if (t == 0) {
+    if (P->curriculum) B.extras[T] = red[0] / (float)N;
+    B.extras[T + 1] = count;
+  }
+  if (P->send_timeouts)
+    for (int e = t; e < N; e += 256) B.extras_time_outs[e] = B.time_out[e];
+}
+
+int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
+                            int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
+                            hipStream_t stream) {
+  (void)num_obs; (void)n_term_rows; (void)measure_heights;
+  int blocks = (n_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
+  hipLaunchKernelGGL(lgx_post_physics_kernel, dim3(blocks), dim3(ENV_THREADS), 0, stream, dp, b, step, draws);
+  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
+                         const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
+                         hipStream_t stream) {
+  (void)n_envs; (void)n_term_rows;
+  if (n <= 0) return 0;
+  int blocks = (n + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
+  hipLaunchKernelGGL(lgx_reset_idx_kernel, dim3(blocks), dim3(LGX_ENV_BLOCK), 0, stream, dp, b, ids, n, step,
+                     init_done, draws);
+  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -1,0 +1,36 @@
+// Internal (non-ABI) declarations shared by the lgx HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/lgx.h"
+
+#define LGX_MAX_LANE_PTS 48
+
+// device-resident model: the ABI model + the per-lane (per-leg) contact candidate tables
+struct lgx_dev_model {
+  lgx_model m;
+  int32_t lane_npts[4];
+  int32_t max_lane_npts;
+  int32_t pad;
+  int32_t lane_pts[4][LGX_MAX_LANE_PTS];
+};
+
+int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
+                       int32_t nsub, int32_t from_actions, hipStream_t stream);
+int lgx_launch_clip_actions(float* a, int64_t n, float clip, hipStream_t stream);
+int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
+                            int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
+                            hipStream_t stream);
+int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
+                         const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
+                         hipStream_t stream);
+int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
+                            hipStream_t stream);
+int lgx_launch_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m, const float* w,
+                             hipStream_t stream);
+int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
+                           const float* const* weights, const float* const* biases, int32_t act, hipStream_t stream);
+
+// scratch layout (floats): [blocks][LGX_MAX_TERMS + 2] reduction partials
+#define LGX_ENV_BLOCK 64
+#define LGX_PARTIAL_STRIDE (LGX_MAX_TERMS + 2)

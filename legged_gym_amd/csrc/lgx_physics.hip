@@ -1,0 +1,612 @@
+// lgx physics kernel: `decimation` fused substeps of floating-base 4x3-DoF articulated
+// dynamics with implicit PD drives, joint-limit springs and compliant ground contact.
+// Replaces Isaac Gym PhysX `gym.simulate` as driven by LeggedRobot.step
+// (legged_robot.py:89-99; model/drive setup legged_robot.py:645-740).  Model: DESIGN.md §3.
+//
+// Mapping (CDNA4, wave64): one env per 4-lane quad, lane = leg.  A wave holds 16 envs.
+// The joint-space mass matrix of a quadruped is "arrowhead": a 6x6 base block A coupled to
+// four independent 3x3 leg blocks D_l through 6x3 blocks B_l.  Each lane builds its leg's
+// B_l/D_l (composite-rigid-body algorithm on a 3-link chain), its leg's bias forces
+// (RNEA) and its leg's contact terms; the base Schur complement A - sum_l B_l D_l^-1 B_l^T
+// is formed with two quad shuffles per entry and solved redundantly in all 4 lanes; the
+// leg back-substitution is lane-local again.  All state stays in VGPRs across substeps;
+// HBM traffic per env-step = state in + state out (+ actuator-net history).
+#include "lgx_device.h"
+#include "lgx_internal.h"
+
+namespace {
+
+struct sv { f3 a, l; };  // spatial vector (angular; linear), reference point = base origin O
+LGX_DEV sv sv0() { return sv{mk3(0, 0, 0), mk3(0, 0, 0)}; }
+LGX_DEV sv add(sv x, sv y) { return sv{x.a + y.a, x.l + y.l}; }
+LGX_DEV sv scale(float s, sv x) { return sv{s * x.a, s * x.l}; }
+LGX_DEV float dot(sv x, sv y) { return dot(x.a, y.a) + dot(x.l, y.l); }
+LGX_DEV sv crm(sv V, sv s) { return sv{cross(V.a, s.a), cross(V.a, s.l) + cross(V.l, s.a)}; }
+LGX_DEV sv crf(sv V, sv f) { return sv{cross(V.a, f.a) + cross(V.l, f.l), cross(V.a, f.l)}; }
+
+// compact spatial inertia about O: [[Ibar, skew(h)], [skew(h)^T, m 1]], h = m c
+struct SI { float m; f3 h; float I[6]; };  // I: xx yy zz xy xz yz
+LGX_DEV SI si_add(const SI& x, const SI& y) {
+  SI r; r.m = x.m + y.m; r.h = x.h + y.h;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) r.I[i] = x.I[i] + y.I[i];
+  return r;
+}
+LGX_DEV sv si_mul(const SI& s, sv v) {
+  f3 Ia = mk3(s.I[0] * v.a.x + s.I[3] * v.a.y + s.I[4] * v.a.z, s.I[3] * v.a.x + s.I[1] * v.a.y + s.I[5] * v.a.z,
+              s.I[4] * v.a.x + s.I[5] * v.a.y + s.I[2] * v.a.z);
+  return sv{Ia + cross(s.h, v.l), cross(v.a, s.h) + s.m * v.l};
+}
+LGX_DEV SI body_si(const lgx_model* __restrict__ M, int b, float scale, const m33& R, f3 o) {
+  const float* in = M->body_inertia[b];
+  m33 Ib = {{in[0], in[3], in[4], in[3], in[1], in[5], in[4], in[5], in[2]}};
+  m33 T = mul(R, Ib);
+  float Iw[6];  // T R^T, symmetric part
+  Iw[0] = T.a[0] * R.a[0] + T.a[1] * R.a[1] + T.a[2] * R.a[2];
+  Iw[1] = T.a[3] * R.a[3] + T.a[4] * R.a[4] + T.a[5] * R.a[5];
+  Iw[2] = T.a[6] * R.a[6] + T.a[7] * R.a[7] + T.a[8] * R.a[8];
+  Iw[3] = T.a[0] * R.a[3] + T.a[1] * R.a[4] + T.a[2] * R.a[5];
+  Iw[4] = T.a[0] * R.a[6] + T.a[1] * R.a[7] + T.a[2] * R.a[8];
+  Iw[5] = T.a[3] * R.a[6] + T.a[4] * R.a[7] + T.a[5] * R.a[8];
+  f3 c = o + mul(R, mk3(M->body_com[b][0], M->body_com[b][1], M->body_com[b][2]));
+  float m = M->body_mass[b] * scale;
+  float cc = dot(c, c);
+  SI s;
+  s.m = m;
+  s.h = m * c;
+  s.I[0] = Iw[0] * scale + m * (cc - c.x * c.x);
+  s.I[1] = Iw[1] * scale + m * (cc - c.y * c.y);
+  s.I[2] = Iw[2] * scale + m * (cc - c.z * c.z);
+  s.I[3] = Iw[3] * scale - m * c.x * c.y;
+  s.I[4] = Iw[4] * scale - m * c.x * c.z;
+  s.I[5] = Iw[5] * scale - m * c.y * c.z;
+  return s;
+}
+
+// packed symmetric 6x6 (upper triangle, row-major): idx(i,j), i<=j
+LGX_DEV constexpr int sidx(int i, int j) { return i <= j ? (i * 11 - i * i) / 2 + j : (j * 11 - j * j) / 2 + i; }
+
+LGX_DEV void si_to_sym6(const SI& s, float* A) {  // A[21]
+  A[sidx(0, 0)] = s.I[0]; A[sidx(1, 1)] = s.I[1]; A[sidx(2, 2)] = s.I[2];
+  A[sidx(0, 1)] = s.I[3]; A[sidx(0, 2)] = s.I[4]; A[sidx(1, 2)] = s.I[5];
+  // top-right skew(h): [[0,-hz,hy],[hz,0,-hx],[-hy,hx,0]]
+  A[sidx(0, 3)] = 0.f;     A[sidx(0, 4)] = -s.h.z; A[sidx(0, 5)] = s.h.y;
+  A[sidx(1, 3)] = s.h.z;   A[sidx(1, 4)] = 0.f;    A[sidx(1, 5)] = -s.h.x;
+  A[sidx(2, 3)] = -s.h.y;  A[sidx(2, 4)] = s.h.x;  A[sidx(2, 5)] = 0.f;
+  A[sidx(3, 3)] = s.m; A[sidx(4, 4)] = s.m; A[sidx(5, 5)] = s.m;
+  A[sidx(3, 4)] = 0.f; A[sidx(3, 5)] = 0.f; A[sidx(4, 5)] = 0.f;
+}
+
+LGX_DEV float sv_get(const sv& v, int i) {
+  return i == 0 ? v.a.x : i == 1 ? v.a.y : i == 2 ? v.a.z : i == 3 ? v.l.x : i == 4 ? v.l.y : v.l.z;
+}
+
+// 6x6 SPD solve (packed sym), in registers
+LGX_DEV void chol6_solve(float* A, float* b) {
+  float L[21];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    float s = A[sidx(j, j)];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= L[sidx(j, k)] * L[sidx(j, k)];
+    float d = sqrtf(fmaxf(s, 1e-20f));
+    L[sidx(j, j)] = d;
+    float inv = 1.0f / d;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      float t = A[sidx(i, j)];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= L[sidx(i, k)] * L[sidx(j, k)];
+      L[sidx(i, j)] = t * inv;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t -= L[sidx(i, k)] * b[k];
+    b[i] = t / L[sidx(i, i)];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    float t = b[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) t -= L[sidx(k, i)] * b[k];
+    b[i] = t / L[sidx(i, i)];
+  }
+}
+
+// inverse of a symmetric positive-definite 3x3 (packed d00 d11 d22 d01 d02 d12)
+LGX_DEV void inv3sym(const float* D, float* Di) {
+  float c00 = D[1] * D[2] - D[5] * D[5];
+  float c01 = D[4] * D[5] - D[3] * D[2];
+  float c02 = D[3] * D[5] - D[4] * D[1];
+  float det = D[0] * c00 + D[3] * c01 + D[4] * c02;
+  float id = 1.0f / det;
+  Di[0] = c00 * id;
+  Di[3] = c01 * id;
+  Di[4] = c02 * id;
+  Di[1] = (D[0] * D[2] - D[4] * D[4]) * id;
+  Di[5] = (D[3] * D[4] - D[0] * D[5]) * id;
+  Di[2] = (D[0] * D[1] - D[3] * D[3]) * id;
+}
+LGX_DEV f3 sym3_mul(const float* D, f3 x) {
+  return mk3(D[0] * x.x + D[3] * x.y + D[4] * x.z, D[3] * x.x + D[1] * x.y + D[5] * x.z,
+             D[4] * x.x + D[5] * x.y + D[2] * x.z);
+}
+
+// Jacobian column c (0..5) of the base part of a point velocity v_P = v + w x P: e_c x P | e_{c-3}
+LGX_DEV f3 jb_col(int c, f3 P) {
+  return c == 0 ? mk3(0.f, -P.z, P.y) : c == 1 ? mk3(P.z, 0.f, -P.x) : c == 2 ? mk3(-P.y, P.x, 0.f)
+       : c == 3 ? mk3(1.f, 0.f, 0.f) : c == 4 ? mk3(0.f, 1.f, 0.f) : mk3(0.f, 0.f, 1.f);
+}
+
+LGX_DEV m33 sel3(int k, const m33& a, const m33& b, const m33& c) {
+  m33 r;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) r.a[i] = k == 0 ? a.a[i] : (k == 1 ? b.a[i] : c.a[i]);
+  return r;
+}
+LGX_DEV f3 sel3(int k, f3 a, f3 b, f3 c) { return k == 0 ? a : (k == 1 ? b : c); }
+LGX_DEV sv sel3(int k, const sv& a, const sv& b, const sv& c) { return sv{sel3(k, a.a, b.a, c.a), sel3(k, a.l, b.l, c.l)}; }
+
+struct LegSys {     // lane-private pieces of the arrowhead system
+  float Ap[21];     // base-block additions from this lane (contacts)
+  float B[6][3];    // base-leg coupling
+  float D[6];       // leg block (packed sym 3x3)
+  float rb[6];      // base rhs partial
+  float rl[3];      // leg rhs
+};
+
+// adds J^T W J and J^T f for a point P on leg body `k` (k = -1: base), W = wt*I + (wn - wt) n n^T
+LGX_DEV void add_contact(LegSys& L, f3 P, f3 n, float wn, float wt, f3 f, int k, const sv* S) {
+  f3 Jc[9];  // 6 base + up to 3 leg columns
+#pragma unroll
+  for (int c = 0; c < 6; ++c) Jc[c] = jb_col(c, P);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) Jc[6 + j] = (j <= k) ? cross(S[j].a, P) + S[j].l : mk3(0.f, 0.f, 0.f);
+  f3 WJ[9];
+  float dw = wn - wt;
+#pragma unroll
+  for (int c = 0; c < 9; ++c) WJ[c] = wt * Jc[c] + (dw * dot(n, Jc[c])) * n;
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = i; j < 6; ++j) L.Ap[sidx(i, j)] += dot(Jc[i], WJ[j]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) L.B[i][j] += dot(Jc[i], WJ[6 + j]);
+  L.D[0] += dot(Jc[6], WJ[6]); L.D[1] += dot(Jc[7], WJ[7]); L.D[2] += dot(Jc[8], WJ[8]);
+  L.D[3] += dot(Jc[6], WJ[7]); L.D[4] += dot(Jc[6], WJ[8]); L.D[5] += dot(Jc[7], WJ[8]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) L.rb[i] += dot(Jc[i], f);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) L.rl[j] += dot(Jc[6 + j], f);
+}
+
+// solve the arrowhead system; returns base solution xb[6] (all lanes) and leg solution xl
+LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon, bool lane0, float* xb, f3& xl) {
+  float Di[6];
+  inv3sym(L.D, Di);
+  // Y = Di B^T (3x6); Schur partial = Ap - B Y ; rb partial = rb - B Di rl
+  f3 Y[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) Y[i] = sym3_mul(Di, mk3(L.B[i][0], L.B[i][1], L.B[i][2]));
+  f3 Dr = sym3_mul(Di, mk3(L.rl[0], L.rl[1], L.rl[2]));
+  float A[21], rb[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+#pragma unroll
+    for (int j = i; j < 6; ++j) {
+      float v = L.Ap[sidx(i, j)] - (L.B[i][0] * Y[j].x + L.B[i][1] * Y[j].y + L.B[i][2] * Y[j].z);
+      if (lane0) v += Acommon[sidx(i, j)];
+      A[sidx(i, j)] = quad_sum(v);
+    }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    float v = L.rb[i] - (L.B[i][0] * Dr.x + L.B[i][1] * Dr.y + L.B[i][2] * Dr.z);
+    if (lane0) v += rbcommon[i];
+    rb[i] = quad_sum(v);
+  }
+  chol6_solve(A, rb);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) xb[i] = rb[i];
+  f3 t = mk3(L.rl[0], L.rl[1], L.rl[2]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) t = t - xb[i] * mk3(L.B[i][0], L.B[i][1], L.B[i][2]);
+  xl = sym3_mul(Di, t);
+}
+
+}  // namespace
+
+#define PHYS_BLOCK 64
+#define MAX_LANE_PTS 48
+
+__global__ void __launch_bounds__(PHYS_BLOCK)
+lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* __restrict__ P, lgx_buffers B,
+                   int32_t nsub, int32_t from_actions) {
+  const lgx_model* __restrict__ M = &DM->m;
+  const int tid = threadIdx.x;
+  const int gl = blockIdx.x * PHYS_BLOCK + tid;
+  const int e = gl >> 2;
+  const int leg = gl & 3;
+  const bool lane0 = leg == 0;
+  const int N = P->num_envs;
+  const bool valid = e < N;
+  const int ec = valid ? e : N - 1;  // inactive quads compute on a clamped env, never store
+  __shared__ float4 slot_state[PHYS_BLOCK][MAX_LANE_PTS];  // per candidate: status, fslide.xyz
+
+  const float dt = M->sim_dt;
+  // ---- load state
+  const float* rs = B.root_states + (int64_t)ec * 13;
+  f3 pos = mk3(rs[0], rs[1], rs[2]);
+  float qx = rs[3], qy = rs[4], qz = rs[5], qw = rs[6];
+  f3 vlin = mk3(rs[7], rs[8], rs[9]);
+  f3 wang = mk3(rs[10], rs[11], rs[12]);
+  float th[3], thd[3], tgt[3], act[3];
+  const float* ds = B.dof_state + (int64_t)ec * 24 + leg * 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) { th[k] = ds[2 * k]; thd[k] = ds[2 * k + 1]; }
+  float mscale[4];
+  mscale[0] = B.body_mass_scale[(int64_t)ec * 13];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) mscale[1 + k] = B.body_mass_scale[(int64_t)ec * 13 + 1 + 3 * leg + k];
+  const float mu = 0.5f * ((B.friction ? B.friction[ec] : 1.0f) + M->ground_friction);
+  const int ctrl = P->control_type;
+  float hist[30];
+  const bool use_hist = from_actions && P->use_actuator_history;
+  if (from_actions) {
+    const float* a = B.actions + (int64_t)ec * 12 + leg * 3;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) act[k] = a[k];
+  }
+  if (ctrl == LGX_CTRL_POS_DRIVE) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int j = 3 * leg + k;
+      // _compute_poses (legged_robot.py:394-397); identical every substep
+      tgt[k] = from_actions ? clampf(act[k] * P->action_scale + P->default_dof_pos[j], P->soft_lower[j], P->soft_upper[j])
+                            : B.dof_targets[(int64_t)ec * 12 + j];
+    }
+  }
+  if (use_hist) {
+    const float* h = B.act_hist + (int64_t)ec * 120 + leg * 30;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) hist[i] = h[i];
+  }
+  const int npts = DM->lane_npts[leg];
+  const int maxpts = DM->max_lane_npts;
+  f3 cf_leg[4] = {mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0)};
+  f3 cf_base = mk3(0, 0, 0);
+  float tq[3] = {0.f, 0.f, 0.f};
+
+  for (int s = 0; s < nsub; ++s) {
+    // ---- Go1 actuator-net history (go1.py:79-98), model_ins per substep
+    if (use_hist) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        int j = 3 * leg + k;
+        float pe = act[k] - th[k];
+        float pes = (pe - P->act_pos_err_mean[j]) / P->act_pos_err_std[j];
+        float vs = (thd[k] - P->act_vel_mean[j]) / P->act_vel_std[j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { hist[10 * k + i] = hist[10 * k + i + 1]; hist[10 * k + 5 + i] = hist[10 * k + 6 + i]; }
+        hist[10 * k + 4] = pes;
+        hist[10 * k + 9] = vs;
+      }
+      if (valid) {
+        float* mi = B.model_ins + ((int64_t)s * N + e) * 120 + leg * 30;
+#pragma unroll
+        for (int i = 0; i < 30; i += 2) *reinterpret_cast<float2*>(mi + i) = make_float2(hist[i], hist[i + 1]);
+      }
+    }
+    // ---- explicit-torque controllers (_compute_torques, legged_robot.py:370-392)
+    float tex[3] = {0.f, 0.f, 0.f};
+    if (ctrl != LGX_CTRL_POS_DRIVE && !from_actions) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) tex[k] = B.torques[(int64_t)ec * 12 + 3 * leg + k];  // caller-provided torques
+    } else if (ctrl != LGX_CTRL_POS_DRIVE) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        int j = 3 * leg + k;
+        float a = act[k] * P->action_scale, t;
+        if (ctrl == LGX_CTRL_P) t = P->p_gains[j] * (a + P->default_dof_pos[j] - th[k]) - P->d_gains[j] * thd[k];
+        else if (ctrl == LGX_CTRL_V)
+          t = P->p_gains[j] * (a - thd[k]) - P->d_gains[j] * (thd[k] - B.last_dof_vel[(int64_t)ec * 12 + j]) / dt;
+        else t = a;
+        tex[k] = clampf(t, -P->torque_limits[j], P->torque_limits[j]);
+      }
+    }
+    // ---- kinematics
+    m33 R0 = quat_to_mat(qx, qy, qz, qw);
+    m33 Rb[3];
+    f3 ob[3];
+    sv S[3];
+    {
+      m33 Rp = R0;
+      f3 op = mk3(0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        int j = 3 * leg + k;
+        m33 E;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) E.a[i] = M->joint_rot[j][i];
+        m33 Rjf = mul(Rp, E);
+        f3 oj = op + mul(Rp, mk3(M->joint_pos[j][0], M->joint_pos[j][1], M->joint_pos[j][2]));
+        f3 ax = mk3(M->joint_axis[j][0], M->joint_axis[j][1], M->joint_axis[j][2]);
+        f3 aw = mul(Rjf, ax);
+        Rb[k] = mul(Rjf, axis_angle(ax, th[k]));
+        ob[k] = oj;
+        S[k] = sv{aw, cross(oj, aw)};
+        Rp = Rb[k];
+        op = oj;
+      }
+    }
+    SI Ibase = body_si(M, 0, mscale[0], R0, mk3(0, 0, 0));
+    SI Il[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) Il[k] = body_si(M, 1 + 3 * leg + k, mscale[1 + k], Rb[k], ob[k]);
+    // ---- RNEA bias forces, A_0 = (0, -w x v - g)
+    sv V0 = sv{wang, vlin};
+    sv A0 = sv{mk3(0, 0, 0), mk3(0, 0, 0) - cross(wang, vlin) - mk3(M->gravity[0], M->gravity[1], M->gravity[2])};
+    sv Vk[3], fk[3];
+    {
+      sv Vp = V0, Ap = A0;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        sv V = add(Vp, scale(thd[k], S[k]));
+        sv A = add(Ap, scale(thd[k], crm(V, S[k])));
+        fk[k] = add(si_mul(Il[k], A), crf(V, si_mul(Il[k], V)));
+        Vk[k] = V;
+        Vp = V; Ap = A;
+      }
+    }
+    sv F2 = fk[2], F1 = add(fk[1], F2), F0 = add(fk[0], F1);
+    float Cl[3] = {dot(S[0], F0), dot(S[1], F1), dot(S[2], F2)};
+    sv fbase = add(si_mul(Ibase, A0), crf(V0, si_mul(Ibase, V0)));
+    // ---- CRBA: composite inertias, B = [IC_k S_k], D_kk' = S_k . IC_k' S_k'
+    SI IC2 = Il[2], IC1 = si_add(Il[1], IC2), IC0 = si_add(Il[0], IC1);
+    sv Fc[3] = {si_mul(IC0, S[0]), si_mul(IC1, S[1]), si_mul(IC2, S[2])};
+    LegSys L0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) L0.B[i][k] = sv_get(Fc[k], i);
+    L0.D[0] = dot(S[0], Fc[0]); L0.D[1] = dot(S[1], Fc[1]); L0.D[2] = dot(S[2], Fc[2]);
+    L0.D[3] = dot(S[0], Fc[1]); L0.D[4] = dot(S[0], Fc[2]); L0.D[5] = dot(S[1], Fc[2]);
+    // base block common part: total composite inertia (quad-reduced)
+    float Acom[21];
+    {
+      SI tot = IC0;
+      tot.m = quad_sum(tot.m);
+      tot.h = mk3(quad_sum(tot.h.x), quad_sum(tot.h.y), quad_sum(tot.h.z));
+#pragma unroll
+      for (int i = 0; i < 6; ++i) tot.I[i] = quad_sum(tot.I[i]);
+      tot = si_add(tot, Ibase);
+      si_to_sym6(tot, Acom);
+    }
+    // H u and bias: rb = A u_b - dt f_base + sum_l (B_l qd_l - dt F0_l);  rl = B^T u_b + D qd + dt(g - C)
+    float ub[6] = {wang.x, wang.y, wang.z, vlin.x, vlin.y, vlin.z};
+    float rbcom[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) s2 += Acom[sidx(i, j)] * ub[j];
+      rbcom[i] = s2 - dt * sv_get(fbase, i);
+    }
+    float rb0[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rb0[i] = L0.B[i][0] * thd[0] + L0.B[i][1] * thd[1] + L0.B[i][2] * thd[2] - dt * sv_get(F0, i);
+    float rl0[3];
+    {
+      f3 Dq = sym3_mul(L0.D, mk3(thd[0], thd[1], thd[2]));
+      float dqv[3] = {Dq.x, Dq.y, Dq.z};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        float s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) s2 += L0.B[i][k] * ub[i];
+        rl0[k] = s2 + dqv[k] - dt * Cl[k];
+      }
+    }
+    // ---- drives and limits
+    float Dimp[3] = {0.f, 0.f, 0.f};
+    bool impl[3] = {false, false, false};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int j = 3 * leg + k;
+      float g = 0.f;
+      if (ctrl == LGX_CTRL_POS_DRIVE) {
+        float eff = M->dof_effort[j];
+        float te = M->kp[j] * (tgt[k] - th[k]) - M->kd[j] * thd[k];
+        if (fabsf(te) <= eff) {
+          impl[k] = true;
+          Dimp[k] += dt * (M->kd[j] + dt * M->kp[j]);
+          g += M->kp[j] * (tgt[k] - th[k]);
+        } else {
+          g += te > 0.f ? eff : -eff;
+        }
+      } else {
+        g += tex[k];
+      }
+      float lo = M->dof_lower[j], hi = M->dof_upper[j];
+      if (lo < hi) {
+        if (th[k] < lo) { Dimp[k] += dt * (M->limit_c + dt * M->limit_k); g += M->limit_k * (lo - th[k]); }
+        else if (th[k] > hi) { Dimp[k] += dt * (M->limit_c + dt * M->limit_k); g -= M->limit_k * (th[k] - hi); }
+      }
+      rl0[k] += dt * g;
+    }
+    L0.D[0] += Dimp[0]; L0.D[1] += Dimp[1]; L0.D[2] += Dimp[2];
+    // ---- contacts: two passes (pass 0 implicit stick, pass 1 with slide / drop decisions)
+    const float kn = M->contact_k, cn = M->contact_c, ct = M->friction_c;
+    const float wn = dt * (cn + dt * kn);
+    float xb[6];
+    f3 xl;
+    for (int pass = 0; pass < 2; ++pass) {
+      LegSys L = L0;
+#pragma unroll
+      for (int i = 0; i < 21; ++i) L.Ap[i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) L.rb[i] = rb0[i];
+      L.rl[0] = rl0[0]; L.rl[1] = rl0[1]; L.rl[2] = rl0[2];
+      for (int c = 0; c < maxpts; ++c) {
+        if (c >= npts) break;
+        int pi = DM->lane_pts[leg][c];
+        int db = M->point_dyn[pi];
+        int k = db == 0 ? -1 : (db - 1) % 3;
+        m33 R = db == 0 ? R0 : sel3(k, Rb[0], Rb[1], Rb[2]);
+        f3 ol = db == 0 ? mk3(0, 0, 0) : sel3(k, ob[0], ob[1], ob[2]);
+        f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
+        f3 n;
+        float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
+        float rad = M->point_radius[pi];
+        float depth = (h - (Pp.z + pos.z)) * n.z + rad;
+        float4 st = slot_state[tid][c];
+        if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[tid][c] = st; }
+        if (depth <= 0.f || st.x == 0.f) continue;
+        f3 Pc = Pp - rad * n;
+        float wt = (pass == 0 || st.x == 1.f) ? dt * ct : 0.f;
+        f3 f = (dt * kn * depth) * n;
+        if (pass == 1 && st.x == 2.f) f = f + dt * mk3(st.y, st.z, st.w);
+        add_contact(L, Pc, n, wn, wt, f, k, S);
+      }
+      arrow_solve(L, Acom, rbcom, lane0, xb, xl);
+      // contact status (after pass 0) / reported forces (after pass 1, last substep)
+      const bool report = pass == 1 && s == nsub - 1;
+      if (pass == 0 || report) {
+        sv Vb = sv{mk3(xb[0], xb[1], xb[2]), mk3(xb[3], xb[4], xb[5])};
+        sv Vl[3];
+        Vl[0] = add(Vb, scale(xl.x, S[0]));
+        Vl[1] = add(Vl[0], scale(xl.y, S[1]));
+        Vl[2] = add(Vl[1], scale(xl.z, S[2]));
+        for (int c = 0; c < maxpts; ++c) {
+          if (c >= npts) break;
+          float4 st = slot_state[tid][c];
+          if (st.x == 0.f) continue;
+          int pi = DM->lane_pts[leg][c];
+          int db = M->point_dyn[pi];
+          int k = db == 0 ? -1 : (db - 1) % 3;
+          m33 R = db == 0 ? R0 : sel3(k, Rb[0], Rb[1], Rb[2]);
+          f3 ol = db == 0 ? mk3(0, 0, 0) : sel3(k, ob[0], ob[1], ob[2]);
+          f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
+          f3 n;
+          float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
+          float rad = M->point_radius[pi];
+          float depth = (h - (Pp.z + pos.z)) * n.z + rad;
+          f3 Pc = Pp - rad * n;
+          sv V = db == 0 ? Vb : sel3(k, Vl[0], Vl[1], Vl[2]);
+          f3 vp = V.l + cross(V.a, Pc);
+          float vn = dot(vp, n);
+          float fn = kn * depth - (cn + dt * kn) * vn;
+          f3 vt = vp - vn * n;
+          if (pass == 0) {
+            float vtn = sqrtf(dot(vt, vt));
+            if (fn <= 0.f) st.x = 0.f;
+            else if (ct * vtn > mu * fn) {
+              float sc = -mu * fn / vtn;
+              st = make_float4(2.f, sc * vt.x, sc * vt.y, sc * vt.z);
+            } else st.x = 1.f;
+            slot_state[tid][c] = st;
+          } else {
+            fn = fmaxf(fn, 0.f);
+            f3 ft = st.x == 1.f ? (-ct) * vt : mk3(st.y, st.z, st.w);
+            f3 F = fn * n + ft;
+            int rep = M->point_report[pi];
+            if (rep == 0) cf_base = cf_base + F;
+            else {
+              int r = rep - (1 + 4 * leg);
+              cf_leg[0] = r == 0 ? cf_leg[0] + F : cf_leg[0];
+              cf_leg[1] = r == 1 ? cf_leg[1] + F : cf_leg[1];
+              cf_leg[2] = r == 2 ? cf_leg[2] + F : cf_leg[2];
+              cf_leg[3] = r == 3 ? cf_leg[3] + F : cf_leg[3];
+            }
+          }
+        }
+      }
+    }
+    // ---- joint outputs and integration
+    float qdn[3] = {xl.x, xl.y, xl.z};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      int j = 3 * leg + k;
+      float q2 = qdn[k];
+      float vl = M->dof_vel_limit[j];
+      if (vl > 0.f) q2 = clampf(q2, -vl, vl);
+      if (ctrl == LGX_CTRL_POS_DRIVE) {
+        float eff = M->dof_effort[j];
+        float t = impl[k] ? M->kp[j] * (tgt[k] - th[k] - dt * qdn[k]) - M->kd[j] * qdn[k]
+                          : M->kp[j] * (tgt[k] - th[k]) - M->kd[j] * thd[k];
+        tq[k] = clampf(t, -eff, eff);
+      } else {
+        tq[k] = tex[k];
+      }
+      th[k] = th[k] + dt * q2;
+      thd[k] = q2;
+    }
+    wang = mk3(xb[0], xb[1], xb[2]);
+    vlin = mk3(xb[3], xb[4], xb[5]);
+    pos = pos + dt * vlin;
+    {
+      f3 qv = mk3(qx, qy, qz);
+      f3 wq = cross(wang, qv);
+      float dqx = 0.5f * (qw * wang.x + wq.x), dqy = 0.5f * (qw * wang.y + wq.y), dqz = 0.5f * (qw * wang.z + wq.z);
+      float dqw = -0.5f * dot(wang, qv);
+      qx += dt * dqx; qy += dt * dqy; qz += dt * dqz; qw += dt * dqw;
+      float inv = 1.0f / sqrtf(qx * qx + qy * qy + qz * qz + qw * qw);
+      qx *= inv; qy *= inv; qz *= inv; qw *= inv;
+    }
+  }
+
+  // ---- write back
+  cf_base = mk3(quad_sum(cf_base.x), quad_sum(cf_base.y), quad_sum(cf_base.z));
+  if (!valid) return;
+  float* dso = B.dof_state + (int64_t)e * 24 + leg * 6;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) *reinterpret_cast<float2*>(dso + 2 * k) = make_float2(th[k], thd[k]);
+  float* tqo = B.torques + (int64_t)e * 12 + leg * 3;
+  if (nsub > 0) { tqo[0] = tq[0]; tqo[1] = tq[1]; tqo[2] = tq[2]; }
+  if (ctrl == LGX_CTRL_POS_DRIVE && from_actions) {
+    float* to = B.dof_targets + (int64_t)e * 12 + leg * 3;
+    to[0] = tgt[0]; to[1] = tgt[1]; to[2] = tgt[2];
+  }
+  float* cfo = B.contact_forces + (int64_t)e * LGX_MAX_BODIES * 3;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float* d = cfo + (1 + 4 * leg + r) * 3;
+    d[0] = cf_leg[r].x; d[1] = cf_leg[r].y; d[2] = cf_leg[r].z;
+  }
+  if (use_hist) {
+    float* h = B.act_hist + (int64_t)e * 120 + leg * 30;
+#pragma unroll
+    for (int i = 0; i < 30; i += 2) *reinterpret_cast<float2*>(h + i) = make_float2(hist[i], hist[i + 1]);
+  }
+  if (lane0) {
+    cfo[0] = cf_base.x; cfo[1] = cf_base.y; cfo[2] = cf_base.z;
+    float* ro = B.root_states + (int64_t)e * 13;
+    ro[0] = pos.x; ro[1] = pos.y; ro[2] = pos.z;
+    ro[3] = qx; ro[4] = qy; ro[5] = qz; ro[6] = qw;
+    ro[7] = vlin.x; ro[8] = vlin.y; ro[9] = vlin.z;
+    ro[10] = wang.x; ro[11] = wang.y; ro[12] = wang.z;
+  }
+}
+
+// clip actions in place (legged_robot.py:85-86): one thread per element
+__global__ void lgx_clip_actions_kernel(float* a, int64_t n, float clip) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) a[i] = clampf(a[i], -clip, clip);
+}
+
+int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
+                       int32_t nsub, int32_t from_actions, hipStream_t stream) {
+  int blocks = (n_envs * 4 + PHYS_BLOCK - 1) / PHYS_BLOCK;
+  hipLaunchKernelGGL(lgx_physics_kernel, dim3(blocks), dim3(PHYS_BLOCK), 0, stream, dm, dp, b, nsub, from_actions);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int lgx_launch_clip_actions(float* a, int64_t n, float clip, hipStream_t stream) {
+  int blocks = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(lgx_clip_actions_kernel, dim3(blocks), dim3(256), 0, stream, a, n, clip);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}

@@ -1,0 +1,55 @@
+"""ANYmal-C env (legged_gym/envs/anymal_c/anymal.py:46-80).
+
+The SEA LSTM actuator is only reachable through `_compute_torques`, which this fork's step
+path does not call (the step uses the PhysX position drive, legged_robot.py:93-96); the
+hidden/cell state buffers and `actuator_torques()` (lgx_actuator_lstm, HIP) are provided so
+the LSTM path exists with the reference's semantics (input [a*scale + q0 - q, qd] x in_scale,
+torque = out_scale * Linear(h), state zeroed on reset).
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from legged_gym_amd import LEGGED_GYM_ROOT_DIR
+from legged_gym_amd.envs.base.legged_robot import LeggedRobot
+from legged_gym_amd.sim.model import load_actuator_net
+
+
+def pack_lstm_weights(net):
+    order = ["in_scale", "out_scale", "w_ih_l0", "w_hh_l0", "b_ih_l0", "b_hh_l0", "w_ih_l1", "w_hh_l1", "b_ih_l1",
+             "b_hh_l1", "w_lin", "b_lin"]
+    return np.concatenate([np.asarray(net[k], np.float32).ravel() for k in order])
+
+
+class Anymal(LeggedRobot):
+    def _init_buffers(self):
+        super()._init_buffers()
+        M = self.num_envs * self.num_actions
+        self.sea_input = torch.zeros(M, 1, 2, device=self.device)
+        self.sea_hidden_state = torch.zeros(2, M, 8, device=self.device)
+        self.sea_cell_state = torch.zeros(2, M, 8, device=self.device)
+        self.sea_hidden_state_per_env = self.sea_hidden_state.view(2, self.num_envs, self.num_actions, 8)
+        self.sea_cell_state_per_env = self.sea_cell_state.view(2, self.num_envs, self.num_actions, 8)
+        self._sea_tau = torch.zeros(M, device=self.device)
+        if getattr(self.cfg.control, "use_actuator_network", False):
+            net = load_actuator_net(self.cfg.control.actuator_net_file.format(LEGGED_GYM_ROOT_DIR=LEGGED_GYM_ROOT_DIR))
+            self.actuator_net_weights = torch.tensor(pack_lstm_weights(net), device=self.device)
+
+    def reset_idx(self, env_ids):
+        super().reset_idx(env_ids)
+        self.sea_hidden_state_per_env[:, env_ids] = 0.0   # anymal.py:56-60
+        self.sea_cell_state_per_env[:, env_ids] = 0.0
+
+    def actuator_torques(self, actions):
+        """anymal.py:62-78 on the lgx LSTM kernel: [N, 12] torques, hidden state advanced."""
+        from legged_gym_amd.sim import lib as lgxlib
+        lib = lgxlib.load()
+        self.sea_input[:, 0, 0] = (actions * self.cfg.control.action_scale + self.default_dof_pos - self.dof_pos).flatten()
+        self.sea_input[:, 0, 1] = self.dof_vel.flatten()
+        stream = C.c_void_p(torch.cuda.current_stream(torch.device(self.device)).cuda_stream)
+        lgxlib.check(lib.lgx_actuator_lstm(C.c_void_p(self.sea_input.data_ptr()), C.c_void_p(self.sea_hidden_state.data_ptr()),
+                                           C.c_void_p(self.sea_cell_state.data_ptr()), C.c_void_p(self._sea_tau.data_ptr()),
+                                           self._sea_tau.numel(), C.c_void_p(self.actuator_net_weights.data_ptr()), stream),
+                     "lgx_actuator_lstm")
+        return self._sea_tau.view(self.num_envs, self.num_actions)

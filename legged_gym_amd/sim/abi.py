@@ -1,0 +1,134 @@
+"""ctypes mirror of include/lgx.h (the C-ABI of liblgx.so).
+
+The struct layouts below must match the header field for field; `check_layout(lib)` compares
+them with the library's own `lgx_struct_sizes` so a drift fails loudly at load time.
+This module only describes the ABI; loading the product library is `legged_gym_amd.sim.lib`.
+"""
+import ctypes as C
+
+NUM_DOF = 12
+NUM_DYN = 13
+MAX_BODIES = 17
+MAX_POINTS = 128
+MAX_OBS = 256
+MAX_HEIGHT_POINTS = 192
+MAX_TERMS = 24
+
+# reward term ids (enum lgx_reward_term) keyed by the reference's `_reward_<name>` suffix
+REWARD_IDS = {
+    "lin_vel_z": 0, "ang_vel_xy": 1, "orientation": 2, "base_height": 3, "torques": 4, "energy": 5,
+    "dof_vel": 6, "dof_acc": 7, "action_rate": 8, "collision": 9, "termination": 10,
+    "dof_pos_limits": 11, "dof_vel_limits": 12, "torque_limits": 13, "tracking_lin_vel": 14,
+    "tracking_ang_vel": 15, "feet_air_time": 16, "stumble": 17, "stand_still": 18,
+    "feet_contact_forces": 19, "hip_motion": 20,
+}
+CTRL = {"POS_DRIVE": 0, "P": 1, "V": 2, "T": 3}
+
+DRAW_CMD, DRAW_PUSH, DRAW_RESET_DOF, DRAW_RESET_XY = 0, 3, 5, 17
+DRAW_RESET_VEL, DRAW_RESET_CMD, DRAW_CURRIC, DRAW_NOISE = 19, 25, 28, 32
+
+f32, i32, i64, u64 = C.c_float, C.c_int32, C.c_int64, C.c_uint64
+PF, PU8, PI64, PI16, PI32 = C.POINTER(C.c_float), C.POINTER(C.c_uint8), C.POINTER(C.c_int64), C.POINTER(C.c_int16), C.POINTER(C.c_int32)
+
+
+class LgxModel(C.Structure):
+    _fields_ = [
+        ("joint_rot", f32 * 9 * NUM_DOF), ("joint_pos", f32 * 3 * NUM_DOF), ("joint_axis", f32 * 3 * NUM_DOF),
+        ("dof_lower", f32 * NUM_DOF), ("dof_upper", f32 * NUM_DOF), ("dof_vel_limit", f32 * NUM_DOF),
+        ("dof_effort", f32 * NUM_DOF), ("kp", f32 * NUM_DOF), ("kd", f32 * NUM_DOF),
+        ("body_mass", f32 * NUM_DYN), ("body_com", f32 * 3 * NUM_DYN), ("body_inertia", f32 * 6 * NUM_DYN),
+        ("num_points", i32), ("num_report_bodies", i32),
+        ("point_pos", f32 * 3 * MAX_POINTS), ("point_radius", f32 * MAX_POINTS),
+        ("point_dyn", i32 * MAX_POINTS), ("point_report", i32 * MAX_POINTS),
+        ("contact_k", f32), ("contact_c", f32), ("friction_c", f32), ("limit_k", f32), ("limit_c", f32),
+        ("ground_friction", f32), ("gravity", f32 * 3), ("sim_dt", f32),
+    ]
+
+
+class LgxEnvParams(C.Structure):
+    _fields_ = [
+        ("num_envs", i32), ("num_obs", i32), ("decimation", i32), ("control_type", i32),
+        ("action_scale", f32), ("clip_actions", f32), ("clip_obs", f32), ("dt", f32),
+        ("default_dof_pos", f32 * NUM_DOF), ("soft_lower", f32 * NUM_DOF), ("soft_upper", f32 * NUM_DOF),
+        ("dof_vel_limits", f32 * NUM_DOF), ("torque_limits", f32 * NUM_DOF),
+        ("p_gains", f32 * NUM_DOF), ("d_gains", f32 * NUM_DOF),
+        ("soft_dof_vel_limit", f32), ("soft_torque_limit", f32),
+        ("max_episode_length", f32), ("max_episode_length_s", f32),
+        ("resample_interval", i32), ("push_robots", i32), ("push_interval", i32), ("max_push_vel_xy", f32),
+        ("heading_command", i32), ("cmd_ranges", f32 * 2 * 4),
+        ("obs_scale_lin_vel", f32), ("obs_scale_ang_vel", f32), ("obs_scale_dof_pos", f32),
+        ("obs_scale_dof_vel", f32), ("obs_scale_height", f32),
+        ("add_noise", i32), ("noise_scale_vec", f32 * MAX_OBS),
+        ("terrain_kind", i32), ("measure_heights", i32), ("num_height_points", i32),
+        ("height_points", f32 * 2 * MAX_HEIGHT_POINTS),
+        ("border_size", f32), ("horizontal_scale", f32), ("vertical_scale", f32),
+        ("curriculum", i32), ("custom_origins", i32), ("max_terrain_level", i32), ("terrain_num_cols", i32),
+        ("terrain_env_length", f32), ("base_init_state", f32 * 13),
+        ("num_terms", i32), ("term_ids", i32 * MAX_TERMS), ("term_scales", f32 * MAX_TERMS),
+        ("termination_slot", i32), ("termination_scale", f32), ("only_positive_rewards", i32),
+        ("tracking_sigma", f32), ("base_height_target", f32), ("max_contact_force", f32),
+        ("num_feet", i32), ("feet_indices", i32 * 4),
+        ("num_penalised", i32), ("penalised_indices", i32 * 16),
+        ("num_termination_bodies", i32), ("termination_indices", i32 * 8),
+        ("send_timeouts", i32), ("use_actuator_history", i32),
+        ("act_pos_err_mean", f32 * NUM_DOF), ("act_pos_err_std", f32 * NUM_DOF),
+        ("act_vel_mean", f32 * NUM_DOF), ("act_vel_std", f32 * NUM_DOF),
+        ("seed", u64),
+    ]
+
+
+BUFFER_FIELDS = [
+    ("root_states", PF), ("dof_state", PF), ("dof_targets", PF), ("torques", PF), ("contact_forces", PF),
+    ("actions", PF), ("last_actions", PF), ("last_dof_vel", PF), ("last_root_vel", PF), ("commands", PF),
+    ("base_lin_vel", PF), ("base_ang_vel", PF), ("projected_gravity", PF), ("feet_air_time", PF),
+    ("obs", PF), ("rew", PF), ("reset", PU8), ("time_out", PU8), ("episode_length", PI64),
+    ("episode_sums", PF), ("measured_heights", PF), ("env_origins", PF), ("terrain_levels", PI64),
+    ("terrain_types", PI64), ("terrain_origins", PF), ("height_samples", PI16), ("hf_rows", i32), ("hf_cols", i32),
+    ("body_mass_scale", PF), ("friction", PF), ("act_hist", PF), ("model_ins", PF),
+    ("act_net_w", PF), ("act_net_scale", PF), ("act_dvel", PF),
+    ("extras", PF), ("extras_time_outs", PU8), ("scratch", PF),
+]
+
+
+class LgxBuffers(C.Structure):
+    _fields_ = BUFFER_FIELDS
+
+
+def declare(lib, prefix="lgx"):
+    """Attach argtypes/restypes of the product C-ABI to a loaded CDLL."""
+    vp = C.c_void_p
+    sigs = {
+        "last_error": (C.c_char_p, []),
+        "version": (C.c_int, []),
+        "struct_sizes": (None, [C.POINTER(C.c_int64)]),
+        "scratch_floats": (C.c_int64, [i32, i32]),
+        "sim_create": (C.c_int, [C.POINTER(LgxModel), C.POINTER(LgxEnvParams), C.POINTER(LgxBuffers), C.c_int,
+                                 C.POINTER(vp)]),
+        "sim_destroy": (C.c_int, [vp]),
+        "step": (C.c_int, [vp, i64, vp]),
+        "simulate": (C.c_int, [vp, i32, vp]),
+        "post_physics": (C.c_int, [vp, i64, vp]),
+        "reset_idx": (C.c_int, [vp, vp, i32, i64, i32, vp]),
+        "set_draws": (C.c_int, [vp, vp]),
+        "actuator_mlp": (C.c_int, [vp, vp, i64, vp, vp, vp]),
+        "actuator_lstm": (C.c_int, [vp, vp, vp, vp, i64, vp, vp]),
+        "mlp_forward": (C.c_int, [vp, vp, i64, i32, C.POINTER(i32), C.POINTER(vp), C.POINTER(vp), i32, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, f"{prefix}_{name}")
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
+            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws",
+            "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward"]
+
+
+def check_layout(sizes_fn):
+    out = (C.c_int64 * 3)()
+    sizes_fn(out)
+    mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers))
+    if tuple(out) != mine:
+        raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)} vs bindings {mine}")

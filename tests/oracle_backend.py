@@ -1,0 +1,134 @@
+"""Test-only backend that runs the CPU oracle (oracle/liblgx_oracle.so) behind the env API.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this module.
+It plugs into `LeggedRobot._make_backend` so that the very same host-side setup (configs,
+asset, reward ordering, buffers, C-ABI structs) drives the oracle on CPU tensors.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import torch
+
+from legged_gym_amd.sim import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liblgx_oracle.so")
+_LIB = None
+
+
+def load_oracle():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    lib = C.CDLL(ORACLE_SO)
+    vp, i64, i32 = C.c_void_p, C.c_int64, C.c_int32
+    M, P, B = C.POINTER(abi.LgxModel), C.POINTER(abi.LgxEnvParams), C.POINTER(abi.LgxBuffers)
+    sigs = {
+        "lgxo_step": (C.c_int, [M, P, B, vp, i64]),
+        "lgxo_post_physics": (C.c_int, [M, P, B, vp, i64]),
+        "lgxo_reset_idx": (C.c_int, [M, P, B, vp, vp, i32, i64, i32]),
+        "lgxo_simulate": (None, [M, P, B, i32]),
+        "lgxo_compute_targets": (None, [M, P, B]),
+        "lgxo_explicit_torques": (None, [P, B]),
+        "lgxo_actuator_mlp": (None, [vp, vp, i64, vp, vp]),
+        "lgxo_actuator_lstm": (None, [vp, vp, vp, vp, i64, vp]),
+        "lgxo_uniform": (C.c_float, [C.c_uint64, i32, i32, i64, C.c_uint32]),
+        "lgxo_struct_sizes": (None, [C.POINTER(C.c_int64)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    abi.check_layout(lib.lgxo_struct_sizes)
+    _LIB = lib
+    return lib
+
+
+def vp(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def uninet_torch_layout(packed_t):
+    """Unpack the kernel's transposed UniNet weights back into torch Linear layout."""
+    w = packed_t.detach().cpu().numpy()
+    dims = [30, 128, 128, 128, 3]
+    out, p = [], 0
+    for l in range(4):
+        n_in, n_out = dims[l], dims[l + 1]
+        wt = w[p:p + n_in * n_out].reshape(n_in, n_out); p += n_in * n_out
+        b = w[p:p + n_out]; p += n_out
+        out += [wt.T.ravel(), b]
+    return torch.tensor(np.concatenate(out).astype(np.float32))
+
+
+class OracleBackend:
+    def __init__(self, env, model, params, bufs):
+        self.lib = load_oracle()
+        self.env = env
+        self.m, self.p, self.b = model, params, bufs
+        self.draws = None
+        self._act_w = None
+        if getattr(env, "actuator_net_weights", None) is not None and params.use_actuator_history:
+            self._act_w = uninet_torch_layout(env.actuator_net_weights)
+
+    def _args(self):
+        return C.byref(self.m), C.byref(self.p), C.byref(self.b)
+
+    def step(self, counter):
+        self.lib.lgxo_step(*self._args(), vp(self.draws), counter)
+        e = self.env
+        if self._act_w is not None:
+            rows = e._model_ins_all.numel() // 30
+            self.lib.lgxo_actuator_mlp(vp(e._model_ins_all), vp(e.actuator_dvel), rows, vp(self._act_w),
+                                       vp(e.actuator_net_scale))
+
+    def simulate(self, n):
+        self.lib.lgxo_simulate(*self._args(), n)
+
+    def post_physics(self, counter):
+        self.lib.lgxo_post_physics(*self._args(), vp(self.draws), counter)
+
+    def reset_idx(self, ids_i32, counter, init_done):
+        ids = ids_i32.cpu().contiguous()
+        self.lib.lgxo_reset_idx(*self._args(), vp(self.draws), vp(ids), ids.numel(), counter, int(init_done))
+
+    def set_draws(self, draws):
+        self.draws = draws
+
+    def close(self):
+        pass
+
+
+def make_env(task, num_envs=8, device="cpu", backend="oracle", overrides=None, seed=1):
+    """Build a registered task with either the oracle (CPU) or the product (GPU) backend."""
+    import legged_gym_amd.envs  # noqa: F401  (registrations)
+    from legged_gym_amd.utils.helpers import get_args
+    from legged_gym_amd.utils.task_registry import task_registry
+
+    env_cfg, _ = task_registry.get_cfgs(task)
+    env_cfg = _fresh_cfg(env_cfg)
+    env_cfg.env.num_envs = num_envs
+    env_cfg.seed = seed
+    if overrides:
+        overrides(env_cfg)
+    args = get_args(["--sim_device", device, "--headless"])
+    cls = task_registry.get_task_class(task)
+    if backend == "oracle":
+        cls = type(cls.__name__ + "Oracle", (cls,), {"_make_backend": lambda self, m, p, b: OracleBackend(self, m, p, b)})
+        task_registry_cls = dict(task_registry.task_classes)
+        task_registry.task_classes[task] = cls
+        try:
+            env, _ = task_registry.make_env(task, args=args, env_cfg=env_cfg)
+        finally:
+            task_registry.task_classes.update(task_registry_cls)
+        return env
+    env, _ = task_registry.make_env(task, args=args, env_cfg=env_cfg)
+    return env
+
+
+def _fresh_cfg(cfg):
+    """Configs are mutable singletons in the registry: build a fresh instance of the same class."""
+    return type(cfg)()
