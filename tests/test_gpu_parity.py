@@ -164,8 +164,9 @@ def test_actuator_mlp_matches_torch_and_oracle(gpu):
     ol = load_oracle()
     oout = torch.empty(rows, 3)
     wt = uninet_torch_layout(w)
+    scale_h = scale.cpu()
     ol.lgxo_actuator_mlp(C.c_void_p(x.data_ptr()), C.c_void_p(oout.data_ptr()), rows, C.c_void_p(wt.data_ptr()),
-                         C.c_void_p(scale.cpu().data_ptr()))
+                         C.c_void_p(scale_h.data_ptr()))
     ok, e = close(out, oout, 1e-4, 1e-4)
     assert ok, f"actuator mlp vs oracle max err {e}"
 
