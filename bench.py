@@ -1,0 +1,160 @@
+"""bench.py — headline measurement: rsl_rl-style PPO training throughput (env-steps/s, whole
+node) for Go1 on rough trimesh terrain with the 187-point height scan, 4096 envs per GPU
+(BASELINE.json metric; workload = configs[2] "C3", which fits one GPU; N>1 = configs[3]).
+
+One "step" = one PPO iteration: 24 x (policy act on the fused MFMA MLP + lgx_step) + GAE +
+5 epochs x 4 minibatches of PPO (autograd, RCCL gradient all-reduce when N>1).
+value = 24 * envs_per_gpu * world * K / max-over-ranks wall time of K iterations.
+
+Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N>1 the driver uses
+torch.distributed.run (one rank per GPU, env vars RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# algorithmic work per env-step: physics kernel = fused 4 substeps (VALU),
+# actuator MLP = 4 substeps x 4 legs x 2 x (30*128 + 128*128*2 + 128*3) FLOP
+ACT_MLP_FLOP_PER_ENV_STEP = 4 * 4 * 2 * (30 * 128 + 128 * 128 * 2 + 128 * 3)
+MI355X_F32_MFMA_PEAK_TFLOPS = 157.3
+MI355X_HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--task", default="go1_rough")
+    p.add_argument("--num_envs", type=int, default=4096)
+    p.add_argument("--no_cpu_baseline", action="store_true")
+    p.add_argument("--cpu_envs", type=int, default=256)
+    return p.parse_args()
+
+
+def mlp_flop_per_sample(dims):
+    return 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+
+
+def cpu_baseline(task, n_envs):
+    """Oracle env (C restatement, OpenMP over envs) + torch-CPU PPO, one PPO iteration."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    from oracle_backend import make_env
+    from legged_gym_amd.rl.runner import OnPolicyRunner
+    from legged_gym_amd.utils.helpers import class_to_dict
+    from legged_gym_amd.utils.task_registry import task_registry
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    env = make_env(task, num_envs=n_envs, device="cpu", backend="oracle")
+    _, train_cfg = task_registry.get_cfgs(task)
+    runner = OnPolicyRunner(env, class_to_dict(type(train_cfg)()), None, device="cpu")
+    runner.learn(1)  # warm
+    t0 = time.time()
+    runner.learn(1)
+    dt = time.time() - t0
+    steps = runner.num_steps_per_env * n_envs
+    return dict(value=steps / dt, unit="env-steps/s", cores=threads, kind="port",
+                sample=f"1 PPO iteration ({runner.num_steps_per_env} steps x {n_envs} envs, {task}) of the C oracle "
+                       f"env (OpenMP {threads} threads) + torch-CPU ActorCritic/PPO; {dt:.1f}s")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    device = f"cuda:{local}"
+    import legged_gym_amd.envs  # noqa: F401
+    from legged_gym_amd.sim import lib as lgxlib
+    from legged_gym_amd.utils.helpers import get_args
+    from legged_gym_amd.utils.task_registry import task_registry
+
+    env_cfg, train_cfg = task_registry.get_cfgs(args.task)
+    env_cfg = type(env_cfg)()
+    train_cfg = type(train_cfg)()
+    env_cfg.env.num_envs = args.num_envs
+    env_cfg.seed = 1 + rank
+    train_cfg.seed = 1 + rank
+    cli = get_args(["--sim_device", device, "--rl_device", device, "--headless", "--task", args.task])
+    env, _ = task_registry.make_env(args.task, args=cli, env_cfg=env_cfg)
+    runner, _ = task_registry.make_alg_runner(env, name=args.task, args=cli, train_cfg=train_cfg, log_root=None)
+    lib = lgxlib.load()
+    handle = env._backend.handle
+
+    runner.learn(args.warmup)
+    lib.lgx_profile_enable(handle, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.learn(args.steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    lib.lgx_profile_enable(handle, 0)
+    ms = (C.c_double * 3)()
+    cnt = (C.c_int64 * 3)()
+    lgxlib.check(lib.lgx_profile_collect(handle, ms, cnt), "lgx_profile_collect")
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    N = args.num_envs
+    steps_per_iter = runner.num_steps_per_env
+    value = steps_per_iter * N * world * args.steps / elapsed
+
+    # roofline of the dominant lgx kernel class (HIP-event durations over the timed region)
+    names = ["lgx_physics_kernel", "lgx_mlp_forward_kernel(actuator)", "lgx_post_physics_kernel"]
+    avg = [ms[i] / cnt[i] if cnt[i] else 0.0 for i in range(3)]
+    dom = max(range(3), key=lambda i: ms[i])
+    act_avg_ms = avg[1]
+    act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
+    roof = {"kernel": names[1], "bound": "mfma",
+            "achieved": (act_flop / (act_avg_ms * 1e-3) / 1e12) if act_avg_ms else None,
+            "peak": MI355X_F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
+            "note": ("actuator-net MLP (f32 MFMA) launch; dominant lgx kernel class by time is "
+                     f"{names[dom]} ({avg[dom]:.3f} ms/launch, VALU-bound physics, see DESIGN.md §5)")}
+    if roof["achieved"] is not None:
+        roof["frac"] = roof["achieved"] / roof["peak"]
+    it_ms = 1000.0 * elapsed / args.steps
+    kernels = {n: {"avg_ms": round(a, 4), "launches": int(c), "share_of_iteration": round(m / args.steps / it_ms, 4)}
+               for n, a, c, m in zip(names, avg, cnt, ms)}
+    out = {
+        "metric": "env-steps/sec (whole node), Go1 rough-terrain 4096 envs/GPU",
+        "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": it_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic (procedural curriculum terrain, random-init policy)",
+        "config": {"workload": f"C3 {args.task}: Go1 trimesh curriculum terrain + 187-point height scan, "
+                               f"actuator-net history+MLP, PPO 24 steps x {N} envs/GPU, 5 epochs x 4 minibatches",
+                   "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "lgx_kernels": kernels,
+        "last_iteration": runner.last_iteration_stats,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.task, args.cpu_envs)
+        except Exception as e:  # reported, never silently replaced
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

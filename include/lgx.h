@@ -250,6 +250,20 @@ int lgx_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m,
 int lgx_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
                     const float* const* weights, const float* const* biases, int32_t act, void* stream);
 
+/* In-library kernel timing for the measurement harness (bench.py): when enabled, every
+ * lgx_step records hipEvents on the launch stream around each kernel class
+ * (0 physics, 1 actuator MLP, 2 post-physics incl. extras finalize).  lgx_profile_collect
+ * synchronises those events (call it OUTSIDE timed regions), writes per class the summed
+ * milliseconds and launch count to ms[3] / count[3], and clears the record. */
+int lgx_profile_enable(lgx_sim* sim, int32_t on);
+int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
+
+/* Generalised advantage estimation (rsl_rl RolloutStorage.compute_returns, before the
+ * advantage normalisation): rewards/values/dones [T,N] (dones uint8), last_values [N] ->
+ * returns, advantages (= returns - values) [T,N]. */
+int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_values, float* returns,
+            float* advantages, int32_t T, int32_t N, float gamma, float lam, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

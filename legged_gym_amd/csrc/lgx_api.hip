@@ -6,6 +6,7 @@
 
 #include <new>
 #include <string>
+#include <vector>
 
 #include "lgx_internal.h"
 
@@ -36,7 +37,24 @@ struct lgx_sim {
   lgx_env_params* d_params;
   const float* draws;
   int32_t n_term_rows;
+  bool profiling;
+  std::vector<hipEvent_t> ev[3];  // (start, stop) pairs per kernel class
+  std::vector<hipEvent_t> pool;
 };
+
+static hipEvent_t take_event(lgx_sim* s) {
+  if (!s->pool.empty()) { hipEvent_t e = s->pool.back(); s->pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+static void mark(lgx_sim* s, int cls, hipStream_t st) {
+  if (!s->profiling) return;
+  hipEvent_t e = take_event(s);
+  if (!e) return;
+  (void)hipEventRecord(e, st);
+  s->ev[cls].push_back(e);
+}
 
 extern "C" {
 
@@ -116,6 +134,7 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   s->params = *params;
   s->bufs = *bufs;
   s->draws = nullptr;
+  s->profiling = false;
   s->n_term_rows = params->num_terms + (params->termination_slot >= 0 ? 1 : 0);
   if ((rc = hip_check(hipMalloc(&s->d_model, sizeof(lgx_dev_model)), "hipMalloc(model)"))) { delete s; return rc; }
   if ((rc = hip_check(hipMalloc(&s->d_params, sizeof(lgx_env_params)), "hipMalloc(params)"))) {
@@ -130,6 +149,8 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
 
 int lgx_sim_destroy(lgx_sim* s) {
   if (!s) return 0;
+  for (auto& v : s->ev) for (hipEvent_t e : v) (void)hipEventDestroy(e);
+  for (hipEvent_t e : s->pool) (void)hipEventDestroy(e);
   (void)hipFree(s->d_model);
   (void)hipFree(s->d_params);
   delete s;
@@ -163,17 +184,53 @@ int lgx_step(lgx_sim* s, int64_t step, void* stream) {
   int rc = launch_check(lgx_launch_clip_actions(s->bufs.actions, (int64_t)p.num_envs * 12, p.clip_actions, st),
                         "lgx_step: clip launch");
   if (rc) return rc;
+  mark(s, 0, st);
   rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, st),
                     "lgx_step: physics launch");
+  mark(s, 0, st);
   if (rc) return rc;
   if (p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel) {
     // UniNet on every (substep, env, leg) row of this step's model_ins; result = dVel
+    mark(s, 1, st);
     rc = launch_check(lgx_launch_actuator_mlp(s->bufs.model_ins, s->bufs.act_dvel, (int64_t)p.decimation * p.num_envs * 4,
                                               s->bufs.act_net_w, s->bufs.act_net_scale, st),
                       "lgx_step: actuator mlp launch");
+    mark(s, 1, st);
     if (rc) return rc;
   }
-  return lgx_post_physics(s, step, stream);
+  mark(s, 2, st);
+  rc = lgx_post_physics(s, step, stream);
+  mark(s, 2, st);
+  return rc;
+}
+
+int lgx_profile_enable(lgx_sim* s, int32_t on) {
+  if (!s) return fail(LGX_EINVAL, "lgx_profile_enable: null sim");
+  s->profiling = on != 0;
+  return 0;
+}
+
+int lgx_profile_collect(lgx_sim* s, double* ms, int64_t* count) {
+  if (!s || !ms || !count) return fail(LGX_EINVAL, "lgx_profile_collect: null argument");
+  for (int c = 0; c < 3; ++c) {
+    double tot = 0.0;
+    int64_t n = 0;
+    auto& v = s->ev[c];
+    for (size_t i = 0; i + 1 < v.size(); i += 2) {
+      int rc = hip_check(hipEventSynchronize(v[i + 1]), "hipEventSynchronize");
+      if (rc) return rc;
+      float t = 0.f;
+      rc = hip_check(hipEventElapsedTime(&t, v[i], v[i + 1]), "hipEventElapsedTime");
+      if (rc) return rc;
+      tot += t;
+      ++n;
+    }
+    for (hipEvent_t e : v) s->pool.push_back(e);
+    v.clear();
+    ms[c] = tot;
+    count[c] = n;
+  }
+  return 0;
 }
 
 int lgx_reset_idx(lgx_sim* s, const int32_t* env_ids, int32_t n, int64_t step, int32_t init_done, void* stream) {
@@ -199,6 +256,15 @@ int lgx_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const in
   if (!x || !y || !dims || !weights || !biases || rows < 0) return fail(LGX_EINVAL, "lgx_mlp_forward: bad arguments");
   return launch_check(lgx_launch_mlp_forward(x, y, rows, nl, dims, weights, biases, act, (hipStream_t)stream),
                       "lgx_mlp_forward: launch (widths must be 1..512, layers 1..6)");
+}
+
+int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_values, float* returns,
+            float* advantages, int32_t T, int32_t N, float gamma, float lam, void* stream) {
+  if (!rewards || !values || !dones || !last_values || !returns || !advantages)
+    return fail(LGX_EINVAL, "lgx_gae: null argument");
+  return launch_check(lgx_launch_gae(rewards, values, dones, last_values, returns, advantages, T, N, gamma, lam,
+                                     (hipStream_t)stream),
+                      "lgx_gae: launch (T, N must be > 0)");
 }
 
 }  // extern "C"

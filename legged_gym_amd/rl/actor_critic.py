@@ -1,0 +1,143 @@
+"""rsl_rl-compatible ActorCritic (the policy the reference trains: legged_robot_config.py:216-224,
+built by OnPolicyRunner at task_registry.py:160; upstream rsl_rl v1.0.x `ActorCritic`).
+
+Training forward/backward uses torch autograd (library GEMMs).  The no-grad rollout forward
+(`act` under inference mode, `act_inference`, `evaluate`) runs on the lgx fused MLP kernel
+(f32 MFMA, all layers in one launch with the activations resident in LDS) when the module
+lives on a GPU; weights are re-transposed for the kernel lazily after each optimizer step.
+"""
+import ctypes as C
+
+import torch
+import torch.nn as nn
+from torch.distributions import Normal
+
+
+def get_activation(name):
+    table = {"elu": nn.ELU(), "selu": nn.SELU(), "relu": nn.ReLU(), "crelu": nn.ReLU(), "lrelu": nn.LeakyReLU(),
+             "tanh": nn.Tanh(), "sigmoid": nn.Sigmoid()}
+    if name not in table:
+        print("invalid activation function!")
+        return None
+    return table[name]
+
+
+def _mlp(n_in, hidden, n_out, act):
+    layers = [nn.Linear(n_in, hidden[0]), act]
+    for i in range(len(hidden)):
+        if i == len(hidden) - 1:
+            layers.append(nn.Linear(hidden[i], n_out))
+        else:
+            layers += [nn.Linear(hidden[i], hidden[i + 1]), act]
+    return nn.Sequential(*layers)
+
+
+class _FusedMLP:
+    """Inference-only view of an nn.Sequential(Linear, act, ..., Linear) on lgx_mlp_forward."""
+
+    ACT = {nn.ELU: 1, nn.Tanh: 2}
+
+    def __init__(self, seq):
+        self.linears = [m for m in seq if isinstance(m, nn.Linear)]
+        acts = {type(m) for m in seq if not isinstance(m, nn.Linear)}
+        self.act = self.ACT.get(next(iter(acts)), 0) if len(acts) == 1 else 0
+        self.dims = [self.linears[0].in_features] + [l.out_features for l in self.linears]
+        self.ok = self.act != 0 and max(self.dims) <= 512 and len(self.linears) <= 6
+        self._ver = None
+        self._wt = self._b = None
+
+    def _refresh(self):
+        ver = tuple(l.weight._version for l in self.linears) + tuple(l.bias._version for l in self.linears)
+        if ver != self._ver or self._wt is None or self._wt[0].device != self.linears[0].weight.device:
+            with torch.no_grad():
+                self._wt = [l.weight.detach().t().contiguous() for l in self.linears]
+                self._b = [l.bias.detach().contiguous() for l in self.linears]
+            self._ver = ver
+            n = len(self.linears)
+            self._dims_c = (C.c_int32 * (n + 1))(*self.dims)
+            self._wp = (C.c_void_p * n)(*[t.data_ptr() for t in self._wt])
+            self._bp = (C.c_void_p * n)(*[t.data_ptr() for t in self._b])
+
+    def __call__(self, x):
+        from legged_gym_amd.sim import lib as lgxlib
+        lib = lgxlib.load()
+        self._refresh()
+        x = x.contiguous()
+        y = torch.empty(x.shape[0], self.dims[-1], device=x.device, dtype=torch.float)
+        stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
+        lgxlib.check(lib.lgx_mlp_forward(C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), x.shape[0],
+                                         len(self.linears), self._dims_c, self._wp, self._bp, self.act, stream),
+                     "lgx_mlp_forward")
+        return y
+
+
+class ActorCritic(nn.Module):
+    is_recurrent = False
+
+    def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=(256, 256, 256),
+                 critic_hidden_dims=(256, 256, 256), activation="elu", init_noise_std=1.0, **kwargs):
+        if kwargs:
+            print("ActorCritic.__init__ got unexpected arguments, which will be ignored: " + str(list(kwargs.keys())))
+        super().__init__()
+        act = get_activation(activation)
+        self.actor = _mlp(num_actor_obs, list(actor_hidden_dims), num_actions, act)
+        self.critic = _mlp(num_critic_obs, list(critic_hidden_dims), 1, act)
+        print(f"Actor MLP: {self.actor}")
+        print(f"Critic MLP: {self.critic}")
+        self.std = nn.Parameter(init_noise_std * torch.ones(num_actions))
+        self.distribution = None
+        Normal.set_default_validate_args(False)
+        self._fused_actor = _FusedMLP(self.actor)
+        self._fused_critic = _FusedMLP(self.critic)
+        self.use_fused_inference = True
+
+    @staticmethod
+    def init_weights(sequential, scales):
+        [torch.nn.init.orthogonal_(module.weight, gain=scales[idx]) for idx, module in
+         enumerate(mod for mod in sequential if isinstance(mod, nn.Linear))]
+
+    def reset(self, dones=None):
+        pass
+
+    def forward(self):
+        raise NotImplementedError
+
+    @property
+    def action_mean(self):
+        return self.distribution.mean
+
+    @property
+    def action_std(self):
+        return self.distribution.stddev
+
+    @property
+    def entropy(self):
+        return self.distribution.entropy().sum(dim=-1)
+
+    def _fused_ok(self, x, fused):
+        return (self.use_fused_inference and fused.ok and x.is_cuda and
+                (torch.is_inference_mode_enabled() or not torch.is_grad_enabled()))
+
+    def _actor_mean(self, observations):
+        if self._fused_ok(observations, self._fused_actor):
+            return self._fused_actor(observations)
+        return self.actor(observations)
+
+    def update_distribution(self, observations):
+        mean = self._actor_mean(observations)
+        self.distribution = Normal(mean, mean * 0.0 + self.std)
+
+    def act(self, observations, **kwargs):
+        self.update_distribution(observations)
+        return self.distribution.sample()
+
+    def get_actions_log_prob(self, actions):
+        return self.distribution.log_prob(actions).sum(dim=-1)
+
+    def act_inference(self, observations):
+        return self._actor_mean(observations)
+
+    def evaluate(self, critic_observations, **kwargs):
+        if self._fused_ok(critic_observations, self._fused_critic):
+            return self._fused_critic(critic_observations)
+        return self.critic(critic_observations)

@@ -1,0 +1,20 @@
+"""Python shims over the PPO-side HIP kernels of liblgx.so (no fallback on GPU tensors)."""
+import ctypes as C
+
+import torch
+
+
+def _vp(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def gae(rewards, values, dones, last_values, returns, advantages, gamma, lam):
+    """rewards/values/returns/advantages [T,N,1] f32, dones [T,N,1] uint8, last_values [N,1]."""
+    from legged_gym_amd.sim import lib as lgxlib
+    lib = lgxlib.load()
+    T, N = rewards.shape[0], rewards.shape[1]
+    for t in (rewards, values, dones, returns, advantages, last_values):
+        assert t.is_cuda and t.is_contiguous()
+    stream = C.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+    lgxlib.check(lib.lgx_gae(_vp(rewards), _vp(values), _vp(dones), _vp(last_values), _vp(returns), _vp(advantages),
+                             T, N, float(gamma), float(lam), stream), "lgx_gae")

@@ -1,0 +1,166 @@
+"""PPO with the rsl_rl v1.0.x algorithm and hyper-parameter contract
+(legged_robot_config.py:226-239; upstream rsl_rl `PPO`), data-parallel over ranks.
+
+Data parallelism (new; the reference is single-GPU): every rank owns its envs and a full
+ActorCritic replica.  Per minibatch the flat fp32 gradient is all-reduced (RCCL over xGMI when
+the process group backend is "nccl") and averaged before clip_grad_norm, advantage
+normalisation uses global statistics, and the KL used by the adaptive learning rate is the
+global mean, so every rank applies the identical Adam step and N ranks x B envs reproduce
+1 rank x N*B envs up to reduction order.
+"""
+import torch
+import torch.nn as nn
+import torch.optim as optim
+
+from .actor_critic import ActorCritic
+from .storage import RolloutStorage
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 else None
+
+
+class PPO:
+    actor_critic: ActorCritic
+
+    def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998, lam=0.95,
+                 value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
+                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu"):
+        self.device = device
+        self.desired_kl = desired_kl
+        self.schedule = schedule
+        self.learning_rate = learning_rate
+        self.actor_critic = actor_critic.to(self.device)
+        self.storage = None
+        fused = str(device).startswith("cuda")
+        self.optimizer = optim.Adam(self.actor_critic.parameters(), lr=learning_rate, fused=fused or None)
+        self.transition = RolloutStorage.Transition()
+        self.clip_param = clip_param
+        self.num_learning_epochs = num_learning_epochs
+        self.num_mini_batches = num_mini_batches
+        self.value_loss_coef = value_loss_coef
+        self.entropy_coef = entropy_coef
+        self.gamma = gamma
+        self.lam = lam
+        self.max_grad_norm = max_grad_norm
+        self.use_clipped_value_loss = use_clipped_value_loss
+        self.dist = _dist()
+        if self.dist is not None:
+            self._broadcast_params()
+
+    # ---------------------------------------------------------------- setup / modes
+    def init_storage(self, num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape, action_shape):
+        self.storage = RolloutStorage(num_envs, num_transitions_per_env, actor_obs_shape, critic_obs_shape,
+                                      action_shape, self.device)
+
+    def test_mode(self):
+        self.actor_critic.test()
+
+    def train_mode(self):
+        self.actor_critic.train()
+
+    def _broadcast_params(self):
+        with torch.no_grad():
+            for p in self.actor_critic.parameters():
+                self.dist.broadcast(p.data, src=0)
+
+    # ---------------------------------------------------------------- rollout
+    def act(self, obs, critic_obs):
+        t = self.transition
+        t.actions = self.actor_critic.act(obs).detach()
+        t.values = self.actor_critic.evaluate(critic_obs).detach()
+        t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
+        t.action_mean = self.actor_critic.action_mean.detach()
+        t.action_sigma = self.actor_critic.action_std.detach()
+        t.observations = obs
+        t.critic_observations = critic_obs
+        return t.actions
+
+    def process_env_step(self, rewards, dones, infos):
+        t = self.transition
+        t.rewards = rewards.clone()
+        t.dones = dones
+        if "time_outs" in infos:  # bootstrap on time-outs
+            t.rewards += self.gamma * torch.squeeze(t.values * infos["time_outs"].unsqueeze(1).to(self.device), 1)
+        self.storage.add_transitions(t)
+        t.clear()
+        self.actor_critic.reset(dones)
+
+    def _adv_stats(self, adv):
+        if self.dist is None:
+            return adv.mean(), adv.std()
+        s = torch.stack([adv.sum(), (adv * adv).sum(), torch.tensor(float(adv.numel()), device=adv.device)])
+        self.dist.all_reduce(s)
+        n = s[2]
+        mean = s[0] / n
+        var = (s[1] - n * mean * mean) / (n - 1)
+        return mean, var.clamp(min=0).sqrt()
+
+    def compute_returns(self, last_critic_obs):
+        last_values = self.actor_critic.evaluate(last_critic_obs).detach()
+        self.storage.compute_returns(last_values, self.gamma, self.lam, reduce_stats=self._adv_stats)
+
+    # ---------------------------------------------------------------- update
+    def _allreduce_grads(self):
+        params = [p for p in self.actor_critic.parameters() if p.grad is not None]
+        flat = torch.cat([p.grad.reshape(-1) for p in params])
+        self.dist.all_reduce(flat)
+        flat /= self.dist.get_world_size()
+        off = 0
+        for p in params:
+            n = p.grad.numel()
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+            off += n
+
+    def update(self):
+        mean_value_loss = 0.0
+        mean_surrogate_loss = 0.0
+        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        for (obs_b, cobs_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b, old_sigma_b, _hid, _mask) in gen:
+            self.actor_critic.act(obs_b)
+            logp_b = self.actor_critic.get_actions_log_prob(act_b)
+            value_b = self.actor_critic.evaluate(cobs_b)
+            mu_b = self.actor_critic.action_mean
+            sigma_b = self.actor_critic.action_std
+            entropy_b = self.actor_critic.entropy
+            if self.desired_kl is not None and self.schedule == "adaptive":
+                with torch.inference_mode():
+                    kl = torch.sum(torch.log(sigma_b / old_sigma_b + 1.e-5) +
+                                   (torch.square(old_sigma_b) + torch.square(old_mu_b - mu_b)) /
+                                   (2.0 * torch.square(sigma_b)) - 0.5, axis=-1)
+                    kl_mean = torch.mean(kl)
+                    if self.dist is not None:
+                        self.dist.all_reduce(kl_mean)
+                        kl_mean /= self.dist.get_world_size()
+                    kl_mean = kl_mean.item()
+                    if kl_mean > self.desired_kl * 2.0:
+                        self.learning_rate = max(1e-5, self.learning_rate / 1.5)
+                    elif self.desired_kl / 2.0 > kl_mean > 0.0:
+                        self.learning_rate = min(1e-2, self.learning_rate * 1.5)
+                    for g in self.optimizer.param_groups:
+                        g["lr"] = self.learning_rate
+            ratio = torch.exp(logp_b - torch.squeeze(old_logp_b))
+            adv = torch.squeeze(adv_b)
+            surrogate = -adv * ratio
+            surrogate_clipped = -adv * torch.clamp(ratio, 1.0 - self.clip_param, 1.0 + self.clip_param)
+            surrogate_loss = torch.max(surrogate, surrogate_clipped).mean()
+            if self.use_clipped_value_loss:
+                value_clipped = target_v_b + (value_b - target_v_b).clamp(-self.clip_param, self.clip_param)
+                value_loss = torch.max((value_b - ret_b).pow(2), (value_clipped - ret_b).pow(2)).mean()
+            else:
+                value_loss = (ret_b - value_b).pow(2).mean()
+            loss = surrogate_loss + self.value_loss_coef * value_loss - self.entropy_coef * entropy_b.mean()
+            self.optimizer.zero_grad()
+            loss.backward()
+            if self.dist is not None:
+                self._allreduce_grads()
+            nn.utils.clip_grad_norm_(self.actor_critic.parameters(), self.max_grad_norm)
+            self.optimizer.step()
+            mean_value_loss += value_loss.detach()
+            mean_surrogate_loss += surrogate_loss.detach()
+        n = self.num_learning_epochs * self.num_mini_batches
+        mean_value_loss = (mean_value_loss / n).item()
+        mean_surrogate_loss = (mean_surrogate_loss / n).item()
+        self.storage.clear()
+        return mean_value_loss, mean_surrogate_loss

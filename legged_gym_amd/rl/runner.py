@@ -1,0 +1,164 @@
+"""OnPolicyRunner with the rsl_rl v1.0.x contract consumed by the reference
+(task_registry.py:159-167, train.py:43, play.py:65-71): `OnPolicyRunner(env, train_cfg_dict,
+log_dir, device)`, `learn(num_learning_iterations, init_at_random_ep_len)`, `save`, `load`,
+`get_inference_policy`, `alg.actor_critic`; checkpoint dict {model_state_dict,
+optimizer_state_dict, iter, infos} saved every `save_interval` iterations as model_<it>.pt.
+
+Timing: `collection_time` (act + env.step + storage) and `learn_time` (GAE + update) per
+iteration, fps = num_steps_per_env * num_envs / (collection + learn), as rsl_rl logs it;
+`last_iteration_stats` keeps them for bench.py.
+"""
+import os
+import statistics
+import time
+from collections import deque
+
+import torch
+
+from .actor_critic import ActorCritic  # noqa: F401  (resolved by name from the cfg)
+from .ppo import PPO  # noqa: F401
+
+
+class OnPolicyRunner:
+    def __init__(self, env, train_cfg, log_dir=None, device="cpu"):
+        self.cfg = train_cfg["runner"]
+        self.alg_cfg = train_cfg["algorithm"]
+        self.policy_cfg = train_cfg["policy"]
+        self.device = device
+        self.env = env
+        num_critic_obs = self.env.num_privileged_obs if self.env.num_privileged_obs is not None else self.env.num_obs
+        ac_class = {"ActorCritic": ActorCritic}[self.cfg["policy_class_name"]]
+        actor_critic = ac_class(self.env.num_obs, num_critic_obs, self.env.num_actions, **self.policy_cfg).to(self.device)
+        alg_class = {"PPO": PPO}[self.cfg["algorithm_class_name"]]
+        self.alg = alg_class(actor_critic, device=self.device, **self.alg_cfg)
+        self.num_steps_per_env = self.cfg["num_steps_per_env"]
+        self.save_interval = self.cfg["save_interval"]
+        self.alg.init_storage(self.env.num_envs, self.num_steps_per_env, [self.env.num_obs],
+                              [self.env.num_privileged_obs], [self.env.num_actions])
+        self.log_dir = log_dir
+        self.writer = None
+        self.tot_timesteps = 0
+        self.tot_time = 0
+        self.current_learning_iteration = 0
+        self.last_iteration_stats = {}
+        _, _ = self.env.reset()
+
+    def _writer(self):
+        if self.writer is None and self.log_dir is not None:
+            try:
+                from torch.utils.tensorboard import SummaryWriter
+                self.writer = SummaryWriter(log_dir=self.log_dir, flush_secs=10)
+            except Exception:
+                self.writer = False
+        return self.writer or None
+
+    def learn(self, num_learning_iterations, init_at_random_ep_len=False):
+        if init_at_random_ep_len:
+            self.env.episode_length_buf = torch.randint_like(self.env.episode_length_buf,
+                                                             high=int(self.env.max_episode_length))
+        obs = self.env.get_observations()
+        privileged_obs = self.env.get_privileged_observations()
+        critic_obs = privileged_obs if privileged_obs is not None else obs
+        obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
+        self.alg.actor_critic.train()
+        ep_infos = []
+        rewbuffer = deque(maxlen=100)
+        lenbuffer = deque(maxlen=100)
+        cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
+        sync = torch.cuda.synchronize if str(self.device).startswith("cuda") else (lambda: None)
+        tot_iter = self.current_learning_iteration + num_learning_iterations
+        for it in range(self.current_learning_iteration, tot_iter):
+            start = time.time()
+            with torch.inference_mode():
+                for _ in range(self.num_steps_per_env):
+                    actions = self.alg.act(obs, critic_obs)
+                    obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
+                    critic_obs = privileged_obs if privileged_obs is not None else obs
+                    obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
+                    rewards, dones = rewards.to(self.device), dones.to(self.device)
+                    self.alg.process_env_step(rewards, dones, infos)
+                    if self.log_dir is not None:
+                        if "episode" in infos:
+                            ep_infos.append(infos["episode"])
+                        cur_reward_sum += rewards
+                        cur_episode_length += 1
+                        new_ids = (dones > 0).nonzero(as_tuple=False)
+                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
+                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
+                        cur_reward_sum[new_ids] = 0
+                        cur_episode_length[new_ids] = 0
+                sync()
+                stop = time.time()
+                collection_time = stop - start
+                start = stop
+                self.alg.compute_returns(critic_obs)
+            mean_value_loss, mean_surrogate_loss = self.alg.update()
+            sync()
+            stop = time.time()
+            learn_time = stop - start
+            self.last_iteration_stats = dict(collection_time=collection_time, learn_time=learn_time,
+                                             value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
+                                             learning_rate=self.alg.learning_rate)
+            if self.log_dir is not None:
+                self.log(locals())
+                if it % self.save_interval == 0:
+                    self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
+            ep_infos.clear()
+        self.current_learning_iteration += num_learning_iterations
+        if self.log_dir is not None:
+            self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))
+
+    def log(self, locs, width=80, pad=35):
+        self.tot_timesteps += self.num_steps_per_env * self.env.num_envs
+        self.tot_time += locs["collection_time"] + locs["learn_time"]
+        it_time = locs["collection_time"] + locs["learn_time"]
+        w = self._writer()
+        lines = []
+        if locs["ep_infos"]:
+            for key in locs["ep_infos"][0]:
+                vals = torch.stack([torch.as_tensor(ep[key], device=self.device).reshape(()) for ep in locs["ep_infos"]])
+                value = vals.mean().item()
+                if w:
+                    w.add_scalar("Episode/" + key, value, locs["it"])
+                lines.append(f"{'Mean episode ' + key + ':':>{pad}} {value:.4f}")
+        fps = int(self.num_steps_per_env * self.env.num_envs / it_time)
+        if w:
+            w.add_scalar("Loss/value_function", locs["mean_value_loss"], locs["it"])
+            w.add_scalar("Loss/surrogate", locs["mean_surrogate_loss"], locs["it"])
+            w.add_scalar("Loss/learning_rate", self.alg.learning_rate, locs["it"])
+            w.add_scalar("Policy/mean_noise_std", self.alg.actor_critic.std.mean().item(), locs["it"])
+            w.add_scalar("Perf/total_fps", fps, locs["it"])
+            w.add_scalar("Perf/collection time", locs["collection_time"], locs["it"])
+            w.add_scalar("Perf/learning_time", locs["learn_time"], locs["it"])
+        header = f" \033[1m Learning iteration {locs['it']}/{self.current_learning_iteration + locs['num_learning_iterations']} \033[0m "
+        s = f"{'#' * width}\n{header.center(width, ' ')}\n\n"
+        s += f"{'Computation:':>{pad}} {fps:.0f} steps/s (collection: {locs['collection_time']:.3f}s, learning {locs['learn_time']:.3f}s)\n"
+        s += f"{'Value function loss:':>{pad}} {locs['mean_value_loss']:.4f}\n"
+        s += f"{'Surrogate loss:':>{pad}} {locs['mean_surrogate_loss']:.4f}\n"
+        s += f"{'Mean action noise std:':>{pad}} {self.alg.actor_critic.std.mean().item():.2f}\n"
+        if len(locs["rewbuffer"]) > 0:
+            s += f"{'Mean reward:':>{pad}} {statistics.mean(locs['rewbuffer']):.2f}\n"
+            s += f"{'Mean episode length:':>{pad}} {statistics.mean(locs['lenbuffer']):.2f}\n"
+        s += "\n".join(lines) + "\n" + "-" * width + "\n"
+        s += f"{'Total timesteps:':>{pad}} {self.tot_timesteps}\n{'Iteration time:':>{pad}} {it_time:.2f}s\n"
+        print(s)
+
+    def save(self, path, infos=None):
+        torch.save({"model_state_dict": self.alg.actor_critic.state_dict(),
+                    "optimizer_state_dict": self.alg.optimizer.state_dict(),
+                    "iter": self.current_learning_iteration, "infos": infos}, path)
+
+    def load(self, path, load_optimizer=True):
+        d = torch.load(path, map_location=self.device, weights_only=True)
+        self.alg.actor_critic.load_state_dict(d["model_state_dict"])
+        if load_optimizer:
+            self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
+        self.current_learning_iteration = d["iter"]
+        return d["infos"]
+
+    def get_inference_policy(self, device=None):
+        self.alg.actor_critic.eval()
+        if device is not None:
+            self.alg.actor_critic.to(device)
+        return self.alg.actor_critic.act_inference

@@ -1,0 +1,117 @@
+"""Rollout storage with the rsl_rl RolloutStorage contract (transitions, GAE, minibatches).
+
+GAE (rsl_rl compute_returns: gamma/lam recursion with done masking, then advantage
+normalisation) runs as ONE HIP kernel (lgx GAE, one thread per env over the T steps) on the
+GPU; the normalisation statistics are optionally all-reduced across ranks so that N ranks x B
+envs normalise exactly like 1 rank x N*B envs.
+"""
+import torch
+
+
+class RolloutStorage:
+    class Transition:
+        def __init__(self):
+            self.observations = None
+            self.critic_observations = None
+            self.actions = None
+            self.rewards = None
+            self.dones = None
+            self.values = None
+            self.actions_log_prob = None
+            self.action_mean = None
+            self.action_sigma = None
+            self.hidden_states = None
+
+        def clear(self):
+            self.__init__()
+
+    def __init__(self, num_envs, num_transitions_per_env, obs_shape, privileged_obs_shape, actions_shape,
+                 device="cpu"):
+        self.device = device
+        self.obs_shape = obs_shape
+        self.privileged_obs_shape = privileged_obs_shape
+        self.actions_shape = actions_shape
+        T, N = num_transitions_per_env, num_envs
+        f = dict(device=device)
+        self.observations = torch.zeros(T, N, *obs_shape, **f)
+        self.privileged_observations = (torch.zeros(T, N, *privileged_obs_shape, **f)
+                                        if privileged_obs_shape[0] is not None else None)
+        self.rewards = torch.zeros(T, N, 1, **f)
+        self.actions = torch.zeros(T, N, *actions_shape, **f)
+        self.dones = torch.zeros(T, N, 1, **f).byte()
+        self.actions_log_prob = torch.zeros(T, N, 1, **f)
+        self.values = torch.zeros(T, N, 1, **f)
+        self.returns = torch.zeros(T, N, 1, **f)
+        self.advantages = torch.zeros(T, N, 1, **f)
+        self.mu = torch.zeros(T, N, *actions_shape, **f)
+        self.sigma = torch.zeros(T, N, *actions_shape, **f)
+        self.num_transitions_per_env = T
+        self.num_envs = N
+        self.step = 0
+
+    def add_transitions(self, t: "RolloutStorage.Transition"):
+        if self.step >= self.num_transitions_per_env:
+            raise AssertionError("Rollout buffer overflow")
+        s = self.step
+        self.observations[s].copy_(t.observations)
+        if self.privileged_observations is not None:
+            self.privileged_observations[s].copy_(t.critic_observations)
+        self.actions[s].copy_(t.actions)
+        self.rewards[s].copy_(t.rewards.view(-1, 1))
+        self.dones[s].copy_(t.dones.view(-1, 1))
+        self.values[s].copy_(t.values)
+        self.actions_log_prob[s].copy_(t.actions_log_prob.view(-1, 1))
+        self.mu[s].copy_(t.action_mean)
+        self.sigma[s].copy_(t.action_sigma)
+        self.step += 1
+
+    def clear(self):
+        self.step = 0
+
+    def compute_returns(self, last_values, gamma, lam, reduce_stats=None):
+        """rsl_rl RolloutStorage.compute_returns (+ optional cross-rank statistics)."""
+        if self.returns.is_cuda:
+            from legged_gym_amd.rl import fused
+            fused.gae(self.rewards, self.values, self.dones, last_values, self.returns, self.advantages, gamma, lam)
+        else:
+            advantage = 0
+            for step in reversed(range(self.num_transitions_per_env)):
+                next_values = last_values if step == self.num_transitions_per_env - 1 else self.values[step + 1]
+                not_term = 1.0 - self.dones[step].float()
+                delta = self.rewards[step] + not_term * gamma * next_values - self.values[step]
+                advantage = delta + not_term * gamma * lam * advantage
+                self.returns[step] = advantage + self.values[step]
+            self.advantages = self.returns - self.values
+        adv = self.advantages
+        if reduce_stats is None:
+            mean, std = adv.mean(), adv.std()
+        else:
+            mean, std = reduce_stats(adv)
+        self.advantages = (adv - mean) / (std + 1e-8)
+
+    def get_statistics(self):
+        done = self.dones.clone()
+        done[-1] = 1
+        flat = done.permute(1, 0, 2).reshape(-1, 1)
+        idx = torch.cat((flat.new_tensor([-1], dtype=torch.int64), flat.nonzero(as_tuple=False)[:, 0]))
+        lengths = idx[1:] - idx[:-1]
+        return lengths.float().mean(), self.rewards.mean()
+
+    def mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        batch_size = self.num_envs * self.num_transitions_per_env
+        mb = batch_size // num_mini_batches
+        indices = torch.randperm(num_mini_batches * mb, requires_grad=False, device=self.device)
+        obs = self.observations.flatten(0, 1)
+        cobs = self.privileged_observations.flatten(0, 1) if self.privileged_observations is not None else obs
+        actions = self.actions.flatten(0, 1)
+        values = self.values.flatten(0, 1)
+        returns = self.returns.flatten(0, 1)
+        old_logp = self.actions_log_prob.flatten(0, 1)
+        adv = self.advantages.flatten(0, 1)
+        mu = self.mu.flatten(0, 1)
+        sigma = self.sigma.flatten(0, 1)
+        for _ in range(num_epochs):
+            for i in range(num_mini_batches):
+                b = indices[i * mb:(i + 1) * mb]
+                yield obs[b], cobs[b], actions[b], values[b], adv[b], returns[b], old_logp[b], mu[b], sigma[b], \
+                    (None, None), None

@@ -113,6 +113,9 @@ def declare(lib, prefix="lgx"):
         "actuator_mlp": (C.c_int, [vp, vp, i64, vp, vp, vp]),
         "actuator_lstm": (C.c_int, [vp, vp, vp, vp, i64, vp, vp]),
         "mlp_forward": (C.c_int, [vp, vp, i64, i32, C.POINTER(i32), C.POINTER(vp), C.POINTER(vp), i32, vp]),
+        "gae": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp]),
+        "profile_enable": (C.c_int, [vp, i32]),
+        "profile_collect": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}")
@@ -123,7 +126,8 @@ def declare(lib, prefix="lgx"):
 
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
             "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws",
-            "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward"]
+            "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
+            "lgx_profile_enable", "lgx_profile_collect"]
 
 
 def check_layout(sizes_fn):

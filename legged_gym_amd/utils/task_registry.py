@@ -8,10 +8,12 @@ rsl_rl-compatible `OnPolicyRunner` (legged_gym_amd.rl) unless `rsl_rl` is import
 import os
 import shutil
 from datetime import datetime
-from typing import Tuple
+from typing import TYPE_CHECKING, Tuple
 
 from legged_gym_amd import LEGGED_GYM_ROOT_DIR
-from legged_gym_amd.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO
+
+if TYPE_CHECKING:  # avoid the envs/__init__ -> task_registry import cycle
+    from legged_gym_amd.envs.base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO
 
 from .helpers import class_to_dict, get_args, get_load_path, parse_sim_params, set_seed, update_cfg_from_args
 
@@ -30,7 +32,7 @@ class TaskRegistry:
         self.env_cfgs = {}
         self.train_cfgs = {}
 
-    def register(self, name: str, task_class, env_cfg: LeggedRobotCfg, train_cfg: LeggedRobotCfgPPO):
+    def register(self, name: str, task_class, env_cfg: "LeggedRobotCfg", train_cfg: "LeggedRobotCfgPPO"):
         self.task_classes[name] = task_class
         self.env_cfgs[name] = env_cfg
         self.train_cfgs[name] = train_cfg
@@ -38,7 +40,7 @@ class TaskRegistry:
     def get_task_class(self, name: str):
         return self.task_classes[name]
 
-    def get_cfgs(self, name) -> Tuple[LeggedRobotCfg, LeggedRobotCfgPPO]:
+    def get_cfgs(self, name) -> Tuple["LeggedRobotCfg", "LeggedRobotCfgPPO"]:
         train_cfg = self.train_cfgs[name]
         env_cfg = self.env_cfgs[name]
         env_cfg.seed = train_cfg.seed  # task_registry.py:63-64
