@@ -250,6 +250,20 @@ int lgx_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m,
 int lgx_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
                     const float* const* weights, const float* const* biases, int32_t act, void* stream);
 
+/* Batched fused MLP forward: `count` (1 or 2) independent MLPs in ONE launch (rollout: actor
+ * mean + critic value).  Same per-network contract as lgx_mlp_forward. */
+typedef struct lgx_mlp_desc {
+  const float* x;
+  float* y;
+  int64_t rows;
+  int32_t nl;
+  int32_t act;
+  int32_t dims[7];
+  const float* weights[6];
+  const float* biases[6];
+} lgx_mlp_desc;
+int lgx_mlp_forward_batch(const lgx_mlp_desc* descs, int32_t count, void* stream);
+
 /* In-library kernel timing for the measurement harness (bench.py): when enabled, every
  * lgx_step records hipEvents on the launch stream around each kernel class
  * (0 physics, 1 actuator MLP, 2 post-physics incl. extras finalize).  lgx_profile_collect

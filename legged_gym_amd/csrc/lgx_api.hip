@@ -258,6 +258,12 @@ int lgx_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const in
                       "lgx_mlp_forward: launch (widths must be 1..512, layers 1..6)");
 }
 
+int lgx_mlp_forward_batch(const lgx_mlp_desc* descs, int32_t count, void* stream) {
+  if (!descs) return fail(LGX_EINVAL, "lgx_mlp_forward_batch: null descs");
+  return launch_check(lgx_launch_mlp_forward2(descs, count, (hipStream_t)stream),
+                      "lgx_mlp_forward_batch: launch (count 1..2, widths 1..512, layers 1..6)");
+}
+
 int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_values, float* returns,
             float* advantages, int32_t T, int32_t N, float gamma, float lam, void* stream) {
   if (!rewards || !values || !dones || !last_values || !returns || !advantages)

@@ -31,6 +31,7 @@ int lgx_launch_actuator_lstm(const float* x, float* h, float* c, float* tau, int
 int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
                            const float* const* weights, const float* const* biases, int32_t act, hipStream_t stream);
 
+int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t stream);
 int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream);
 

@@ -1,34 +1,46 @@
-// Fused MLP forward on f32 MFMA (v_mfma_f32_32x32x2_f32: exact f32, one rounding per product,
+// Fused MLP forward on f32 MFMA (v_mfma_f32_16x16x4_f32: exact f32, one rounding per product,
 // the f32 matrix peak of gfx950).  Used for
 //   * the Go1 actuator network (UniNet core, go1.py:22-35,100-105): 30-128-128-128-3, tanh,
 //     evaluated for decimation x N x 4 leg rows per env-step in ONE launch (the reference runs
 //     4 legs x 4 substeps of small GEMMs plus 96 host<->device copies per env-step);
-//   * rsl_rl ActorCritic inference in the rollout (obs-512-256-128-{12,1}, ELU).
+//   * rsl_rl ActorCritic inference in the rollout (obs-512-256-128-{12,1}, ELU): actor and
+//     critic run in the SAME launch (blockIdx.y selects the network).
 //
-// Tiling: a 256-thread workgroup (4 waves) owns BM = 32 rows for ALL layers; the activation
-// tile stays in LDS between layers (ping-pong, padded row stride -> conflict-free column
-// reads), so HBM traffic = input rows + output rows + weights (L2-resident).  Each wave owns
-// output column tiles w, w+4, ... (32 columns each, <= 4 per wave for widths <= 512);
-// A fragments come from LDS (lane l: row l&31, k = k0 + (l>>5)), B fragments from the
-// transposed weights W^T [in][out] in global memory (lane l: column l&31 -> coalesced 128 B).
+// Tiling (256-thread workgroup = 4 waves; no barrier inside a layer's K loop):
+//   * a row tile of BM = 16*RS rows stays in LDS across ALL layers: layer input and output
+//     live at opposite ends of one activation region whose row strides are = 2 (mod 32), which
+//     makes the MFMA A-fragment reads (16 rows x 2 k per 32-lane half) bank-conflict free;
+//     HBM traffic is the input and output rows only;
+//   * B fragments stream straight from the transposed weights W^T [in][out] (L2-resident,
+//     16 consecutive columns per 4 k-rows = 4 x 64 B per load) into a double-buffered ring
+//     of 8 VGPRs per lane, one group of k-steps ahead of the MFMAs consuming the other ring;
+//   * wave w owns output column tiles w, w+4, ... (16 columns each); a layer with TPW tiles
+//     per wave processes G = 8/TPW k-steps per group, so every group is 8 B loads + 8*RS MFMAs;
+//   * LDS is only the activation tile (<= 50 KB) -> 3-4 workgroups per CU hide the latency;
+//   * grid-stride over row tiles (persistent when rows >> grid * BM).
 #include "lgx_device.h"
 #include "lgx_internal.h"
 
-#define MLP_BM 32
 #define MLP_THREADS 256
 #define MLP_MAX_W 512
-#define MLP_LDS_STRIDE (MLP_MAX_W + 4)
 #define MLP_MAX_LAYERS 6
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct MlpArgs {
+  const float* x;
+  float* y;
+  int64_t rows;
   int32_t nl;
+  int32_t act;                      // 1 elu, 2 tanh
   int32_t dims[MLP_MAX_LAYERS + 1];
   const float* wt[MLP_MAX_LAYERS];  // [in][out]
   const float* b[MLP_MAX_LAYERS];
-  int32_t act;                      // 1 elu, 2 tanh
   const float* out_scale;           // optional per-output-column scale
+};
+
+struct MlpBatch {
+  MlpArgs m[2];
 };
 
 LGX_DEV float activate(float x, int act) {
@@ -37,119 +49,223 @@ LGX_DEV float activate(float x, int act) {
   return x;
 }
 
+__host__ __device__ inline int pad32(int n) { return (n + 31) & ~31; }
+__host__ __device__ inline int pad16(int n) { return (n + 15) & ~15; }
+__host__ __device__ inline int act_stride(int n) { return pad32(n) + 2; }  // == 2 (mod 32)
+
+// one layer: acc = in[BM x K] @ W^T[K x N]; TPW = column tiles per wave, G = k-steps per group
+template <int RS, int TPW, int MAXT>
+LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* __restrict__ W, int K, int N,
+                       int wave, int ln16, int lq, f32x4 (&acc)[RS][MAXT]) {
+  constexpr int G = 8 / TPW;
+  const int Kp = pad32(K);
+  int col[TPW];
+  bool cv[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    col[t] = (wave + 4 * t) * 16 + ln16;
+    cv[t] = col[t] < N;
+  }
+  float bA[G][TPW], bB[G][TPW];
+  auto load = [&](float (&b)[G][TPW], int k0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int k = k0 + 4 * g + lq;
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) b[g][t] = (cv[t] && k < K) ? W[(int64_t)k * N + col[t]] : 0.f;
+    }
+  };
+  auto compute = [&](const float (&b)[G][TPW], int k0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int k = k0 + 4 * g + lq;
+      float av[RS];
+#pragma unroll
+      for (int r = 0; r < RS; ++r) av[r] = in_lds[(r * 16 + ln16) * s_in + k];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int r = 0; r < RS; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b[g][t], acc[r][t], 0, 0, 0);
+    }
+  };
+  constexpr int KG = 4 * G;  // k per group
+  load(bA, 0);
+  for (int k0 = 0; k0 < Kp; k0 += 2 * KG) {
+    if (k0 + KG < Kp) load(bB, k0 + KG);
+    compute(bA, k0);
+    if (k0 + KG >= Kp) break;
+    if (k0 + 2 * KG < Kp) load(bA, k0 + 2 * KG);
+    compute(bB, k0 + KG);
+  }
+}
+
+template <int RS, int ACTW, int MAXT>
 __global__ void __launch_bounds__(MLP_THREADS)
-lgx_mlp_forward_kernel(const float* __restrict__ X, float* __restrict__ Y, int64_t rows, MlpArgs a) {
-  __shared__ float lds[2 * MLP_BM * MLP_LDS_STRIDE];  // 132 KB static (gfx950: 160 KB LDS per CU)
-  float* buf0 = lds;
-  float* buf1 = lds + MLP_BM * MLP_LDS_STRIDE;
+lgx_mlp_forward_kernel(MlpBatch batch) {
+  constexpr int BM = 16 * RS;
+  __shared__ float act_lds[BM * ACTW];
+  const MlpArgs& a = batch.m[blockIdx.y];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * MLP_BM;
-  const int k0 = a.dims[0];
-  const int k0p = (k0 + 1) & ~1;
-  // stage input tile (zero-padded rows and the odd K column)
-  for (int idx = tid; idx < MLP_BM * k0p; idx += MLP_THREADS) {
-    int r = idx / k0p, k = idx - r * k0p;
-    int64_t gr = r0 + r;
-    buf0[r * MLP_LDS_STRIDE + k] = (gr < rows && k < k0) ? X[gr * k0 + k] : 0.f;
-  }
-  __syncthreads();
-  float* in = buf0;
-  float* out = buf1;
-  const int arow = lane & 31;
-  const int akk = lane >> 5;
-  for (int l = 0; l < a.nl; ++l) {
-    const int K = a.dims[l], Nn = a.dims[l + 1];
-    const int Kp = (K + 1) & ~1;
-    const int ntiles = (Nn + 31) >> 5;
-    const float* __restrict__ W = a.wt[l];
-    const float* __restrict__ bias = a.b[l];
-    const bool last = l == a.nl - 1;
-    f32x16 acc[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-    int col[4];
-    bool cv[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      int tile = wave + 4 * t;
-      col[t] = tile * 32 + arow;
-      cv[t] = tile < ntiles && col[t] < Nn;
+  const int ln16 = lane & 15;
+  const int lq = lane >> 4;
+  const int64_t ntiles_rows = (a.rows + BM - 1) / BM;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles_rows; tile += gridDim.x) {
+    const int64_t r0 = tile * BM;
+    const int K0 = a.dims[0];
+    const int K0p = pad32(K0);
+    int s_in = act_stride(K0);
+    int in_off = 0;
+    for (int idx = tid; idx < BM * K0p; idx += MLP_THREADS) {
+      int r = idx / K0p, k = idx - r * K0p;
+      int64_t gr = r0 + r;
+      act_lds[r * s_in + k] = (gr < a.rows && k < K0) ? a.x[gr * K0 + k] : 0.f;
     }
-    const bool any = wave < ntiles;
-    if (any) {
-      for (int k = 0; k < Kp; k += 2) {
-        int kk = k + akk;
-        float av = in[arow * MLP_LDS_STRIDE + kk];
-        bool kval = kk < K;
+    __syncthreads();
+    for (int l = 0; l < a.nl; ++l) {
+      const int K = a.dims[l], N = a.dims[l + 1];
+      const bool last = l == a.nl - 1;
+      const int s_out = act_stride(N);
+      const int out_off = (in_off == 0) ? ACTW * BM - BM * s_out : 0;
+      const int ntile = pad16(N) >> 4;
+      const int tpw = (ntile + 3) >> 2;
+      f32x4 acc[RS][MAXT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          if (wave + 4 * t < ntiles) {  // wave-uniform
-            float bv = (cv[t] && kval) ? W[(int64_t)kk * Nn + col[t]] : 0.f;
-            acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[t], 0, 0, 0);
+      for (int r = 0; r < RS; ++r)
+#pragma unroll
+        for (int t = 0; t < MAXT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* in_lds = act_lds + in_off;
+      if constexpr (MAXT >= 8) {
+        if (tpw > 4) mlp_layer<RS, 8, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else if (tpw > 2) mlp_layer<RS, 4, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else if (tpw > 1) mlp_layer<RS, 2, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else mlp_layer<RS, 1, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+      } else {
+        if (tpw > 1) mlp_layer<RS, 2, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else mlp_layer<RS, 1, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+      }
+      // epilogue: bias + activation -> LDS output region (zero pad to pad32) or Y
+      const int Np32 = pad32(N);
+#pragma unroll
+      for (int t = 0; t < MAXT; ++t) {
+        const int ct = wave + 4 * t;
+        if (t >= tpw) break;
+        const int col = ct * 16 + ln16;
+        const bool cv = col < N;
+        const float bb = cv ? a.b[l][col] : 0.f;
+        const float sc = (last && a.out_scale && cv) ? a.out_scale[col] : 1.f;
+#pragma unroll
+        for (int r = 0; r < RS; ++r)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = r * 16 + lq * 4 + i;
+            const float v = acc[r][t][i] + bb;
+            if (!last) {
+              if (col < Np32) act_lds[out_off + row * s_out + col] = cv ? activate(v, a.act) : 0.f;
+            } else if (cv) {
+              const int64_t gr = r0 + row;
+              if (gr < a.rows) a.y[gr * N + col] = v * sc;
+            }
           }
+      }
+      if (!last) {
+        // columns [pad16(N), pad32(N)) have no owning tile: zero them for the next layer's k reads
+        const int p16 = pad16(N);
+        for (int idx = tid; idx < BM * (Np32 - p16); idx += MLP_THREADS) {
+          int r = idx / (Np32 - p16), cc = p16 + idx % (Np32 - p16);
+          act_lds[out_off + r * s_out + cc] = 0.f;
         }
       }
-    }
-    // epilogue: bias + activation -> next LDS tile or Y
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      int tile = wave + 4 * t;
-      if (tile >= ntiles) continue;
-      int c = tile * 32 + (lane & 31);
-      if (c >= Nn) continue;
-      float bb = bias[c];
-      float sc = (last && a.out_scale) ? a.out_scale[c] : 1.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        int r = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5);
-        float v = acc[t][i] + bb;
-        if (!last) {
-          out[r * MLP_LDS_STRIDE + c] = activate(v, a.act);
-        } else {
-          int64_t gr = r0 + r;
-          if (gr < rows) Y[gr * Nn + c] = v * sc;
-        }
-      }
-    }
-    if (!last) {
-      // zero the odd pad column used by the next layer's k-pairs
-      if ((Nn & 1) && tid < MLP_BM) out[tid * MLP_LDS_STRIDE + Nn] = 0.f;
-      __syncthreads();
-      float* t = in; in = out; out = t;
+      __syncthreads();  // outputs visible to every wave; input region free for reuse
+      in_off = out_off;
+      s_in = s_out;
     }
   }
 }
 
-static int launch_mlp(const float* x, float* y, int64_t rows, const MlpArgs& a, hipStream_t stream) {
-  if (rows <= 0) return 0;
+static bool valid(const MlpArgs& a, int actw) {
+  if (a.nl < 1 || a.nl > MLP_MAX_LAYERS || a.rows < 0) return false;
   for (int l = 0; l <= a.nl; ++l)
-    if (a.dims[l] <= 0 || a.dims[l] > MLP_MAX_W) return -1;
-  int64_t blocks = (rows + MLP_BM - 1) / MLP_BM;
-  hipLaunchKernelGGL(lgx_mlp_forward_kernel, dim3((unsigned)blocks), dim3(MLP_THREADS), 0, stream, x, y, rows, a);
+    if (a.dims[l] <= 0 || a.dims[l] > MLP_MAX_W) return false;
+  for (int l = 0; l < a.nl; ++l)
+    if (act_stride(a.dims[l]) + act_stride(a.dims[l + 1]) > actw) return false;
+  return true;
+}
+
+static int needed_actw(const MlpArgs& a) {
+  int w = 0;
+  for (int l = 0; l < a.nl; ++l) {
+    int s = act_stride(a.dims[l]) + act_stride(a.dims[l + 1]);
+    w = s > w ? s : w;
+  }
+  return w;
+}
+
+static int launch_batch(const MlpBatch& b, int count, hipStream_t stream) {
+  int64_t rows = 0;
+  int actw = 0;
+  for (int i = 0; i < count; ++i) {
+    const MlpArgs& a = b.m[i];
+    if (a.nl < 1 || a.nl > MLP_MAX_LAYERS) return -1;
+    for (int l = 0; l <= a.nl; ++l)
+      if (a.dims[l] <= 0 || a.dims[l] > MLP_MAX_W) return -1;
+    rows = a.rows > rows ? a.rows : rows;
+    int w = needed_actw(a);
+    actw = w > actw ? w : actw;
+  }
+  if (rows == 0) return 0;
+  int maxw = 0;
+  for (int i = 0; i < count; ++i)
+    for (int l = 1; l <= b.m[i].nl; ++l) maxw = b.m[i].dims[l] > maxw ? b.m[i].dims[l] : maxw;
+  const bool narrow = actw <= 264 && maxw <= 128;
+  if (!narrow && actw > 1032) return -1;
+  // narrow nets (actuator MLP, <= 128 wide): 32-row tiles, 33 KB LDS; wide (policy): 16-row tiles
+  const int bm = narrow ? 32 : 16;
+  int64_t tiles = (rows + bm - 1) / bm;
+  int64_t grid = tiles < 2048 ? tiles : 2048;
+  dim3 g((unsigned)grid, (unsigned)count);
+  if (narrow)
+    hipLaunchKernelGGL((lgx_mlp_forward_kernel<2, 264, 2>), g, dim3(MLP_THREADS), 0, stream, b);
+  else if (actw <= 776)
+    hipLaunchKernelGGL((lgx_mlp_forward_kernel<1, 776, 8>), g, dim3(MLP_THREADS), 0, stream, b);
+  else
+    hipLaunchKernelGGL((lgx_mlp_forward_kernel<1, 1032, 8>), g, dim3(MLP_THREADS), 0, stream, b);
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+static void fill(MlpArgs& a, const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
+                 const float* const* weights, const float* const* biases, int32_t act) {
+  a.x = x; a.y = y; a.rows = rows; a.nl = nl; a.act = act; a.out_scale = nullptr;
+  for (int l = 0; l <= nl && l <= MLP_MAX_LAYERS; ++l) a.dims[l] = dims[l];
+  for (int l = 0; l < nl && l < MLP_MAX_LAYERS; ++l) { a.wt[l] = weights[l]; a.b[l] = biases[l]; }
 }
 
 int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,
                            const float* const* weights, const float* const* biases, int32_t act, hipStream_t stream) {
   if (nl < 1 || nl > MLP_MAX_LAYERS) return -1;
-  MlpArgs a{};
-  a.nl = nl;
-  for (int l = 0; l <= nl; ++l) a.dims[l] = dims[l];
-  for (int l = 0; l < nl; ++l) { a.wt[l] = weights[l]; a.b[l] = biases[l]; }
-  a.act = act;
-  a.out_scale = nullptr;
-  return launch_mlp(x, y, rows, a, stream);
+  MlpBatch b{};
+  fill(b.m[0], x, y, rows, nl, dims, weights, biases, act);
+  return launch_batch(b, 1, stream);
+}
+
+int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t stream) {
+  if (count < 1 || count > 2) return -1;
+  MlpBatch b{};
+  for (int i = 0; i < count; ++i) {
+    if (d[i].nl < 1 || d[i].nl > MLP_MAX_LAYERS) return -1;
+    fill(b.m[i], d[i].x, d[i].y, d[i].rows, d[i].nl, d[i].dims, d[i].weights, d[i].biases, d[i].act);
+  }
+  return launch_batch(b, count, stream);
 }
 
 // packed actuator weights: W0t[30x128] b0 W1t[128x128] b1 W2t[128x128] b2 W3t[128x3] b3 (see lgx.h)
 int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
                             hipStream_t stream) {
-  MlpArgs a{};
-  a.nl = 4;
+  MlpBatch b{};
+  MlpArgs& a = b.m[0];
+  a.x = in; a.y = out; a.rows = rows; a.nl = 4; a.act = 2; a.out_scale = out_scale;
   const int d[5] = {30, 128, 128, 128, 3};
   const float* p = w;
   for (int l = 0; l < 4; ++l) {
@@ -158,9 +274,7 @@ int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const flo
     a.b[l] = p; p += d[l + 1];
   }
   a.dims[4] = 3;
-  a.act = 2;
-  a.out_scale = out_scale;
-  return launch_mlp(in, out, rows, a, stream);
+  return launch_batch(b, 1, stream);
 }
 
 // ---------------------------------------------------------------- ANYmal SEA LSTM

@@ -58,17 +58,39 @@ class _FusedMLP:
             self._wp = (C.c_void_p * n)(*[t.data_ptr() for t in self._wt])
             self._bp = (C.c_void_p * n)(*[t.data_ptr() for t in self._b])
 
-    def __call__(self, x):
-        from legged_gym_amd.sim import lib as lgxlib
-        lib = lgxlib.load()
+    def desc(self, x, y):
+        from legged_gym_amd.sim import abi
         self._refresh()
+        d = abi.LgxMlpDesc()
+        d.x, d.y, d.rows, d.nl, d.act = x.data_ptr(), y.data_ptr(), x.shape[0], len(self.linears), self.act
+        for i, v in enumerate(self.dims):
+            d.dims[i] = v
+        for i in range(len(self.linears)):
+            d.weights[i] = self._wt[i].data_ptr()
+            d.biases[i] = self._b[i].data_ptr()
+        return d
+
+    def invalidate(self):
+        self._ver = None
+
+    def __call__(self, x):
+        return run_fused([(self, x)])[0]
+
+
+def run_fused(pairs):
+    """One lgx_mlp_forward_batch launch for up to two (fused_mlp, input) pairs."""
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim import lib as lgxlib
+    lib = lgxlib.load()
+    outs, descs = [], (abi.LgxMlpDesc * len(pairs))()
+    for i, (m, x) in enumerate(pairs):
         x = x.contiguous()
-        y = torch.empty(x.shape[0], self.dims[-1], device=x.device, dtype=torch.float)
-        stream = C.c_void_p(torch.cuda.current_stream(x.device).cuda_stream)
-        lgxlib.check(lib.lgx_mlp_forward(C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), x.shape[0],
-                                         len(self.linears), self._dims_c, self._wp, self._bp, self.act, stream),
-                     "lgx_mlp_forward")
-        return y
+        y = torch.empty(x.shape[0], m.dims[-1], device=x.device, dtype=torch.float)
+        descs[i] = m.desc(x, y)
+        outs.append((x, y))
+    stream = C.c_void_p(torch.cuda.current_stream(pairs[0][1].device).cuda_stream)
+    lgxlib.check(lib.lgx_mlp_forward_batch(descs, len(pairs), stream), "lgx_mlp_forward_batch")
+    return [y for _, y in outs]
 
 
 class ActorCritic(nn.Module):
@@ -98,6 +120,11 @@ class ActorCritic(nn.Module):
 
     def reset(self, dones=None):
         pass
+
+    def invalidate_fused(self):
+        """Call after parameters change outside autograd-visible in-place ops (optimizer step, load)."""
+        self._fused_actor.invalidate()
+        self._fused_critic.invalidate()
 
     def forward(self):
         raise NotImplementedError
@@ -136,6 +163,14 @@ class ActorCritic(nn.Module):
 
     def act_inference(self, observations):
         return self._actor_mean(observations)
+
+    def act_and_evaluate(self, observations, critic_observations):
+        """Rollout fast path: actor mean + critic value in ONE fused MFMA launch, then sample."""
+        if self._fused_ok(observations, self._fused_actor) and self._fused_critic.ok:
+            mean, value = run_fused([(self._fused_actor, observations), (self._fused_critic, critic_observations)])
+            self.distribution = Normal(mean, mean * 0.0 + self.std)
+            return self.distribution.sample(), value
+        return self.act(observations), self.evaluate(critic_observations)
 
     def evaluate(self, critic_observations, **kwargs):
         if self._fused_ok(critic_observations, self._fused_critic):

@@ -68,8 +68,12 @@ class PPO:
     # ---------------------------------------------------------------- rollout
     def act(self, obs, critic_obs):
         t = self.transition
-        t.actions = self.actor_critic.act(obs).detach()
-        t.values = self.actor_critic.evaluate(critic_obs).detach()
+        if hasattr(self.actor_critic, "act_and_evaluate"):
+            actions, values = self.actor_critic.act_and_evaluate(obs, critic_obs)
+            t.actions, t.values = actions.detach(), values.detach()
+        else:
+            t.actions = self.actor_critic.act(obs).detach()
+            t.values = self.actor_critic.evaluate(critic_obs).detach()
         t.actions_log_prob = self.actor_critic.get_actions_log_prob(t.actions).detach()
         t.action_mean = self.actor_critic.action_mean.detach()
         t.action_sigma = self.actor_critic.action_std.detach()
@@ -159,6 +163,8 @@ class PPO:
             self.optimizer.step()
             mean_value_loss += value_loss.detach()
             mean_surrogate_loss += surrogate_loss.detach()
+        if hasattr(self.actor_critic, "invalidate_fused"):
+            self.actor_critic.invalidate_fused()
         n = self.num_learning_epochs * self.num_mini_batches
         mean_value_loss = (mean_value_loss / n).item()
         mean_surrogate_loss = (mean_surrogate_loss / n).item()

@@ -152,6 +152,8 @@ class OnPolicyRunner:
     def load(self, path, load_optimizer=True):
         d = torch.load(path, map_location=self.device, weights_only=True)
         self.alg.actor_critic.load_state_dict(d["model_state_dict"])
+        if hasattr(self.alg.actor_critic, "invalidate_fused"):
+            self.alg.actor_critic.invalidate_fused()
         if load_optimizer:
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
         self.current_learning_iteration = d["iter"]

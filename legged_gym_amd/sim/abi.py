@@ -94,6 +94,11 @@ class LgxBuffers(C.Structure):
     _fields_ = BUFFER_FIELDS
 
 
+class LgxMlpDesc(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("rows", i64), ("nl", i32), ("act", i32), ("dims", i32 * 7),
+                ("weights", C.c_void_p * 6), ("biases", C.c_void_p * 6)]
+
+
 def declare(lib, prefix="lgx"):
     """Attach argtypes/restypes of the product C-ABI to a loaded CDLL."""
     vp = C.c_void_p
@@ -115,6 +120,7 @@ def declare(lib, prefix="lgx"):
         "mlp_forward": (C.c_int, [vp, vp, i64, i32, C.POINTER(i32), C.POINTER(vp), C.POINTER(vp), i32, vp]),
         "gae": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp]),
         "profile_enable": (C.c_int, [vp, i32]),
+        "mlp_forward_batch": (C.c_int, [C.POINTER(LgxMlpDesc), i32, vp]),
         "profile_collect": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
     for name, (res, args) in sigs.items():
@@ -127,7 +133,7 @@ def declare(lib, prefix="lgx"):
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
             "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
-            "lgx_profile_enable", "lgx_profile_collect"]
+            "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch"]
 
 
 def check_layout(sizes_fn):

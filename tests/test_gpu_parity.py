@@ -254,3 +254,40 @@ def test_rough_terrain_step_matches_oracle(gpu):
     assert ok, f"obs max err {e}"
     ok, e = close(dev.actuator_dvel, ora.actuator_dvel, 1e-3, 1e-3)
     assert ok, f"dVel max err {e}"
+
+
+def test_mlp_forward_batch_actor_critic(gpu):
+    """act_and_evaluate (one batched launch) == torch autograd modules."""
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    torch.manual_seed(0)
+    ac = ActorCritic(235, 235, 12, [512, 256, 128], [512, 256, 128]).to(gpu)
+    obs = torch.randn(4096 + 5, 235, device=gpu)
+    with torch.inference_mode():
+        _, v = ac.act_and_evaluate(obs, obs)
+        mean = ac.action_mean
+        ref_mean = ac.actor(obs)
+        ref_v = ac.critic(obs)
+    ok, e = close(mean, ref_mean, 2e-4, 2e-4)
+    assert ok, f"actor mean max err {e}"
+    ok, e = close(v, ref_v, 2e-4, 2e-4)
+    assert ok, f"critic value max err {e}"
+
+
+def test_gae_kernel_matches_torch_loop(gpu):
+    from legged_gym_amd.rl.storage import RolloutStorage
+    T, N = 24, 1000
+    gen = torch.Generator().manual_seed(1)
+    st_c = RolloutStorage(N, T, [4], [None], [2], "cpu")
+    st_c.rewards.copy_(torch.randn(T, N, 1, generator=gen))
+    st_c.values.copy_(torch.randn(T, N, 1, generator=gen))
+    st_c.dones.copy_((torch.rand(T, N, 1, generator=gen) < 0.1).byte())
+    last = torch.randn(N, 1, generator=gen)
+    st_g = RolloutStorage(N, T, [4], [None], [2], str(gpu))
+    for name in ("rewards", "values", "dones"):
+        getattr(st_g, name).copy_(getattr(st_c, name))
+    st_c.compute_returns(last, 0.99, 0.95)
+    st_g.compute_returns(last.to(gpu), 0.99, 0.95)
+    ok, e = close(st_g.returns, st_c.returns, 1e-4, 1e-5)
+    assert ok, f"returns max err {e}"
+    ok, e = close(st_g.advantages, st_c.advantages, 1e-4, 1e-4)
+    assert ok, f"advantages max err {e}"

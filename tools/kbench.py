@@ -1,0 +1,74 @@
+"""Kernel micro-benchmarks on the GPU box (timing with torch.cuda events on the launch stream)."""
+import ctypes as C
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def timeit(fn, iters=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def mlp_bench():
+    from legged_gym_amd.envs.go1.go1 import pack_uninet_weights
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    from legged_gym_amd.sim import lib as lgxlib
+    from legged_gym_amd.sim.model import load_actuator_net
+    import legged_gym_amd
+    dev = torch.device("cuda:0")
+    lib = lgxlib.load()
+    net = load_actuator_net(os.path.join(legged_gym_amd.LEGGED_GYM_ROOT_DIR, "resources/actuator_nets/go1_net.npz"))
+    w = torch.tensor(pack_uninet_weights(net), device=dev)
+    sc = torch.tensor(net["vel_std"], device=dev)
+    rows = 4 * 4096 * 4
+    x = torch.randn(rows, 30, device=dev)
+    y = torch.empty(rows, 3, device=dev)
+    fn = lambda: lib.lgx_actuator_mlp(C.c_void_p(x.data_ptr()), C.c_void_p(y.data_ptr()), rows, C.c_void_p(w.data_ptr()),
+                                      C.c_void_p(sc.data_ptr()), None)
+    ms = timeit(fn)
+    flop = rows * 2 * (30 * 128 + 128 * 128 * 2 + 128 * 3)
+    print(f"actuator mlp rows={rows}: {ms*1e3:.1f} us  {flop/ms/1e9:.1f} TFLOP/s")
+    ac = ActorCritic(235, 235, 12, [512, 256, 128], [512, 256, 128]).to(dev)
+    obs = torch.randn(4096, 235, device=dev)
+    with torch.inference_mode():
+        ms = timeit(lambda: ac.act_and_evaluate(obs, obs))
+        flop = 4096 * 2 * 2 * (235 * 512 + 512 * 256 + 256 * 128 + 128 * 6.5)
+        print(f"actor+critic act_and_evaluate rows=4096: {ms*1e3:.1f} us  {flop/ms/1e9:.1f} TFLOP/s")
+        ms2 = timeit(lambda: (ac.actor(obs), ac.critic(obs)))
+        print(f"  torch (hipBLASLt) actor+critic: {ms2*1e3:.1f} us")
+        big = torch.randn(24576, 235, device=dev)
+        ms3 = timeit(lambda: ac._fused_actor(big), iters=20)
+        f3 = 24576 * 2 * (235 * 512 + 512 * 256 + 256 * 128 + 128 * 12)
+        print(f"actor fused rows=24576: {ms3*1e3:.1f} us {f3/ms3/1e9:.1f} TFLOP/s; torch {timeit(lambda: ac.actor(big), iters=20)*1e3:.1f} us")
+
+
+def env_bench(task="go1_rough", n=4096):
+    from oracle_backend import make_env
+    env = make_env(task, num_envs=n, device="cuda:0", backend="lgx")
+    env.reset()
+    a = torch.randn(n, 12, device="cuda:0") * 0.5
+    ms = timeit(lambda: env.step(a), iters=50)
+    print(f"{task} env.step N={n}: {ms*1e3:.1f} us/step  {n/ms*1e3/1e6:.2f} M env-steps/s (env only)")
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["mlp", "env"]
+    if "mlp" in what:
+        mlp_bench()
+    if "env" in what:
+        env_bench()
