@@ -539,6 +539,12 @@ static void actuator_history(const ctx_t* cx, int e, int substep) {
   }
 }
 
+/* one substep of the Go1 actuator history for all envs (replay of go1.py:79-98) */
+void lgxo_actuator_history(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b, int substep) {
+  ctx_t cx = {m, p, b, NULL, 0};
+  for (int e = 0; e < p->num_envs; ++e) actuator_history(&cx, e, substep);
+}
+
 /* ------------------------------------------------------------------ env step pieces */
 
 void lgxo_compute_targets(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b) {

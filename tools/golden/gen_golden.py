@@ -1,0 +1,476 @@
+"""Golden-vector generator: drives the REFERENCE's own post-physics Python (container-only).
+
+What it does
+  * imports /root/reference/legged_gym (read-only; bytecode writing disabled) behind in-process
+    stand-ins for the two un-vendored dependencies: `isaacgym` (a fake tensor-API backend whose
+    `simulate()` applies SCRIPTED physics outputs, plus the torch_utils helpers the reference
+    imports, restated with their published xyzw semantics) and `rsl_rl` (names only);
+  * wraps the reference env's random draws (torch_rand_float / rand_like / randint_like) so that
+    every draw is taken from a per-step, per-env slot table (the lgx draw layout, lgx.h
+    LGX_DRAW_*): the same table is then injected into the lgx oracle/kernels;
+  * steps the reference `Go1` / `Anymal` envs and records, per step, the inputs (actions,
+    scripted physics state, draw table) and the outputs of the reference's own code
+    (obs, rew, resets, time-outs, extras, commands, feet air time, episode sums, post-reset
+    state, last_* buffers, heights, actuator-net inputs, terrain levels/origins).
+Nothing here ships: the reference never reaches the GPU box, only the .npz vectors do.
+
+Usage: python tools/golden/gen_golden.py            -> tests/golden/*.npz
+"""
+import os
+import sys
+import types
+
+sys.dont_write_bytecode = True
+os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+REF = "/root/reference"
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+OUT = os.path.join(ROOT, "tests", "golden")
+
+from legged_gym_amd.sim import abi  # noqa: E402  (draw-slot layout only)
+
+
+# ----------------------------------------------------------------------------- draw injection
+class DrawCtx:
+    table = None          # torch [N, stride] float32 for the current step
+    ids = None            # env ids the current reference call draws for
+    cursor = None         # next slot
+
+
+def _injected(lower, upper, shape):
+    n, w = shape
+    ids = DrawCtx.ids
+    u = DrawCtx.table[ids][:, DrawCtx.cursor:DrawCtx.cursor + w]
+    assert u.shape == (n, w), (u.shape, shape)
+    DrawCtx.cursor += w
+    return (upper - lower) * u + lower
+
+
+def torch_rand_float(lower, upper, shape, device):
+    if DrawCtx.cursor is not None:
+        return _injected(lower, upper, shape).to(device)
+    return (upper - lower) * torch.rand(*shape, device=device) + lower
+
+
+# ----------------------------------------------------------------------------- isaacgym stand-in
+def make_isaacgym_stub(model):
+    def mod(name):
+        m = types.ModuleType(name)
+        sys.modules[name] = m
+        return m
+
+    ig = mod("isaacgym")
+    gymapi, gymtorch, gymutil, tu, tut = (mod("isaacgym.gymapi"), mod("isaacgym.gymtorch"), mod("isaacgym.gymutil"),
+                                          mod("isaacgym.torch_utils"), mod("isaacgym.terrain_utils"))
+    ig.gymapi, ig.gymtorch, ig.gymutil, ig.torch_utils, ig.terrain_utils = gymapi, gymtorch, gymutil, tu, tut
+
+    # torch_utils (xyzw quaternions) as the reference uses them
+    def to_torch(x, dtype=torch.float, device="cuda:0", requires_grad=False):
+        return torch.tensor(x, dtype=dtype, device=device, requires_grad=requires_grad)
+
+    def normalize(x, eps: float = 1e-9):
+        return x / x.norm(p=2, dim=-1).clamp(min=eps, max=None).unsqueeze(-1)
+
+    def quat_apply(a, b):
+        shape = b.shape
+        a = a.reshape(-1, 4)
+        b = b.reshape(-1, 3)
+        xyz = a[:, :3]
+        t = xyz.cross(b, dim=-1) * 2
+        return (b + a[:, 3:] * t + xyz.cross(t, dim=-1)).view(shape)
+
+    def quat_rotate_inverse(q, v):
+        shape = q.shape
+        q_w = q[:, -1]
+        q_vec = q[:, :3]
+        a = v * (2.0 * q_w ** 2 - 1.0).unsqueeze(-1)
+        b = torch.cross(q_vec, v, dim=-1) * q_w.unsqueeze(-1) * 2.0
+        c = q_vec * torch.bmm(q_vec.view(shape[0], 1, 3), v.view(shape[0], 3, 1)).squeeze(-1) * 2.0
+        return a - b + c
+
+    def get_axis_params(value, axis_idx, x_value=0., dtype=np.float64, n_dims=3):
+        zs = np.zeros((n_dims,))
+        zs[axis_idx] = 1.
+        params = np.where(zs == 1., value, zs)
+        params[0] = x_value
+        return list(params.astype(dtype))
+
+    for f in [to_torch, normalize, quat_apply, quat_rotate_inverse, get_axis_params, torch_rand_float]:
+        setattr(tu, f.__name__, f)
+    tu.__all__ = [f.__name__ for f in [to_torch, normalize, quat_apply, quat_rotate_inverse, get_axis_params,
+                                       torch_rand_float]]
+
+    class Obj:
+        def __init__(self, **k):
+            self.__dict__.update(k)
+
+    class Vec3:
+        def __init__(self, x=0., y=0., z=0.):
+            self.x, self.y, self.z = float(x), float(y), float(z)
+
+    class Transform:
+        def __init__(self, p=None, r=None):
+            self.p = p or Vec3()
+            self.r = r
+
+    for n in ["PlaneParams", "AssetOptions", "HeightFieldParams", "TriangleMeshParams", "CameraProperties"]:
+        setattr(gymapi, n, lambda: Obj(transform=Transform()))
+    gymapi.Vec3, gymapi.Transform = Vec3, Transform
+    gymapi.DOF_MODE_POS, gymapi.SIM_PHYSX, gymapi.KEY_ESCAPE, gymapi.KEY_V = 1, 0, 0, 0
+    gymutil.parse_device_str = lambda s: (s.split(":")[0], int(s.split(":")[1]) if ":" in s else 0)
+    gymtorch.wrap_tensor = lambda t: t
+    gymtorch.unwrap_tensor = lambda t: t
+
+    class FakeGym:
+        """Isaac Gym tensor API stand-in: the physics is scripted (`next_state`)."""
+
+        def __init__(self):
+            self.n = 0
+            self.sim_calls = 0
+            self.next_state = None
+            self.decimation = 4
+
+        def create_sim(self, *a):
+            return "sim"
+
+        def add_ground(self, *a):
+            pass
+
+        def add_triangle_mesh(self, *a):
+            pass
+
+        def add_heightfield(self, *a):
+            pass
+
+        def load_asset(self, *a):
+            return "asset"
+
+        def get_asset_dof_count(self, a):
+            return len(model["dof_names"])
+
+        def get_asset_rigid_body_count(self, a):
+            return len(model["body_names"])
+
+        def get_asset_dof_properties(self, a):
+            dt = np.dtype([("lower", "f4"), ("upper", "f4"), ("velocity", "f4"), ("effort", "f4"), ("driveMode", "i4"),
+                           ("stiffness", "f4"), ("damping", "f4")])
+            p = np.zeros(len(model["joints"]), dt)
+            for i, j in enumerate(model["joints"]):
+                lo, hi = (j["lower"], j["upper"]) if j["lower"] < j["upper"] else (-1e3, 1e3)
+                p[i] = (lo, hi, j["velocity"], j["effort"], 3, 0, 0)
+            return p
+
+        def get_asset_rigid_shape_properties(self, a):
+            return [Obj(friction=1.0) for _ in range(len(model["body_names"]))]
+
+        def get_asset_rigid_body_names(self, a):
+            return list(model["body_names"])
+
+        def get_asset_dof_names(self, a):
+            return list(model["dof_names"])
+
+        def create_env(self, *a):
+            self.n += 1
+            return self.n - 1
+
+        def create_actor(self, *a):
+            return 0
+
+        def get_actor_rigid_body_properties(self, e, h):
+            return [Obj(mass=b["mass"]) for b in model["report_bodies"]]
+
+        def find_actor_rigid_body_handle(self, e, h, name):
+            return model["body_names"].index(name)
+
+        def prepare_sim(self, sim):
+            N, nd, nb = self.n, len(model["dof_names"]), len(model["body_names"])
+            self.root = torch.zeros(N, 13)
+            self.root[:, 6] = 1.0
+            self.dof = torch.zeros(N * nd, 2)
+            self.cf = torch.zeros(N * nb, 3)
+            self.tq = torch.zeros(N * nd)
+
+        def acquire_actor_root_state_tensor(self, s):
+            return self.root
+
+        def acquire_dof_state_tensor(self, s):
+            return self.dof
+
+        def acquire_net_contact_force_tensor(self, s):
+            return self.cf
+
+        def acquire_dof_force_tensor(self, s):
+            return self.tq
+
+        def simulate(self, s):
+            self.sim_calls += 1
+            if self.next_state is not None and self.sim_calls % self.decimation == 0:
+                root, dof, cf, tq = self.next_state
+                self.root.copy_(root)
+                self.dof.copy_(dof)
+                self.cf.copy_(cf)
+                self.tq.copy_(tq)
+
+        def __getattr__(self, name):
+            if name.startswith(("refresh_", "fetch_", "set_", "viewer_", "enable_", "step_", "draw_")):
+                return lambda *a, **k: None
+            raise AttributeError(name)
+
+    gymapi.acquire_gym = lambda: FakeGym()
+    for n in ["rsl_rl", "rsl_rl.env", "rsl_rl.runners"]:
+        mod(n)
+    sys.modules["rsl_rl.env"].VecEnv = object
+    sys.modules["rsl_rl.runners"].OnPolicyRunner = object
+
+
+# ----------------------------------------------------------------------------- instrumentation
+def instrument(env, stride):
+    """Route every post-physics random draw of the reference env through DrawCtx."""
+    N = env.num_envs
+    in_reset = {"on": False}
+
+    def with_ctx(ids, cursor, fn, *a):
+        prev = (DrawCtx.ids, DrawCtx.cursor)
+        DrawCtx.ids, DrawCtx.cursor = ids, cursor
+        try:
+            return fn(*a)
+        finally:
+            DrawCtx.ids, DrawCtx.cursor = prev
+
+    orig_resample = env._resample_commands
+    env._resample_commands = lambda ids: with_ctx(ids, abi.DRAW_RESET_CMD if in_reset["on"] else abi.DRAW_CMD,
+                                                  orig_resample, ids)
+    orig_dofs = env._reset_dofs
+    env._reset_dofs = lambda ids: with_ctx(ids, abi.DRAW_RESET_DOF, orig_dofs, ids)
+    orig_root = env._reset_root_states
+    env._reset_root_states = lambda ids: with_ctx(ids, abi.DRAW_RESET_XY if env.custom_origins else abi.DRAW_RESET_VEL,
+                                                  orig_root, ids)
+    orig_push = env._push_robots
+    env._push_robots = lambda: with_ctx(torch.arange(N), abi.DRAW_PUSH, orig_push)
+    orig_curric = env._update_terrain_curriculum
+
+    def curric(ids):
+        saved = torch.randint_like
+
+        def randint_like(t, high):
+            u = DrawCtx.table[ids][:, abi.DRAW_CURRIC]
+            return torch.clamp((u * float(high)).to(torch.long), max=high - 1).to(t.dtype)
+        torch.randint_like = randint_like
+        try:
+            return orig_curric(ids)
+        finally:
+            torch.randint_like = saved
+    env._update_terrain_curriculum = curric
+    orig_reset_idx = env.reset_idx
+
+    def reset_idx(ids):
+        in_reset["on"] = True
+        try:
+            return orig_reset_idx(ids)
+        finally:
+            in_reset["on"] = False
+    env.reset_idx = reset_idx
+    orig_obs = env.compute_observations
+
+    def compute_observations():
+        saved = torch.rand_like
+        torch.rand_like = lambda t: DrawCtx.table[:, abi.DRAW_NOISE:abi.DRAW_NOISE + t.shape[1]].clone()
+        try:
+            return orig_obs()
+        finally:
+            torch.rand_like = saved
+    env.compute_observations = compute_observations
+
+
+# ----------------------------------------------------------------------------- scripted physics
+def scripted_state(env, gen, step):
+    N, nd, nb = env.num_envs, env.num_dof, env.num_bodies
+    r = lambda *s: torch.rand(*s, generator=gen)
+    root = env.root_states.clone()
+    root[:, :2] += (r(N, 2) - 0.5) * 0.4
+    root[:, 2] += (r(N) - 0.5) * 0.05
+    q = root[:, 3:7] + (r(N, 4) - 0.5) * torch.tensor([0.1, 0.1, 0.6, 0.1])
+    root[:, 3:7] = q / q.norm(dim=1, keepdim=True)
+    root[:, 7:13] = (r(N, 6) - 0.5) * 2.0
+    dof = env.dof_state.clone().view(N, nd, 2)
+    dof[..., 0] = env.default_dof_pos + (r(N, nd) - 0.5) * 0.8
+    dof[..., 1] = (r(N, nd) - 0.5) * 6.0
+    cf = torch.zeros(N, nb, 3)
+    cf[:, :, :] = (r(N, nb, 3) - 0.5) * 0.3                              # small noise on all bodies
+    feet = env.feet_indices
+    contact = r(N, len(feet)) > 0.4
+    cf[:, feet, 2] = torch.where(contact, 5 + 40 * r(N, len(feet)), 0.5 * r(N, len(feet)))
+    cf[:, feet, :2] = (r(N, len(feet), 2) - 0.5) * 20
+    pen = env.penalised_contact_indices
+    cf[:, pen] *= torch.where(r(N, len(pen), 1) < 0.2, 10.0, 1.0)          # some collisions > 0.1 N
+    base_hit = r(N) < (0.08 if step > 1 else 0.0)
+    cf[:, 0, 2] = torch.where(base_hit, 3.0 + r(N), cf[:, 0, 2] * 0.1)      # terminations
+    tq = (r(N, nd) - 0.5) * 30
+    return root, dof.view(N * nd, 2), cf.view(N * nb, 3), tq.view(N * nd)
+
+
+def snapshot(env, keys):
+    out = {}
+    for k in keys:
+        v = getattr(env, k)
+        out[k] = v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v).copy()
+    return out
+
+
+REC_KEYS = ["obs_buf", "rew_buf", "reset_buf", "time_out_buf", "commands", "feet_air_time", "episode_length_buf",
+            "root_states", "dof_state", "last_actions", "last_dof_vel", "last_root_vel", "base_lin_vel", "base_ang_vel",
+            "projected_gravity", "env_origins", "target_poses"]
+
+
+def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, standalone_reset_at=None):
+    import json
+    model = json.load(open(os.path.join(ROOT, "legged_gym_amd", "resources", model_json)))
+    make_isaacgym_stub(model)
+    sys.path.insert(0, REF)
+    from legged_gym.envs import AnymalCRoughCfg, Go1RoughCfg  # noqa: F401
+    import legged_gym.envs as lenvs
+    import legged_gym.envs.base.legged_robot as lr
+    from legged_gym_amd.utils.terrain import Terrain as LgxTerrain
+
+    class TerrainForRef(LgxTerrain):   # same heightfield handed to the reference and to lgx
+        def __init__(self, cfg, n):
+            super().__init__(cfg, n)
+            if self.type == "trimesh":
+                self.vertices = np.zeros((4, 3), np.float32)
+                self.triangles = np.zeros((2, 3), np.uint32)
+    lr.Terrain = TerrainForRef
+    # Go1's actuator net: the TorchScript archive is not loaded (no executing loader); the
+    # recorded quantity is the actuator-net INPUT history (model_ins), which is what the
+    # reference computes on the step path (the MLP output dVel is discarded, go1.py:71-73)
+    class _NoNet(torch.nn.Module):
+        def forward(self, x, *a):
+            return torch.zeros(x.shape[0], 3)
+    torch.jit.load = lambda *a, **k: _NoNet()
+    cfg = cfg_fn()
+    cfg.env.num_envs = num_envs
+    torch.manual_seed(seed)
+    np.random.seed(seed)
+    sp = types.SimpleNamespace(dt=float(np.float32(0.005)), use_gpu_pipeline=False)
+    env = getattr(lenvs, env_cls_name)(cfg, sp, 0, "cpu", True)
+    gym = env.gym
+    stride = abi.DRAW_NOISE + env.num_obs
+    gen = torch.Generator().manual_seed(seed + 100)
+    instrument(env, stride)
+    # initial reset() with injected draws
+    DrawCtx.table = torch.rand(num_envs, stride, generator=gen)
+    init_draws = DrawCtx.table.clone()
+    env.reset()
+    # edge cases: resample (500), time-out (1001), push (751)
+    el = env.episode_length_buf
+    el[0::7] = 499
+    el[1::7] = 1000
+    el[2::7] = 998
+    env.common_step_counter = 748
+    rec = {"name": name, "num_envs": num_envs, "steps": steps, "stride": stride}
+    init_state = snapshot(env, REC_KEYS + ["terrain_levels"] if hasattr(env, "terrain_levels") else REC_KEYS)
+    init_state["episode_sums"] = np.stack([env.episode_sums[k].numpy() for k in env.episode_sums])
+    init_state["common_step_counter"] = np.array(env.common_step_counter)
+    if hasattr(env, "pos_err_buffs"):
+        init_state["act_hist"] = np.concatenate([env.pos_err_buffs, env.vel_buffs], axis=2).astype(np.float32)
+    if env.height_samples is not None:
+        rec["height_samples"] = env.height_samples.numpy().astype(np.int16)
+        rec["terrain_origins"] = env.terrain_origins.numpy()
+        rec["terrain_types"] = env.terrain_types.numpy()
+        init_state["measured_heights"] = np.asarray(env.measured_heights.numpy() if torch.is_tensor(env.measured_heights)
+                                                    else np.zeros((num_envs, 187)), np.float32)
+    rec["episode_keys"] = np.array(list(env.episode_sums.keys()))
+    per_step = {k: [] for k in ["actions", "draws", "next_root", "next_dof", "next_cf", "next_tq", "extras",
+                                "extras_time_outs", "episode_sums", "terrain_levels", "measured_heights", "model_ins",
+                                "reset_ids"] + REC_KEYS}
+    for t in range(steps):
+        DrawCtx.table = torch.rand(num_envs, stride, generator=gen)
+        actions = (torch.rand(num_envs, env.num_actions, generator=gen) - 0.5) * 4.0
+        actions[0, 0] = 150.0  # exercises clip_actions (legged_robot.py:85-86)
+        nxt = scripted_state(env, gen, t)
+        gym.next_state = nxt
+        gym.decimation = cfg.control.decimation
+        env.extras.pop("episode", None)
+        env.step(actions)
+        per_step["actions"].append(actions.numpy())
+        per_step["draws"].append(DrawCtx.table.numpy())
+        for k, v in zip(["next_root", "next_dof", "next_cf", "next_tq"], nxt):
+            per_step[k].append(v.numpy())
+        s = snapshot(env, REC_KEYS)
+        for k in REC_KEYS:
+            per_step[k].append(s[k])
+        ep = env.extras.get("episode", {})
+        per_step["extras"].append(np.array([float(ep.get("rew_" + k, np.nan)) for k in env.episode_sums] +
+                                           [float(ep.get("terrain_level", np.nan))], np.float32))
+        per_step["extras_time_outs"].append(env.extras["time_outs"].numpy().copy() if "time_outs" in env.extras
+                                            else np.zeros(num_envs, bool))
+        per_step["episode_sums"].append(np.stack([env.episode_sums[k].numpy().copy() for k in env.episode_sums]))
+        per_step["terrain_levels"].append(env.terrain_levels.numpy().copy() if hasattr(env, "terrain_levels")
+                                          else np.zeros(num_envs, np.int64))
+        mh = env.measured_heights
+        per_step["measured_heights"].append(mh.numpy().copy() if torch.is_tensor(mh) else np.zeros((num_envs, 1), np.float32))
+        per_step["model_ins"].append(env.model_ins.numpy().copy() if hasattr(env, "model_ins")
+                                     else np.zeros((num_envs, 1), np.float32))
+        per_step["reset_ids"].append(np.zeros(0, np.int32))
+    DrawCtx.cursor = None
+    for k, v in per_step.items():
+        if k == "reset_ids":
+            continue
+        rec["step_" + k] = np.stack(v)
+    for k, v in init_state.items():
+        rec["init_" + k] = v
+    rec["init_draws"] = init_draws.numpy()
+    # reference-side derived constants (checked by tests, e.g. max_episode_length = 1001)
+    rec["max_episode_length"] = np.array(env.max_episode_length)
+    rec["dt"] = np.array(env.dt)
+    rec["push_interval"] = np.array(cfg.domain_rand.push_interval)
+    rec["reward_names"] = np.array(env.reward_names)
+    rec["reward_scales"] = np.array([env.reward_scales[k] for k in env.reward_names])
+    rec["noise_scale_vec"] = env.noise_scale_vec.numpy()
+    rec["dof_pos_limits"] = env.dof_pos_limits.numpy()
+    rec["default_dof_pos"] = env.default_dof_pos.numpy()
+    rec["feet_indices"] = env.feet_indices.numpy()
+    rec["penalised_contact_indices"] = env.penalised_contact_indices.numpy()
+    rec["termination_contact_indices"] = env.termination_contact_indices.numpy()
+    os.makedirs(OUT, exist_ok=True)
+    path = os.path.join(OUT, f"{name}.npz")
+    np.savez_compressed(path, **rec)
+    print(name, "->", path, os.path.getsize(path) // 1024, "KB", "resets per step:",
+          [int(x.sum()) for x in per_step["reset_buf"]])
+    for m in [m for m in list(sys.modules) if m == "legged_gym" or m.startswith("legged_gym.")]:
+        del sys.modules[m]
+    sys.path.remove(REF)
+
+
+def go1_flat():
+    sys.path.insert(0, REF)
+    from legged_gym.envs.go1.go1_config import Go1RoughCfg
+    return Go1RoughCfg()
+
+
+def go1_rough():
+    from legged_gym.envs.go1.go1_config import Go1RoughCfg
+    c = Go1RoughCfg()
+    c.env.num_observations = 235
+    c.terrain.mesh_type = "trimesh"
+    c.terrain.measure_heights = True
+    c.terrain.curriculum = True
+    return c
+
+
+def anymal_rough():
+    from legged_gym.envs.anymal_c.mixed_terrains.anymal_c_rough_config import AnymalCRoughCfg
+    return AnymalCRoughCfg()
+
+
+if __name__ == "__main__":
+    cases = sys.argv[1:] or ["go1_flat", "go1_rough", "anymal_c_rough"]
+    if "go1_flat" in cases:
+        run_case("go1_flat", "Go1", go1_flat, 24, 24, 1, "go1_model.json")
+    if "go1_rough" in cases:
+        run_case("go1_rough", "Go1", go1_rough, 12, 12, 2, "go1_model.json")
+    if "anymal_c_rough" in cases:
+        run_case("anymal_c_rough", "Anymal", anymal_rough, 12, 12, 3, "anymal_c_model.json")
