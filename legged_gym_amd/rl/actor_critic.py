@@ -22,13 +22,48 @@ def get_activation(name):
     return table[name]
 
 
+class _SplitKLinearFn(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is computed as S batched partial products summed
+    over S (split-K over the PPO minibatch dimension).  The library's single GEMM for
+    dW = dY^T X at M = 24576 rows launches only (out/32 x in/256) tiles and runs at ~20 TFLOP/s;
+    S = 8 partial GEMMs fill the 256 CUs (2-5x faster on MI355X, tools/ubench.py)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, splits):
+        ctx.save_for_backward(x, w)
+        ctx.splits = splits
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        S = ctx.splits
+        gx = gy @ w if ctx.needs_input_grad[0] else None
+        M, N = gy.shape
+        K = x.shape[1]
+        gw = torch.bmm(gy.reshape(S, M // S, N).transpose(1, 2), x.reshape(S, M // S, K)).sum(0)
+        gb = gy.sum(0)
+        return gx, gw, gb, None
+
+
+class LgxLinear(nn.Linear):
+    """nn.Linear (same parameters / state_dict) with the split-K weight gradient on GPU."""
+
+    def forward(self, x):
+        if x.is_cuda and torch.is_grad_enabled() and x.dim() == 2 and x.shape[0] >= 4096:
+            for s in (8, 4, 2):
+                if x.shape[0] % s == 0:
+                    return _SplitKLinearFn.apply(x, self.weight, self.bias, s)
+        return super().forward(x)
+
+
 def _mlp(n_in, hidden, n_out, act):
-    layers = [nn.Linear(n_in, hidden[0]), act]
+    layers = [LgxLinear(n_in, hidden[0]), act]
     for i in range(len(hidden)):
         if i == len(hidden) - 1:
-            layers.append(nn.Linear(hidden[i], n_out))
+            layers.append(LgxLinear(hidden[i], n_out))
         else:
-            layers += [nn.Linear(hidden[i], hidden[i + 1]), act]
+            layers += [LgxLinear(hidden[i], hidden[i + 1]), act]
     return nn.Sequential(*layers)
 
 

@@ -291,3 +291,19 @@ def test_gae_kernel_matches_torch_loop(gpu):
     assert ok, f"returns max err {e}"
     ok, e = close(st_g.advantages, st_c.advantages, 1e-4, 1e-4)
     assert ok, f"advantages max err {e}"
+
+
+def test_splitk_linear_gradients_match_torch(gpu):
+    from legged_gym_amd.rl.actor_critic import LgxLinear
+    torch.manual_seed(0)
+    lin = LgxLinear(235, 512).to(gpu)
+    ref = torch.nn.Linear(235, 512).to(gpu)
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(24576, 235, device=gpu, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    g = torch.randn(24576, 512, device=gpu)
+    (lin(x) * g).sum().backward()
+    (ref(x2) * g).sum().backward()
+    for a, b in ((lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad), (x.grad, x2.grad)):
+        ok, e = close(a, b, 1e-2, 1e-4)
+        assert ok, f"split-K grad max err {e}"
