@@ -181,11 +181,9 @@ int lgx_step(lgx_sim* s, int64_t step, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_step: null sim");
   hipStream_t st = (hipStream_t)stream;
   const lgx_env_params& p = s->params;
-  int rc = launch_check(lgx_launch_clip_actions(s->bufs.actions, (int64_t)p.num_envs * 12, p.clip_actions, st),
-                        "lgx_step: clip launch");
-  if (rc) return rc;
+  // action clipping is fused into the physics kernel's action load
   mark(s, 0, st);
-  rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, st),
+  int rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, st),
                     "lgx_step: physics launch");
   mark(s, 0, st);
   if (rc) return rc;

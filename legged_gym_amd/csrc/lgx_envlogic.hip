@@ -4,9 +4,9 @@
 // with no host synchronisation (the reference's reset_buf.nonzero() and per-term launches
 // are replaced by per-env predication and a deterministic two-stage reduction for extras).
 //
-// Block = 256 threads owns 64 envs.  Phases:
+// Block = 256 threads owns 16 envs (256 workgroups at 4096 envs).  Phases:
 //   A  (all 256 lanes) height scan: (env, point) pairs, coalesced int16 gathers
-//   B  (lanes 0..63)   one env per lane: scalar logic, rewards, reset
+//   B  (lanes 0..15)   one env per lane: scalar logic, rewards, reset
 //   C  (all 256 lanes) observation rows: (env, obs index) pairs, coalesced stores
 // Extras (episode means over reset envs) are reduced per block in LDS, then by a one-block
 // finalize kernel in fixed order (bitwise reproducible).
@@ -182,7 +182,7 @@ LGX_DEV void reset_env(const lgx_env_params* __restrict__ P, const lgx_buffers& 
 LGX_DEV void block_partials(float (*lds)[LGX_PARTIAL_STRIDE], int nrows, float* partial_out) {
   __syncthreads();
   int t = threadIdx.x;
-  if (t < nrows + 1) {
+  if (t < nrows + 2) {  // term sums, reset count, terrain-level sum
     float s = 0.f;
     for (int i = 0; i < LGX_ENV_BLOCK; ++i) s += lds[i][t];
     partial_out[t] = s;
@@ -291,6 +291,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
         reset_env(P, B, D, e, step, 0u, true, v.cmd);
       }
       for (int k = 0; k < 4; ++k) cmd_g[k] = v.cmd[k];
+      if (P->curriculum) part[tid][T + 1] = (float)B.terrain_levels[e];
       float* o3 = B.base_lin_vel + (int64_t)e * 3;
       o3[0] = v.blv.x; o3[1] = v.blv.y; o3[2] = v.blv.z;
       o3 = B.base_ang_vel + (int64_t)e * 3;
@@ -360,33 +361,39 @@ lgx_reset_idx_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, const 
   block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
 }
 
-// extras finalize: deterministic sum of block partials; publish only if >= 1 env reset
+// extras finalize: deterministic sum of block partials; publish only if >= 1 env reset.
+// level_scan: sum terrain levels over all envs here (reset_idx path) instead of partials.
 __global__ void __launch_bounds__(256)
-lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks) {
+lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks, int32_t level_scan) {
   const int N = P->num_envs;
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
   __shared__ float red[256];
   __shared__ float sums[LGX_PARTIAL_STRIDE];
   int t = threadIdx.x;
-  if (t <= T) {
+  // 256 threads: each (row, block-slice) pair accumulates, fixed order -> reproducible
+  const int rows = T + 2;
+  for (int r = 0; r < rows; ++r) {
     float s = 0.f;
-    for (int b = 0; b < nblocks; ++b) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + t];
-    sums[t] = s;
-  }
-  float lv = 0.f;
-  if (P->curriculum)
-    for (int e = t; e < N; e += 256) lv += (float)B.terrain_levels[e];
-  red[t] = lv;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (t < w) red[t] += red[t + w];
+    if (r == T + 1 && level_scan) {
+      if (P->curriculum)
+        for (int e = t; e < N; e += 256) s += (float)B.terrain_levels[e];
+    } else {
+      for (int b = t; b < nblocks; b += 256) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + r];
+    }
+    red[t] = s;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (t < w) red[t] += red[t + w];
+      __syncthreads();
+    }
+    if (t == 0) sums[r] = red[0];
     __syncthreads();
   }
   float count = sums[T];
   if (count <= 0.f) return;  // reference keeps stale extras (legged_robot.py:160-161)
   if (t < T) B.extras[t] = (sums[t] / count) / P->max_episode_length_s;
   if (t == 0) {
-    if (P->curriculum) B.extras[T] = red[0] / (float)N;
+    if (P->curriculum) B.extras[T] = sums[T + 1] / (float)N;
     B.extras[T + 1] = count;
   }
   if (P->send_timeouts)
@@ -399,7 +406,7 @@ int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int3
   (void)num_obs; (void)n_term_rows; (void)measure_heights;
   int blocks = (n_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
   hipLaunchKernelGGL(lgx_post_physics_kernel, dim3(blocks), dim3(ENV_THREADS), 0, stream, dp, b, step, draws);
-  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks);
+  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 0);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -411,6 +418,6 @@ int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t
   int blocks = (n + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
   hipLaunchKernelGGL(lgx_reset_idx_kernel, dim3(blocks), dim3(LGX_ENV_BLOCK), 0, stream, dp, b, ids, n, step,
                      init_done, draws);
-  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks);
+  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 1);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

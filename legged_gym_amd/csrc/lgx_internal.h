@@ -4,7 +4,7 @@
 
 #include "../../include/lgx.h"
 
-#define LGX_MAX_LANE_PTS 48
+#define LGX_MAX_LANE_PTS 32
 
 // device-resident model: the ABI model + the per-lane (per-leg) contact candidate tables
 struct lgx_dev_model {
@@ -36,5 +36,5 @@ int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, con
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream);
 
 // scratch layout (floats): [blocks][LGX_MAX_TERMS + 2] reduction partials
-#define LGX_ENV_BLOCK 64
+#define LGX_ENV_BLOCK 16
 #define LGX_PARTIAL_STRIDE (LGX_MAX_TERMS + 2)

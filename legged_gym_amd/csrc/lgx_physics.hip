@@ -11,6 +11,8 @@
 // is formed with two quad shuffles per entry and solved redundantly in all 4 lanes; the
 // leg back-substitution is lane-local again.  All state stays in VGPRs across substeps;
 // HBM traffic per env-step = state in + state out (+ actuator-net history).
+#include <stdlib.h>
+
 #include "lgx_device.h"
 #include "lgx_internal.h"
 
@@ -220,22 +222,51 @@ LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon,
 
 }  // namespace
 
-#define PHYS_BLOCK 64
-#define MAX_LANE_PTS 48
+#define MAX_LANE_PTS 32
+#define HIST_STRIDE 31
 
-__global__ void __launch_bounds__(PHYS_BLOCK)
-lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* __restrict__ P, lgx_buffers B,
+// sum over the PP lanes that share a leg (lane bits 2..): contact terms were split across them
+template <int PP>
+LGX_DEV float psum(float v) {
+  if (PP >= 2) v += __shfl_xor(v, 4);
+  if (PP >= 4) v += __shfl_xor(v, 8);
+  return v;
+}
+
+// PP lanes per leg, 4*PP lanes per env: lane = env*4PP + p*4 + leg.  Every lane of a leg
+// group computes the leg's dynamics (identical values, no extra time); the contact candidates
+// of the leg are dealt round-robin over its PP lanes and their J^T W J terms reduced with
+// shuffles, so the serial contact work per lane shrinks PP-fold while the chip gets PP x
+// more waves (4096 envs x 16 lanes = 1024 waves for PP = 4: all 4 SIMDs of every CU busy).
+template <int PP>
+__global__ void __launch_bounds__(64 * PP)
+lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* __restrict__ P, lgx_buffers B,
                    int32_t nsub, int32_t from_actions) {
-  const lgx_model* __restrict__ M = &DM->m;
+  constexpr int PHYS_BLOCK = 64 * PP;               // 16 envs per workgroup
+  constexpr int LPE = 4 * PP;                       // lanes per env
+  constexpr int SLOTS = (MAX_LANE_PTS + PP - 1) / PP;
+  __shared__ lgx_dev_model smodel;                  // model tables staged once per workgroup
+  __shared__ float4 slot_state[PHYS_BLOCK][SLOTS];  // per own candidate: status, fslide.xyz
+  __shared__ float hist_lds[PHYS_BLOCK * HIST_STRIDE]; // Go1 actuator history of the lane's leg
+  {
+    const int4* src = reinterpret_cast<const int4*>(DMg);
+    int4* dst = reinterpret_cast<int4*>(&smodel);
+    for (int i = threadIdx.x; i < (int)(sizeof(lgx_dev_model) / 16); i += PHYS_BLOCK) dst[i] = src[i];
+    __syncthreads();
+  }
+  const lgx_dev_model* DM = &smodel;
+  const lgx_model* M = &smodel.m;
   const int tid = threadIdx.x;
   const int gl = blockIdx.x * PHYS_BLOCK + tid;
-  const int e = gl >> 2;
-  const int leg = gl & 3;
+  const int e = gl / LPE;
+  const int lie = gl % LPE;
+  const int leg = lie & 3;
+  const int pl = lie >> 2;                          // lane index within the leg group
   const bool lane0 = leg == 0;
+  const bool owner = pl == 0;                       // writes the leg's outputs
   const int N = P->num_envs;
   const bool valid = e < N;
-  const int ec = valid ? e : N - 1;  // inactive quads compute on a clamped env, never store
-  __shared__ float4 slot_state[PHYS_BLOCK][MAX_LANE_PTS];  // per candidate: status, fslide.xyz
+  const int ec = valid ? e : N - 1;  // inactive lanes compute on a clamped env, never store
 
   const float dt = M->sim_dt;
   // ---- load state
@@ -254,12 +285,12 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
   for (int k = 0; k < 3; ++k) mscale[1 + k] = B.body_mass_scale[(int64_t)ec * 13 + 1 + 3 * leg + k];
   const float mu = 0.5f * ((B.friction ? B.friction[ec] : 1.0f) + M->ground_friction);
   const int ctrl = P->control_type;
-  float hist[30];
+  float* hist = hist_lds + threadIdx.x * HIST_STRIDE;
   const bool use_hist = from_actions && P->use_actuator_history;
-  if (from_actions) {
+  if (from_actions) {  // clip (legged_robot.py:85-86) fused into the load
     const float* a = B.actions + (int64_t)ec * 12 + leg * 3;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) act[k] = a[k];
+    for (int k = 0; k < 3; ++k) act[k] = clampf(a[k], -P->clip_actions, P->clip_actions);
   }
   if (ctrl == LGX_CTRL_POS_DRIVE) {
 #pragma unroll
@@ -295,7 +326,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
         hist[10 * k + 4] = pes;
         hist[10 * k + 9] = vs;
       }
-      if (valid) {
+      if (valid && owner) {
         float* mi = B.model_ins + ((int64_t)s * N + e) * 120 + leg * 30;
 #pragma unroll
         for (int i = 0; i < 30; i += 2) *reinterpret_cast<float2*>(mi + i) = make_float2(hist[i], hist[i + 1]);
@@ -445,13 +476,15 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
     float xb[6];
     f3 xl;
     for (int pass = 0; pass < 2; ++pass) {
-      LegSys L = L0;
+      LegSys L;  // this lane's contact terms
 #pragma unroll
       for (int i = 0; i < 21; ++i) L.Ap[i] = 0.f;
 #pragma unroll
-      for (int i = 0; i < 6; ++i) L.rb[i] = rb0[i];
-      L.rl[0] = rl0[0]; L.rl[1] = rl0[1]; L.rl[2] = rl0[2];
-      for (int c = 0; c < maxpts; ++c) {
+      for (int i = 0; i < 6; ++i) { L.rb[i] = 0.f; L.B[i][0] = L.B[i][1] = L.B[i][2] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) L.D[i] = 0.f;
+      L.rl[0] = L.rl[1] = L.rl[2] = 0.f;
+      for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
         if (c >= npts) break;
         int pi = DM->lane_pts[leg][c];
         int db = M->point_dyn[pi];
@@ -463,8 +496,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
         float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
         float rad = M->point_radius[pi];
         float depth = (h - (Pp.z + pos.z)) * n.z + rad;
-        float4 st = slot_state[tid][c];
-        if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[tid][c] = st; }
+        float4 st = slot_state[tid][sl];
+        if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[tid][sl] = st; }
         if (depth <= 0.f || st.x == 0.f) continue;
         f3 Pc = Pp - rad * n;
         float wt = (pass == 0 || st.x == 1.f) ? dt * ct : 0.f;
@@ -472,6 +505,18 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
         if (pass == 1 && st.x == 2.f) f = f + dt * mk3(st.y, st.z, st.w);
         add_contact(L, Pc, n, wn, wt, f, k, S);
       }
+      // reduce the contact terms over the PP lanes of the leg, add the contact-free system
+#pragma unroll
+      for (int i = 0; i < 21; ++i) L.Ap[i] = psum<PP>(L.Ap[i]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        L.rb[i] = psum<PP>(L.rb[i]) + rb0[i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) L.B[i][k] = psum<PP>(L.B[i][k]) + L0.B[i][k];
+        L.D[i] = psum<PP>(L.D[i]) + L0.D[i];
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + rl0[k];
       arrow_solve(L, Acom, rbcom, lane0, xb, xl);
       // contact status (after pass 0) / reported forces (after pass 1, last substep)
       const bool report = pass == 1 && s == nsub - 1;
@@ -481,9 +526,9 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
         Vl[0] = add(Vb, scale(xl.x, S[0]));
         Vl[1] = add(Vl[0], scale(xl.y, S[1]));
         Vl[2] = add(Vl[1], scale(xl.z, S[2]));
-        for (int c = 0; c < maxpts; ++c) {
+        for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
           if (c >= npts) break;
-          float4 st = slot_state[tid][c];
+          float4 st = slot_state[tid][sl];
           if (st.x == 0.f) continue;
           int pi = DM->lane_pts[leg][c];
           int db = M->point_dyn[pi];
@@ -508,7 +553,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
               float sc = -mu * fn / vtn;
               st = make_float4(2.f, sc * vt.x, sc * vt.y, sc * vt.z);
             } else st.x = 1.f;
-            slot_state[tid][c] = st;
+            slot_state[tid][sl] = st;
           } else {
             fn = fmaxf(fn, 0.f);
             f3 ft = st.x == 1.f ? (-ct) * vt : mk3(st.y, st.z, st.w);
@@ -560,8 +605,14 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DM, const lgx_env_params* _
   }
 
   // ---- write back
-  cf_base = mk3(quad_sum(cf_base.x), quad_sum(cf_base.y), quad_sum(cf_base.z));
-  if (!valid) return;
+  cf_base = mk3(psum<PP>(quad_sum(cf_base.x)), psum<PP>(quad_sum(cf_base.y)), psum<PP>(quad_sum(cf_base.z)));
+#pragma unroll
+  for (int r = 0; r < 4; ++r) cf_leg[r] = mk3(psum<PP>(cf_leg[r].x), psum<PP>(cf_leg[r].y), psum<PP>(cf_leg[r].z));
+  if (!valid || !owner) return;
+  if (from_actions) {
+    float* ao = B.actions + (int64_t)e * 12 + leg * 3;
+    ao[0] = act[0]; ao[1] = act[1]; ao[2] = act[2];
+  }
   float* dso = B.dof_state + (int64_t)e * 24 + leg * 6;
 #pragma unroll
   for (int k = 0; k < 3; ++k) *reinterpret_cast<float2*>(dso + 2 * k) = make_float2(th[k], thd[k]);
@@ -600,8 +651,17 @@ __global__ void lgx_clip_actions_kernel(float* a, int64_t n, float clip) {
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                        int32_t nsub, int32_t from_actions, hipStream_t stream) {
-  int blocks = (n_envs * 4 + PHYS_BLOCK - 1) / PHYS_BLOCK;
-  hipLaunchKernelGGL(lgx_physics_kernel, dim3(blocks), dim3(PHYS_BLOCK), 0, stream, dm, dp, b, nsub, from_actions);
+  // lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches
+  const int pp = n_envs >= 16384 ? 1 : (n_envs >= 8192 ? 2 : 4);
+  const char* force = getenv("LGX_PHYS_PP");  // A/B switch for measurements
+  const int ppx = force ? atoi(force) : pp;
+  const int blocks = (n_envs + 15) / 16;       // 16 envs per workgroup of 64*PP lanes
+  if (ppx == 4)
+    hipLaunchKernelGGL(lgx_physics_kernel<4>, dim3(blocks), dim3(256), 0, stream, dm, dp, b, nsub, from_actions);
+  else if (ppx == 2)
+    hipLaunchKernelGGL(lgx_physics_kernel<2>, dim3(blocks), dim3(128), 0, stream, dm, dp, b, nsub, from_actions);
+  else
+    hipLaunchKernelGGL(lgx_physics_kernel<1>, dim3(blocks), dim3(64), 0, stream, dm, dp, b, nsub, from_actions);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -66,9 +66,27 @@ def env_bench(task="go1_rough", n=4096):
     print(f"{task} env.step N={n}: {ms*1e3:.1f} us/step  {n/ms*1e3/1e6:.2f} M env-steps/s (env only)")
 
 
+def phys_ab():
+    """A/B the physics kernel lanes-per-leg variants in one process."""
+    import ctypes as C
+    from oracle_backend import make_env
+    for task in ("go1_flat_bench", "go1_rough"):
+        env = make_env(task, num_envs=4096, device="cuda:0", backend="lgx")
+        env.reset()
+        for pp in ("1", "2", "4", "1", "2", "4"):
+            os.environ["LGX_PHYS_PP"] = pp
+            ms = timeit(lambda: env.simulate(4), iters=20)
+            print(f"{task} physics 4 substeps N=4096 PP={pp}: {ms*1e3:.1f} us")
+        os.environ.pop("LGX_PHYS_PP")
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["mlp", "env"]
     if "mlp" in what:
         mlp_bench()
     if "env" in what:
         env_bench()
+    if "phys" in what:
+        phys_ab()
+
+
