@@ -22,8 +22,14 @@ sys.path.insert(0, ROOT)
 # algorithmic work per env-step: physics kernel = fused 4 substeps (VALU),
 # actuator MLP = 4 substeps x 4 legs x 2 x (30*128 + 128*128*2 + 128*3) FLOP
 ACT_MLP_FLOP_PER_ENV_STEP = 4 * 4 * 2 * (30 * 128 + 128 * 128 * 2 + 128 * 3)
-MI355X_F32_MFMA_PEAK_TFLOPS = 157.3
+MI355X_F32_PEAK_TFLOPS = 157.3      # vector FP32 == f32 MFMA peak (MI355X_MICROARCH.md)
 MI355X_HBM_PEAK_GBS = 8000.0
+# HBM bytes per physics launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE
+# counts half of wide reads), rocprofv3 --pmc passes in profiles/r01_pmc_env_kernels.json
+PHYS_PMC_TRAFFIC_BYTES = int((2 * 6592.1 + 19206.3) * 1024)
+
+
+from legged_gym_amd.sim.flops import physics_flop_per_env_substep  # noqa: E402
 
 
 def parse():
@@ -117,19 +123,27 @@ def main():
     steps_per_iter = runner.num_steps_per_env
     value = steps_per_iter * N * world * args.steps / elapsed
 
-    # roofline of the dominant lgx kernel class (HIP-event durations over the timed region)
+    # roofline of the dominant lgx kernel (HIP-event durations over the timed region)
     names = ["lgx_physics_kernel", "lgx_mlp_forward_kernel(actuator)", "lgx_post_physics_kernel"]
     avg = [ms[i] / cnt[i] if cnt[i] else 0.0 for i in range(3)]
     dom = max(range(3), key=lambda i: ms[i])
-    act_avg_ms = avg[1]
+    decim = env.cfg.control.decimation
+    phys_flop = N * decim * physics_flop_per_env_substep(
+        env._lgx_model.num_points, 4.0, env.cfg.terrain.mesh_type in ("heightfield", "trimesh"))
+    roof = {"kernel": names[0], "bound": "mfma", "compute_pipe": "fp32 VALU",
+            "achieved": (phys_flop / (avg[0] * 1e-3) / 1e12) if avg[0] else None,
+            "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "traffic": PHYS_PMC_TRAFFIC_BYTES if (N == 4096 and args.task == "go1_rough") else None,
+            "algorithmic_per_launch": phys_flop,
+            "note": ("compute roof = FP32 peak (vector FP32 = f32 MFMA = 157.3 TF on gfx950); algorithmic FLOP "
+                     "from legged_gym_amd/sim/flops.py x envs x substeps; traffic = FETCH_SIZE*2 + WRITE_SIZE "
+                     "per launch from profiles/r01_pmc_env_kernels.json; latency-bound, see DESIGN.md 4.1")}
     act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
-    roof = {"kernel": names[1], "bound": "mfma",
-            "achieved": (act_flop / (act_avg_ms * 1e-3) / 1e12) if act_avg_ms else None,
-            "peak": MI355X_F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "traffic": None,
-            "note": ("actuator-net MLP (f32 MFMA) launch; dominant lgx kernel class by time is "
-                     f"{names[dom]} ({avg[dom]:.3f} ms/launch, VALU-bound physics, see DESIGN.md §5)")}
-    if roof["achieved"] is not None:
-        roof["frac"] = roof["achieved"] / roof["peak"]
+    roof2 = {"kernel": names[1], "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None}
+    for r in (roof, roof2):
+        if r["achieved"] is not None:
+            r["frac"] = r["achieved"] / r["peak"]
     it_ms = 1000.0 * elapsed / args.steps
     kernels = {n: {"avg_ms": round(a, 4), "launches": int(c), "share_of_iteration": round(m / args.steps / it_ms, 4)}
                for n, a, c, m in zip(names, avg, cnt, ms)}
@@ -142,6 +156,8 @@ def main():
                                f"actuator-net history+MLP, PPO 24 steps x {N} envs/GPU, 5 epochs x 4 minibatches",
                    "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
         "roofline": roof,
+        "roofline_secondary": roof2,
+        "dominant_lgx_kernel": names[dom],
         "lgx_kernels": kernels,
         "last_iteration": runner.last_iteration_stats,
     }

@@ -80,6 +80,17 @@ def phys_ab():
         os.environ.pop("LGX_PHYS_PP")
 
 
+def phys_run(task="go1_rough", n=4096, steps=10):
+    """Short env-step loop for PMC collection (rocprofv3 --pmc): 10 env steps after reset."""
+    from oracle_backend import make_env
+    env = make_env(task, num_envs=n, device="cuda:0", backend="lgx")
+    env.reset()
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    for _ in range(steps):
+        env.step(torch.randn(n, 12, device="cuda:0", generator=g) * 0.5)
+    torch.cuda.synchronize()
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["mlp", "env"]
     if "mlp" in what:
@@ -88,5 +99,7 @@ if __name__ == "__main__":
         env_bench()
     if "phys" in what:
         phys_ab()
+    if "physrun" in what:
+        phys_run()
 
 
