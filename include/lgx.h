@@ -198,8 +198,9 @@ typedef struct lgx_sim lgx_sim;
 const char* lgx_last_error(void);
 int lgx_version(void);
 
-/* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers): lets bindings verify layout */
-void lgx_struct_sizes(int64_t out[3]);
+/* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers), sizeof(lgx_mlp_desc),
+ * sizeof(lgx_ppo_loss_args), sizeof(lgx_reduce_job): lets bindings verify layout */
+void lgx_struct_sizes(int64_t out[6]);
 
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
@@ -277,6 +278,79 @@ int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
  * returns, advantages (= returns - values) [T,N]. */
 int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_values, float* returns,
             float* advantages, int32_t T, int32_t N, float gamma, float lam, void* stream);
+
+/* ---- PPO update (rsl_rl PPO.update, legged_robot_config.py:226-239): the non-GEMM work of a
+ * minibatch step.  Activations are net-major [2 (actor, critic), M, H]; the GEMMs between
+ * these calls are library GEMMs issued by the host.  All pointers are device pointers. */
+#define LGX_PPO_MAX_ACTIONS 16
+#define LGX_MAX_REDUCE_JOBS 8
+
+/* dst[r, :] = src[idx[r], :] for r < rows (minibatch gather of storage rows) */
+int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width, void* stream);
+
+/* z[n, r, c] = act(z[n, r, c] + b[n, c]) in place; act 0 none, 1 ELU, 2 tanh; cols % 4 == 0 */
+int lgx_bias_act(float* z, const float* b, int64_t rows, int32_t cols, int32_t nets, int32_t act, void* stream);
+
+typedef struct lgx_ppo_loss_args {
+  int64_t rows;                 /* M, minibatch size */
+  int32_t num_actions;          /* A <= LGX_PPO_MAX_ACTIONS */
+  int32_t use_clipped_value_loss;
+  float clip_param, value_loss_coef, entropy_coef;
+  const int64_t* idx;           /* storage row of minibatch row r (NULL: identity) */
+  const float* mu_raw;          /* [M,A] actor output before its bias */
+  const float* v_raw;           /* [M]   critic output before its bias */
+  const float* b4a;             /* [A] */
+  const float* b4c;             /* [1] */
+  const float* std;             /* [A] action std parameter */
+  /* storage (indexed by idx): */
+  const float* actions;         /* [*,A] */
+  const float* old_logp;        /* [*] */
+  const float* old_mu;          /* [*,A] */
+  const float* old_sigma;       /* [*,A] */
+  const float* advantages;      /* [*] normalised */
+  const float* target_values;   /* [*] */
+  const float* returns;         /* [*] */
+  /* outputs */
+  float* d_mu;                  /* [M,A] d loss / d mu */
+  float* d_v;                   /* [M]   d loss / d value */
+  float* partials;              /* [lgx_ppo_loss_partials_floats(M, A)] */
+  float* g_std;                 /* [A] gradient slots in the flat gradient buffer */
+  float* g_b4a;                 /* [A] */
+  float* g_b4c;                 /* [1] */
+  float* stats;                 /* [3]: KL mean (this minibatch), += surrogate mean, += value-loss mean */
+} lgx_ppo_loss_args;
+int64_t lgx_ppo_loss_partials_floats(int64_t rows, int32_t num_actions);
+/* loss = mean(max(-adv r, -adv clip(r))) + c_v mean(value loss) - c_e mean(entropy), with its
+ * gradient (torch autograd tie conventions) and the adaptive-schedule KL */
+int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream);
+
+/* adaptive schedule on the device: lr (double) from KL = kl_sum[0] * kl_scale */
+int lgx_ppo_adapt_lr(const float* kl_sum, float kl_scale, double* lr, double desired_kl, void* stream);
+
+/* output layers backward: partials per 64-row chunk [A*H dW4a | H dW4c | 2H db3];
+ * A3 [2,M,H] (post-ELU) is overwritten by dZ3 */
+int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_actions, int32_t hidden);
+int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3, int64_t rows,
+                 int32_t num_actions, int32_t hidden, float* partials, void* stream);
+
+/* dA [nets,M,H] -> dA * elu'(Y) in place (Y = ELU output) + per-chunk column sums */
+int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int32_t nets);
+int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32_t hidden, int32_t nets, float* partials,
+                       void* stream);
+
+/* dst[j*dst_stride + i] = sum_{s<slices} src[j*job_stride + s*slice_stride + i], i < n, j < count */
+typedef struct lgx_reduce_job {
+  const float* src;
+  float* dst;
+  int64_t n, job_stride, slice_stride, dst_stride;
+  int32_t slices, count;
+} lgx_reduce_job;
+int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream);
+
+/* clip_grad_norm_(max_norm) of (grad_scale * g) fused into torch-Adam (no weight decay) over
+ * one flat parameter buffer; *step is advanced on the device; lr is a device double */
+int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts, float grad_scale,
+                  float max_norm, const double* lr, int64_t* step, float beta1, float beta2, float eps, void* stream);
 
 #ifdef __cplusplus
 }

@@ -23,6 +23,8 @@ static int hip_check(hipError_t e, const char* what) {
   g_err = buf;
   return LGX_EHIP;
 }
+int lgx_fail(int code, const char* msg) { return fail(code, msg); }
+int lgx_hip_status(const char* what) { return hip_check(hipGetLastError(), what); }
 static int launch_check(int rc, const char* what) {
   if (rc == 0) return 0;
   if (rc == -1) return fail(LGX_EINVAL, what);
@@ -61,10 +63,13 @@ extern "C" {
 const char* lgx_last_error(void) { return g_err.c_str(); }
 int lgx_version(void) { return 1; }
 
-void lgx_struct_sizes(int64_t out[3]) {
+void lgx_struct_sizes(int64_t out[6]) {
   out[0] = (int64_t)sizeof(lgx_model);
   out[1] = (int64_t)sizeof(lgx_env_params);
   out[2] = (int64_t)sizeof(lgx_buffers);
+  out[3] = (int64_t)sizeof(lgx_mlp_desc);
+  out[4] = (int64_t)sizeof(lgx_ppo_loss_args);
+  out[5] = (int64_t)sizeof(lgx_reduce_job);
 }
 
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms) {

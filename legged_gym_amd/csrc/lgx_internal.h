@@ -35,6 +35,15 @@ int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t st
 int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream);
 
+// error reporting shared by the translation units (thread-local message, lgx_last_error)
+int lgx_fail(int code, const char* msg);
+int lgx_hip_status(const char* what);  // LGX_OK or LGX_EHIP from hipGetLastError()
+
+// a batch of reduction jobs passed by value to one launch (lgx_reduce_slices)
+struct lgx_reduce_jobs {
+  lgx_reduce_job job[LGX_MAX_REDUCE_JOBS];
+};
+
 // scratch layout (floats): [blocks][LGX_MAX_TERMS + 2] reduction partials
 #define LGX_ENV_BLOCK 16
 #define LGX_PARTIAL_STRIDE (LGX_MAX_TERMS + 2)

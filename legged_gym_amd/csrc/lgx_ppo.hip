@@ -1,0 +1,441 @@
+// lgx PPO update kernels: everything of one rsl_rl PPO minibatch step (rsl_rl v1.0.x
+// `PPO.update`, configured by legged_robot_config.py:226-239) that is not a GEMM:
+//   - minibatch row gather,
+//   - bias + ELU epilogue of the actor/critic hidden layers (net-major [2, M, H] activations),
+//   - the PPO loss and its analytic gradient w.r.t. the action mean, value and std
+//     (clipped surrogate, clipped value loss, entropy bonus; Normal(mu, std) log-prob), with
+//     the KL used by the adaptive learning-rate schedule,
+//   - output-layer backward (dZ3 = (dMU W4) * elu'(A3), dW4, db3 partials),
+//   - ELU backward fused with the bias-gradient column sums,
+//   - split-K / per-chunk partial reductions straight into the flat gradient buffer,
+//   - global-norm gradient clipping (clip_grad_norm_) fused into the Adam step.
+// The GEMMs between them stay on hipBLASLt through torch (mm / bmm).  All reductions are
+// two-stage in a fixed order (bitwise reproducible); the adaptive learning rate and the Adam
+// step counter live on the device so a whole update can be captured in one hipGraph.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+
+#include "lgx_internal.h"
+
+namespace {
+
+constexpr int TPB = 256;
+constexpr int CHUNK = 64;  // rows per workgroup in the backward epilogues
+
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+__device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
+
+// ---------------------------------------------------------------------------------------- gather
+__global__ void __launch_bounds__(TPB)
+gather_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, const int64_t* __restrict__ idx,
+                   int64_t rows, int32_t width) {
+  // one row per 64-lane wave, 4 rows per workgroup
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* s = src + idx[r] * width;
+  float* d = dst + r * width;
+  for (int c = lane; c < width; c += 64) d[c] = s[c];
+}
+
+// ---------------------------------------------------------------------------------------- bias + act
+__global__ void __launch_bounds__(TPB)
+bias_act_kernel(float* __restrict__ z, const float* __restrict__ b, int64_t rows, int32_t cols, int32_t nets,
+                int32_t act) {
+  const int64_t per_net = rows * cols;
+  const int64_t n4 = per_net * nets / 4;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n4; i += (int64_t)gridDim.x * TPB) {
+    int64_t e = i * 4;
+    int net = (int)(e / per_net);
+    int c = (int)(e % cols);
+    float4 v = reinterpret_cast<float4*>(z)[i];
+    const float* bb = b + net * cols + c;
+    v.x += bb[0]; v.y += bb[1]; v.z += bb[2]; v.w += bb[3];
+    if (act == 1) { v.x = elu_f(v.x); v.y = elu_f(v.y); v.z = elu_f(v.z); v.w = elu_f(v.w); }
+    else if (act == 2) { v.x = tanhf(v.x); v.y = tanhf(v.y); v.z = tanhf(v.z); v.w = tanhf(v.w); }
+    reinterpret_cast<float4*>(z)[i] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------- loss
+// One row per thread.  Partials per workgroup (row sums, fixed-order tree-free reduction):
+//   [0, A)      d loss / d std_j          (log-prob path; the entropy term is added in finalize)
+//   [A, 2A)     d loss / d b4a_j          (= sum of dMU over rows)
+//   2A          d loss / d b4c            (= sum of dV)
+//   2A+1        KL sum, 2A+2 surrogate sum, 2A+3 value-loss sum
+__global__ void __launch_bounds__(TPB)
+ppo_loss_kernel(lgx_ppo_loss_args a) {
+  constexpr int MAXA = LGX_PPO_MAX_ACTIONS;
+  const int A = a.num_actions;
+  const int NP = 2 * A + 4;
+  __shared__ float red[TPB][2 * MAXA + 4 + 1];
+  const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  float* my = red[threadIdx.x];
+  for (int k = 0; k < NP; ++k) my[k] = 0.f;
+  if (r < a.rows) {
+    const int64_t g = a.idx ? a.idx[r] : r;
+    const float invM = 1.0f / (float)a.rows;
+    float mu[MAXA], sd[MAXA], act[MAXA];
+    float logp = 0.f, kl = 0.f;
+    const float half_log_2pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
+    for (int j = 0; j < A; ++j) {
+      mu[j] = a.mu_raw[r * A + j] + a.b4a[j];
+      sd[j] = a.std[j];
+      act[j] = a.actions[g * A + j];
+      float var = sd[j] * sd[j];
+      float d = act[j] - mu[j];
+      logp += -(d * d) / (2.f * var) - logf(sd[j]) - half_log_2pi;
+      float so = a.old_sigma[g * A + j], mo = a.old_mu[g * A + j];
+      kl += logf(sd[j] / so + 1.e-5f) + (so * so + (mo - mu[j]) * (mo - mu[j])) / (2.f * var) - 0.5f;
+    }
+    const float adv = a.advantages[g];
+    const float ratio = expf(logp - a.old_logp[g]);
+    const float lo = 1.f - a.clip_param, hi = 1.f + a.clip_param;
+    const float rc = fminf(fmaxf(ratio, lo), hi);
+    const float s1 = -adv * ratio, s2 = -adv * rc;
+    const bool inside = ratio >= lo && ratio <= hi;
+    // torch.maximum backward: ties split the gradient; clamp passes it inside [lo, hi]
+    float dsdr;
+    if (s1 > s2) dsdr = -adv;
+    else if (s1 < s2) dsdr = inside ? -adv : 0.f;
+    else dsdr = 0.5f * (-adv) + 0.5f * (inside ? -adv : 0.f);
+    const float surr = fmaxf(s1, s2);
+    const float dlogp = dsdr * invM * ratio;
+    for (int j = 0; j < A; ++j) {
+      float var = sd[j] * sd[j];
+      float d = act[j] - mu[j];
+      float dm = dlogp * d / var;
+      a.d_mu[r * A + j] = dm;
+      my[A + j] = dm;
+      my[j] = dlogp * (d * d / (var * sd[j]) - 1.f / sd[j]);
+    }
+    // value loss
+    const float v = a.v_raw[r] + a.b4c[0];
+    const float tv = a.target_values[g], ret = a.returns[g];
+    float vl, dv;
+    if (a.use_clipped_value_loss) {
+      float dvt = v - tv;
+      float vc = tv + fminf(fmaxf(dvt, -a.clip_param), a.clip_param);
+      bool vin = dvt >= -a.clip_param && dvt <= a.clip_param;
+      float u1 = (v - ret) * (v - ret), u2 = (vc - ret) * (vc - ret);
+      vl = fmaxf(u1, u2);
+      float g1 = 2.f * (v - ret), g2 = vin ? 2.f * (vc - ret) : 0.f;
+      dv = u1 > u2 ? g1 : (u1 < u2 ? g2 : 0.5f * g1 + 0.5f * g2);
+    } else {
+      vl = (ret - v) * (ret - v);
+      dv = 2.f * (v - ret);
+    }
+    dv *= a.value_loss_coef * invM;
+    a.d_v[r] = dv;
+    my[2 * A] = dv;
+    my[2 * A + 1] = kl;
+    my[2 * A + 2] = surr;
+    my[2 * A + 3] = vl;
+  }
+  __syncthreads();
+  if (threadIdx.x < NP) {
+    float s = 0.f;
+    for (int t = 0; t < TPB; ++t) s += red[t][threadIdx.x];
+    a.partials[(int64_t)blockIdx.x * NP + threadIdx.x] = s;
+  }
+}
+
+// one workgroup: reduce the loss partials, write d std / d b4a / d b4c into the flat gradient,
+// the KL mean and the running loss sums
+__global__ void __launch_bounds__(TPB)
+ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) {
+  const int A = a.num_actions;
+  const int NP = 2 * A + 4;
+  const int k = threadIdx.x;
+  if (k >= NP) return;
+  float s = 0.f;
+  for (int b = 0; b < nblocks; ++b) s += a.partials[(int64_t)b * NP + k];
+  const float invM = 1.0f / (float)a.rows;
+  if (k < A) a.g_std[k] = s - a.entropy_coef / a.std[k];   // entropy: -c_e mean(sum_j log std_j + c)
+  else if (k < 2 * A) a.g_b4a[k - A] = s;
+  else if (k == 2 * A) a.g_b4c[0] = s;
+  else if (k == 2 * A + 1) a.stats[0] = s * invM;          // KL mean of this minibatch (local)
+  else if (k == 2 * A + 2) a.stats[1] += s * invM;         // running surrogate-loss sum
+  else a.stats[2] += s * invM;                             // running value-loss sum
+}
+
+// rsl_rl adaptive schedule (PPO.update): lr /= 1.5 if KL > 2 kl*, *= 1.5 if 0 < KL < kl*/2,
+// bounded [1e-5, 1e-2]; python-float (double) arithmetic as upstream
+__global__ void adapt_lr_kernel(const float* __restrict__ kl_sum, float kl_scale, double* __restrict__ lr,
+                                double desired_kl) {
+  double kl = (double)(kl_sum[0] * kl_scale);
+  double l = lr[0];
+  if (kl > desired_kl * 2.0) l = fmax(1e-5, l / 1.5);
+  else if (desired_kl / 2.0 > kl && kl > 0.0) l = fmin(1e-2, l * 1.5);
+  lr[0] = l;
+}
+
+// ---------------------------------------------------------------------------------------- head bwd
+// per 64-row chunk: dW4 partial = [dMU | dV]^T [A3a | A3c], dZ3 = (dMU W4a | dV w4c) * elu'(A3)
+// written over A3, db3 partial = column sums of dZ3.  Partials row: [A*H (dW4a), H (dW4c), 2H (db3)].
+__global__ void __launch_bounds__(TPB)
+head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, const float* __restrict__ W4a,
+                const float* __restrict__ W4c, float* __restrict__ A3, int64_t rows, int32_t A, int32_t H,
+                float* __restrict__ partials) {
+  extern __shared__ float sm[];
+  float* a3 = sm;                       // [2][CHUNK][H]
+  float* dmu = a3 + 2 * CHUNK * H;      // [CHUNK][A+1]  (last column = dV)
+  float* w4 = dmu + CHUNK * (A + 1);    // [(A+1)][H]
+  const int64_t r0 = (int64_t)blockIdx.x * CHUNK;
+  const int nr = (int)min((int64_t)CHUNK, rows - r0);
+  const int t = threadIdx.x;
+  for (int i = t; i < 2 * CHUNK * H; i += TPB) {
+    int net = i / (CHUNK * H), rem = i % (CHUNK * H), rr = rem / H, c = rem % H;
+    a3[i] = rr < nr ? A3[(int64_t)net * rows * H + (r0 + rr) * H + c] : 0.f;
+  }
+  for (int i = t; i < CHUNK * (A + 1); i += TPB) {
+    int rr = i / (A + 1), j = i % (A + 1);
+    float v = 0.f;
+    if (rr < nr) v = j < A ? d_mu[(r0 + rr) * A + j] : d_v[r0 + rr];
+    dmu[i] = v;
+  }
+  for (int i = t; i < (A + 1) * H; i += TPB) w4[i] = i < A * H ? W4a[i] : W4c[i - A * H];
+  __syncthreads();
+  const int NPr = (A + 1) * H + 2 * H;
+  float* P = partials + (int64_t)blockIdx.x * NPr;
+  // dW4 partial: output (j, c); j < A: actor rows against A3a, j == A: critic against A3c
+  for (int o = t; o < (A + 1) * H; o += TPB) {
+    int j = o / H, c = o % H;
+    const float* col = a3 + (j < A ? 0 : CHUNK * H) + c;
+    float s = 0.f;
+    for (int rr = 0; rr < CHUNK; ++rr) s += dmu[rr * (A + 1) + j] * col[rr * H];
+    P[o] = s;
+  }
+  // dZ3 + db3 partial: thread per (net, column)
+  for (int o = t; o < 2 * H; o += TPB) {
+    int net = o / H, c = o % H;
+    float cs = 0.f;
+    for (int rr = 0; rr < nr; ++rr) {
+      float dA;
+      if (net == 0) {
+        dA = 0.f;
+        for (int j = 0; j < A; ++j) dA += dmu[rr * (A + 1) + j] * w4[j * H + c];
+      } else {
+        dA = dmu[rr * (A + 1) + A] * w4[A * H + c];
+      }
+      float dz = dA * elu_grad_from_out(a3[net * CHUNK * H + rr * H + c]);
+      A3[(int64_t)net * rows * H + (r0 + rr) * H + c] = dz;
+      cs += dz;
+    }
+    P[(A + 1) * H + o] = cs;
+  }
+}
+
+// ---------------------------------------------------------------------------------------- elu bwd
+// dA [nets, rows, H] -> dZ = dA * elu'(Y) in place; partial column sums per 64-row chunk:
+// partials[chunk][net*H + c]
+__global__ void __launch_bounds__(TPB)
+elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64_t rows, int32_t H, int32_t nets,
+                      float* __restrict__ partials) {
+  const int net = blockIdx.y;
+  const int64_t r0 = (int64_t)blockIdx.x * CHUNK;
+  const int nr = (int)min((int64_t)CHUNK, rows - r0);
+  const int64_t base = (int64_t)net * rows * H + r0 * H;
+  float* P = partials + (int64_t)blockIdx.x * nets * H + net * H;
+  for (int c = threadIdx.x; c < H; c += TPB) {
+    float cs = 0.f;
+    for (int rr = 0; rr < nr; ++rr) {
+      int64_t i = base + (int64_t)rr * H + c;
+      float dz = dA[i] * elu_grad_from_out(Y[i]);
+      dA[i] = dz;
+      cs += dz;
+    }
+    P[c] = cs;
+  }
+}
+
+// ---------------------------------------------------------------------------------------- reductions
+// job: dst[j][i] = sum_s src[j*job_stride + s*slice_stride + i] for s < S, i < n, j < count
+__global__ void __launch_bounds__(TPB)
+reduce_slices_kernel(lgx_reduce_jobs jobs) {
+  const lgx_reduce_job& jb = jobs.job[blockIdx.y];
+  const int64_t total = (int64_t)jb.count * jb.n;
+  for (int64_t o = (int64_t)blockIdx.x * TPB + threadIdx.x; o < total; o += (int64_t)gridDim.x * TPB) {
+    int64_t j = o / jb.n, i = o % jb.n;
+    const float* s = jb.src + j * jb.job_stride + i;
+    float acc = 0.f;
+    for (int k = 0; k < jb.slices; ++k) acc += s[(int64_t)k * jb.slice_stride];
+    jb.dst[j * jb.dst_stride + i] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------- clip + Adam
+// stage 1: per-block sums of squares of (scale * g); block 0 also advances the step counter
+__global__ void __launch_bounds__(TPB)
+sumsq_kernel(const float* __restrict__ g, int64_t n, float scale, float* __restrict__ partials,
+             int64_t* __restrict__ step) {
+  __shared__ float red[TPB];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    float v = g[i] * scale;
+    s += v * v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = TPB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x] = red[0];
+    if (blockIdx.x == 0 && step) step[0] += 1;
+  }
+}
+
+// stage 2: every block re-reduces the (few) partials -> global norm -> clip coefficient
+// (torch clip_grad_norm_: coef = min(max_norm / (norm + 1e-6), 1)), then torch Adam
+// (fused form: step_size = lr / bc1; denom = sqrt(v) / sqrt(bc2) + eps)
+__global__ void __launch_bounds__(TPB)
+adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v, int64_t n,
+                 const float* __restrict__ partials, int32_t nparts, float grad_scale, float max_norm,
+                 const double* __restrict__ lr, const int64_t* __restrict__ step, float beta1, float beta2, float eps) {
+  __shared__ float red[TPB];
+  __shared__ float coef_s;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += TPB) s += partials[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = TPB / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float norm = sqrtf(red[0]);
+    float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
+    coef_s = fminf(c, 1.f) * grad_scale;
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  const double t = (double)step[0];
+  const float bc1 = (float)(1.0 - pow((double)beta1, t));
+  const float bc2 = (float)(1.0 - pow((double)beta2, t));
+  const float step_size = (float)(lr[0] / (double)bc1);
+  const float bc2_sqrt = sqrtf(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    float gi = g[i] * coef;
+    g[i] = gi;
+    float mi = beta1 * m[i] + (1.f - beta1) * gi;
+    float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] -= step_size * mi / denom;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- C-ABI
+#define LGX_STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+extern "C" int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width,
+                                   void* stream) {
+  if (!src || !dst || !idx || rows < 0 || width <= 0) return lgx_fail(LGX_EINVAL, "lgx_ppo_gather_rows: bad args");
+  if (rows == 0) return LGX_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(TPB), 0, LGX_STREAM(stream), src, dst,
+                     idx, rows, width);
+  return lgx_hip_status("lgx_ppo_gather_rows");
+}
+
+extern "C" int lgx_bias_act(float* z, const float* b, int64_t rows, int32_t cols, int32_t nets, int32_t act,
+                            void* stream) {
+  if (!z || !b || rows < 0 || cols <= 0 || cols % 4 || nets <= 0 || act < 0 || act > 2)
+    return lgx_fail(LGX_EINVAL, "lgx_bias_act: bad args (cols must be a multiple of 4)");
+  if (rows == 0) return LGX_OK;
+  int64_t n4 = rows * cols * nets / 4;
+  int blocks = (int)std::min<int64_t>((n4 + TPB - 1) / TPB, 4096);
+  hipLaunchKernelGGL(bias_act_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), z, b, rows, cols, nets, act);
+  return lgx_hip_status("lgx_bias_act");
+}
+
+extern "C" int64_t lgx_ppo_loss_partials_floats(int64_t rows, int32_t num_actions) {
+  return ((rows + TPB - 1) / TPB) * (2 * (int64_t)num_actions + 4);
+}
+
+extern "C" int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream) {
+  if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: null args");
+  lgx_ppo_loss_args a = *args;
+  if (a.rows <= 0 || a.num_actions <= 0 || a.num_actions > LGX_PPO_MAX_ACTIONS || !a.mu_raw || !a.v_raw || !a.b4a ||
+      !a.b4c || !a.std || !a.actions || !a.old_logp || !a.old_mu || !a.old_sigma || !a.advantages ||
+      !a.target_values || !a.returns || !a.d_mu || !a.d_v || !a.partials || !a.g_std || !a.g_b4a || !a.g_b4c ||
+      !a.stats)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: bad args");
+  int blocks = (int)((a.rows + TPB - 1) / TPB);
+  hipLaunchKernelGGL(ppo_loss_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), a);
+  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
+  return lgx_hip_status("lgx_ppo_loss");
+}
+
+extern "C" int lgx_ppo_adapt_lr(const float* kl_sum, float kl_scale, double* lr, double desired_kl, void* stream) {
+  if (!kl_sum || !lr) return lgx_fail(LGX_EINVAL, "lgx_ppo_adapt_lr: bad args");
+  hipLaunchKernelGGL(adapt_lr_kernel, dim3(1), dim3(1), 0, LGX_STREAM(stream), kl_sum, kl_scale, lr, desired_kl);
+  return lgx_hip_status("lgx_ppo_adapt_lr");
+}
+
+extern "C" int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_actions, int32_t hidden) {
+  return ((rows + CHUNK - 1) / CHUNK) * ((int64_t)(num_actions + 1) * hidden + 2 * (int64_t)hidden);
+}
+
+extern "C" int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3,
+                            int64_t rows, int32_t num_actions, int32_t hidden, float* partials, void* stream) {
+  if (!d_mu || !d_v || !W4a || !W4c || !A3 || !partials || rows <= 0 || num_actions <= 0 ||
+      num_actions > LGX_PPO_MAX_ACTIONS || hidden <= 0 || hidden > 256)
+    return lgx_fail(LGX_EINVAL, "lgx_head_bwd: bad args (hidden <= 256)");
+  size_t lds = sizeof(float) * (2 * CHUNK * hidden + CHUNK * (num_actions + 1) + (num_actions + 1) * hidden);
+  if (lds > 160 * 1024) return lgx_fail(LGX_EINVAL, "lgx_head_bwd: LDS budget exceeded");
+  int blocks = (int)((rows + CHUNK - 1) / CHUNK);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks), dim3(TPB), lds, LGX_STREAM(stream), d_mu, d_v, W4a, W4c, A3, rows,
+                     num_actions, hidden, partials);
+  return lgx_hip_status("lgx_head_bwd");
+}
+
+extern "C" int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int32_t nets) {
+  return ((rows + CHUNK - 1) / CHUNK) * (int64_t)hidden * nets;
+}
+
+extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32_t hidden, int32_t nets,
+                                  float* partials, void* stream) {
+  if (!dA || !Y || !partials || rows <= 0 || hidden <= 0 || nets <= 0 || nets > 2)
+    return lgx_fail(LGX_EINVAL, "lgx_elu_bwd_colsum: bad args");
+  int chunks = (int)((rows + CHUNK - 1) / CHUNK);
+  hipLaunchKernelGGL(elu_bwd_colsum_kernel, dim3(chunks, nets), dim3(TPB), 0, LGX_STREAM(stream), dA, Y, rows, hidden,
+                     nets, partials);
+  return lgx_hip_status("lgx_elu_bwd_colsum");
+}
+
+extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream) {
+  if (!jobs || njobs <= 0 || njobs > LGX_MAX_REDUCE_JOBS) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job count");
+  lgx_reduce_jobs J;
+  int64_t biggest = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const lgx_reduce_job& j = jobs[i];
+    if (!j.src || !j.dst || j.n <= 0 || j.slices <= 0 || j.count <= 0)
+      return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job");
+    J.job[i] = j;
+    biggest = std::max<int64_t>(biggest, (int64_t)j.count * j.n);
+  }
+  int blocks = (int)std::min<int64_t>((biggest + TPB - 1) / TPB, 2048);
+  hipLaunchKernelGGL(reduce_slices_kernel, dim3(blocks, njobs), dim3(TPB), 0, LGX_STREAM(stream), J);
+  return lgx_hip_status("lgx_reduce_slices");
+}
+
+extern "C" int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
+                             float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
+                             float beta2, float eps, void* stream) {
+  if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 || nparts > 1024)
+    return lgx_fail(LGX_EINVAL, "lgx_adam_clip: bad args");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
+  int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
+  hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
+                     grad_scale, max_norm, lr, step, beta1, beta2, eps);
+  return lgx_hip_status("lgx_adam_clip");
+}

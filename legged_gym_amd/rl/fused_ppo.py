@@ -1,0 +1,333 @@
+"""The PPO update of rsl_rl v1.0.x (`PPO.update`; legged_robot_config.py:226-239) as an explicit
+forward/backward over flat parameter/gradient buffers — no autograd graph, no per-op launches.
+
+Per minibatch (M rows), on one stream, no host synchronisation:
+  gather obs rows (lgx_ppo_gather_rows)
+  hidden layers: library GEMM (mm for layer 1, bmm over {actor, critic} after) + lgx_bias_act
+  heads: mm; lgx_ppo_loss = log-prob / ratio / clipped surrogate / clipped value loss / entropy
+         / KL and the analytic gradient w.r.t. mu, value, std, head biases
+  lgx_ppo_adapt_lr (device-side adaptive schedule; KL all-reduced first when data-parallel)
+  backward: lgx_head_bwd, then per layer split-K bmm for dW, bmm for dA, lgx_elu_bwd_colsum
+  lgx_reduce_slices: all split-K and bias partials -> flat gradient (one launch)
+  [all-reduce of the flat gradient over RCCL when data-parallel]
+  lgx_adam_clip: clip_grad_norm_(max_grad_norm) + Adam on the flat buffers
+The module's nn.Parameters become views of the flat buffer, so state_dict / load_state_dict /
+the rollout's fused inference see the updated weights; the optimizer is `FlatAdam`, whose
+state_dict has torch.optim.Adam's format (checkpoints stay loadable by upstream tooling).
+"""
+import ctypes as C
+
+import torch
+import torch.nn as nn
+
+from legged_gym_amd.sim import abi
+
+
+def _vp(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class FlatAdam:
+    """torch.optim.Adam (no weight decay, no amsgrad) over one flat parameter buffer, with the
+    learning rate and the step counter resident on the device."""
+
+    def __init__(self, params, flat_p, flat_g, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.params = list(params)
+        self.flat_p, self.flat_g = flat_p, flat_g
+        self.m = torch.zeros_like(flat_p)
+        self.v = torch.zeros_like(flat_p)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=flat_p.device)
+        self.lr_dev = torch.full((1,), float(lr), dtype=torch.float64, device=flat_p.device)
+        self.betas, self.eps = betas, eps
+        self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False, maximize=False,
+                                  foreach=None, capturable=False, differentiable=False, fused=None)]
+
+    def _views(self, buf):
+        base = self.flat_p.data_ptr()
+        out = []
+        for p in self.params:
+            off = (p.data_ptr() - base) // 4
+            out.append(buf[off:off + p.numel()].view_as(p))
+        return out
+
+    def zero_grad(self, set_to_none=False):
+        self.flat_g.zero_()
+
+    def state_dict(self):
+        step = float(self.step_dev.item())
+        ms, vs = self._views(self.m), self._views(self.v)
+        state = {i: {"step": torch.tensor(step), "exp_avg": ms[i].clone(), "exp_avg_sq": vs[i].clone()}
+                 for i in range(len(self.params)) if step > 0}
+        g = dict(self.param_groups[0])
+        g["lr"] = float(self.lr_dev.item())
+        g["params"] = list(range(len(self.params)))
+        return {"state": state, "param_groups": [g]}
+
+    def load_state_dict(self, d):
+        g = d["param_groups"][0]
+        self.lr_dev.fill_(float(g["lr"]))
+        self.param_groups[0]["lr"] = float(g["lr"])
+        ms, vs = self._views(self.m), self._views(self.v)
+        step = 0
+        with torch.no_grad():
+            for i, st in d["state"].items():
+                i = int(i)
+                ms[i].copy_(st["exp_avg"])
+                vs[i].copy_(st["exp_avg_sq"])
+                step = int(float(st["step"]))
+        self.step_dev.fill_(step)
+
+
+class FusedPPOUpdate:
+    """Drives the lgx PPO kernels for a standard rsl_rl ActorCritic (identical ELU hidden stacks
+    for actor and critic)."""
+
+    SPLITS = 8
+
+    @staticmethod
+    def supported(ac):
+        def lin(seq):
+            return [m for m in seq if isinstance(m, nn.Linear)], [m for m in seq if not isinstance(m, nn.Linear)]
+        try:
+            la, aa = lin(ac.actor)
+            lc, acr = lin(ac.critic)
+        except AttributeError:
+            return False
+        if not all(isinstance(m, nn.ELU) and m.alpha == 1.0 for m in aa + acr):
+            return False
+        if len(la) != len(lc) or len(la) < 2 or len(aa) != len(la) - 1 or len(acr) != len(lc) - 1:
+            return False
+        ha = [l.out_features for l in la[:-1]]
+        hc = [l.out_features for l in lc[:-1]]
+        return (ha == hc and all(h % 4 == 0 for h in ha) and ha[-1] <= 256 and lc[-1].out_features == 1
+                and la[-1].out_features <= abi.PPO_MAX_ACTIONS and ac.std.dim() == 1)
+
+    def __init__(self, ppo):
+        from legged_gym_amd.sim import lib as lgxlib
+        self.lib = lgxlib.load()
+        self.check = lgxlib.check
+        self.ppo = ppo
+        ac = ppo.actor_critic
+        self.dev = next(ac.parameters()).device
+        la = [m for m in ac.actor if isinstance(m, nn.Linear)]
+        lc = [m for m in ac.critic if isinstance(m, nn.Linear)]
+        self.L = len(la) - 1                       # hidden layers
+        self.hidden = [l.out_features for l in la[:-1]]
+        self.num_obs = la[0].in_features
+        self.num_cobs = lc[0].in_features
+        self.A = la[-1].out_features
+        # flat layout: layer-major so that {actor, critic} blocks of a layer are adjacent
+        order = []
+        for k in range(self.L + 1):
+            order += [la[k].weight, lc[k].weight]
+        for k in range(self.L + 1):
+            order += [la[k].bias, lc[k].bias]
+        order.append(ac.std)
+        n = sum(p.numel() for p in order)
+        self.flat_p = torch.zeros(n, device=self.dev)
+        self.flat_g = torch.zeros(n, device=self.dev)
+        self.off = {}
+        off = 0
+        with torch.no_grad():
+            for p in order:
+                k = p.numel()
+                self.flat_p[off:off + k].copy_(p.data.reshape(-1))
+                self.off[id(p)] = off
+                p.data = self.flat_p[off:off + k].view_as(p)
+                p.grad = self.flat_g[off:off + k].view_as(p)
+                off += k
+        self.n = n
+        self.la, self.lc = la, lc
+        self.W = []    # per layer k < L: stacked [2, out, in] weight view (k >= 1) or per-net views (k == 0)
+        for k in range(self.L + 1):
+            o = self.off[id(la[k].weight)]
+            if k == 0 or k == self.L:
+                self.W.append((la[k].weight, lc[k].weight))
+            else:
+                self.W.append(self.flat_p[o:o + 2 * la[k].weight.numel()].view(2, *la[k].weight.shape))
+        self.Wg = [self.off[id(la[k].weight)] for k in range(self.L + 1)]
+        self.bo = [self.off[id(la[k].bias)] for k in range(self.L + 1)]
+        self.std_off = self.off[id(ac.std)]
+        params = list(ac.parameters())
+        self.optimizer = FlatAdam(params, self.flat_p, self.flat_g, ppo.learning_rate)
+        self.norm_parts = torch.zeros(256, device=self.dev)
+        self.stats = torch.zeros(3, device=self.dev)
+        self.M = None
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self, M):
+        if self.M == M:
+            return
+        dev, h, A = self.dev, self.hidden, self.A
+        self.M = M
+        self.S = self.SPLITS if M % self.SPLITS == 0 else 1
+        self.X = torch.empty(M, self.num_obs, device=dev)
+        self.Xc = torch.empty(M, self.num_cobs, device=dev) if self._separate_critic_obs() else None
+        self.Y = [torch.empty(2, M, hk, device=dev) for hk in h]
+        self.D = [torch.empty(2, M, hk, device=dev) for hk in h[:-1]]
+        self.MU = torch.empty(M, A, device=dev)
+        self.V = torch.empty(M, 1, device=dev)
+        self.dMU = torch.empty(M, A, device=dev)
+        self.dV = torch.empty(M, device=dev)
+        S = self.S
+        self.P = [torch.empty(2, S, h[0], self.num_obs, device=dev)] + \
+                 [torch.empty(2 * S, h[k], h[k - 1], device=dev) for k in range(1, self.L)]
+        self.loss_parts = torch.empty(int(self.lib.lgx_ppo_loss_partials_floats(M, A)), device=dev)
+        self.head_parts = torch.empty(int(self.lib.lgx_head_bwd_partials_floats(M, A, h[-1])), device=dev)
+        self.col_parts = [torch.empty(int(self.lib.lgx_colsum_partials_floats(M, hk, 2)), device=dev) for hk in h[:-1]]
+        self._build_reduce_jobs()
+
+    def _separate_critic_obs(self):
+        st = self.ppo.storage
+        return st is not None and st.privileged_observations is not None
+
+    def _build_reduce_jobs(self):
+        M, S, h, A = self.M, self.S, self.hidden, self.A
+        g = self.flat_g
+        chunks = (M + 63) // 64
+        jobs = []
+
+        def job(src, dst_off, n, count, job_stride, slices, slice_stride, dst_stride):
+            j = abi.LgxReduceJob()
+            j.src = src.data_ptr()
+            j.dst = g.data_ptr() + 4 * dst_off
+            j.n, j.count, j.job_stride, j.slices, j.slice_stride, j.dst_stride = n, count, job_stride, slices, \
+                slice_stride, dst_stride
+            jobs.append(j)
+        n1 = h[0] * self.num_obs
+        job(self.P[0], self.Wg[0], n1, 2, S * n1, S, n1, n1)                        # dW1 (actor, critic)
+        for k in range(1, self.L):
+            nk = h[k] * h[k - 1]
+            job(self.P[k], self.Wg[k], nk, 2, S * nk, S, nk, nk)                    # dW_k stacked
+        nh = (A + 1) * h[-1] + 2 * h[-1]
+        job(self.head_parts, self.Wg[self.L], (A + 1) * h[-1], 1, 0, chunks, nh, 0)  # dW head (actor | critic)
+        hp_b = self.head_parts[(A + 1) * h[-1]:]
+        job(hp_b, self.bo[self.L - 1], 2 * h[-1], 1, 0, chunks, nh, 0)              # db of the last hidden layer
+        for k in range(self.L - 1):
+            job(self.col_parts[k], self.bo[k], 2 * h[k], 1, 0, chunks, 2 * h[k], 0)  # db_k
+        if len(jobs) > abi.MAX_REDUCE_JOBS:
+            raise RuntimeError("too many reduction jobs for one launch")
+        self.jobs = (abi.LgxReduceJob * len(jobs))(*jobs)
+        self.njobs = len(jobs)
+
+    # ------------------------------------------------------------------ update
+    def update(self):
+        ppo = self.ppo
+        st = ppo.storage
+        T, N = st.num_transitions_per_env, st.num_envs
+        B = T * N
+        nmb = ppo.num_mini_batches
+        M = B // nmb
+        self._alloc(M)
+        stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        self.optimizer.lr_dev.fill_(ppo.learning_rate)
+        self.stats.zero_()
+        indices = torch.randperm(nmb * M, requires_grad=False, device=self.dev)   # as rsl_rl's generator
+        obs = st.observations.view(B, -1)
+        cobs = st.privileged_observations.view(B, -1) if st.privileged_observations is not None else None
+        storage = dict(actions=st.actions.view(B, -1), old_logp=st.actions_log_prob.view(B),
+                       old_mu=st.mu.view(B, -1), old_sigma=st.sigma.view(B, -1), advantages=st.advantages.view(B),
+                       target_values=st.values.view(B), returns=st.returns.view(B))
+        args = self._loss_args(storage)
+        for _ in range(ppo.num_learning_epochs):
+            for i in range(nmb):
+                idx = indices[i * M:(i + 1) * M]
+                self._minibatch(idx, obs, cobs, args, stream)
+        n = ppo.num_learning_epochs * nmb
+        s = self.stats.tolist()   # the one host synchronisation of the update
+        ppo.learning_rate = float(self.optimizer.lr_dev.item())
+        self.optimizer.param_groups[0]["lr"] = ppo.learning_rate
+        return s[2] / n, s[1] / n
+
+    def _loss_args(self, storage):
+        a = abi.LgxPpoLossArgs()
+        p = self.ppo
+        a.rows, a.num_actions = self.M, self.A
+        a.use_clipped_value_loss = int(bool(p.use_clipped_value_loss))
+        a.clip_param, a.value_loss_coef, a.entropy_coef = p.clip_param, p.value_loss_coef, p.entropy_coef
+        a.mu_raw, a.v_raw = self.MU.data_ptr(), self.V.data_ptr()
+        a.b4a = self.flat_p.data_ptr() + 4 * self.bo[self.L]
+        a.b4c = a.b4a + 4 * self.A
+        a.std = self.flat_p.data_ptr() + 4 * self.std_off
+        for k, v in storage.items():
+            setattr(a, k, v.data_ptr())
+        a.d_mu, a.d_v, a.partials = self.dMU.data_ptr(), self.dV.data_ptr(), self.loss_parts.data_ptr()
+        a.g_b4a = self.flat_g.data_ptr() + 4 * self.bo[self.L]
+        a.g_b4c = a.g_b4a + 4 * self.A
+        a.g_std = self.flat_g.data_ptr() + 4 * self.std_off
+        a.stats = self.stats.data_ptr()
+        self._keep = storage
+        return a
+
+    def gradients(self, idx, apply=False):
+        """Flat gradient of one minibatch (rows `idx` of the current storage), for tests."""
+        st = self.ppo.storage
+        T, N = st.num_transitions_per_env, st.num_envs
+        B = T * N
+        self._alloc(idx.numel())
+        stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        obs = st.observations.view(B, -1)
+        cobs = st.privileged_observations.view(B, -1) if st.privileged_observations is not None else None
+        storage = dict(actions=st.actions.view(B, -1), old_logp=st.actions_log_prob.view(B),
+                       old_mu=st.mu.view(B, -1), old_sigma=st.sigma.view(B, -1), advantages=st.advantages.view(B),
+                       target_values=st.values.view(B), returns=st.returns.view(B))
+        self._minibatch(idx, obs, cobs, self._loss_args(storage), stream, apply=apply)
+        return self.flat_g.clone()
+
+    def _minibatch(self, idx, obs, cobs, args, stream, apply=True):
+        lib, chk = self.lib, self.check
+        ppo = self.ppo
+        M, S, h, L, A = self.M, self.S, self.hidden, self.L, self.A
+        chk(lib.lgx_ppo_gather_rows(_vp(obs), _vp(self.X), _vp(idx), M, obs.shape[1], stream), "gather")
+        Xc = self.X
+        if cobs is not None:
+            chk(lib.lgx_ppo_gather_rows(_vp(cobs), _vp(self.Xc), _vp(idx), M, cobs.shape[1], stream), "gather")
+            Xc = self.Xc
+        # ---- forward
+        wa, wc = self.W[0]
+        torch.mm(self.X, wa.t(), out=self.Y[0][0])
+        torch.mm(Xc, wc.t(), out=self.Y[0][1])
+        fp = self.flat_p
+        chk(lib.lgx_bias_act(_vp(self.Y[0]), C.c_void_p(fp.data_ptr() + 4 * self.bo[0]), M, h[0], 2, 1, stream), "bias")
+        for k in range(1, L):
+            torch.bmm(self.Y[k - 1], self.W[k].transpose(1, 2), out=self.Y[k])
+            chk(lib.lgx_bias_act(_vp(self.Y[k]), C.c_void_p(fp.data_ptr() + 4 * self.bo[k]), M, h[k], 2, 1, stream),
+                "bias")
+        wha, whc = self.W[L]
+        torch.mm(self.Y[L - 1][0], wha.t(), out=self.MU)
+        torch.mm(self.Y[L - 1][1], whc.t(), out=self.V)
+        # ---- loss, gradient at the heads, KL -> adaptive learning rate
+        args.idx = idx.data_ptr()
+        chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
+        kl_scale = 1.0
+        if ppo.dist is not None:
+            ppo.dist.all_reduce(self.stats[0:1])
+            kl_scale = 1.0 / ppo.dist.get_world_size()
+        if ppo.desired_kl is not None and ppo.schedule == "adaptive":
+            chk(lib.lgx_ppo_adapt_lr(_vp(self.stats), kl_scale, _vp(self.optimizer.lr_dev), ppo.desired_kl, stream),
+                "adapt_lr")
+        # ---- backward
+        chk(lib.lgx_head_bwd(_vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc), _vp(self.Y[L - 1]), M, A, h[-1],
+                             _vp(self.head_parts), stream), "head_bwd")
+        dZ = self.Y[L - 1]                           # dZ of the last hidden layer (in place)
+        for k in range(L - 1, 0, -1):
+            # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
+            torch.bmm(dZ.view(2 * S, M // S, h[k]).transpose(1, 2), self.Y[k - 1].view(2 * S, M // S, h[k - 1]),
+                      out=self.P[k])
+            torch.bmm(dZ, self.W[k], out=self.D[k - 1])
+            chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
+                                       _vp(self.col_parts[k - 1]), stream), "elu_bwd")
+            dZ = self.D[k - 1]
+        torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), self.X.view(S, M // S, -1), out=self.P[0][0])
+        torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.view(S, M // S, -1), out=self.P[0][1])
+        chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
+        if not apply:
+            return
+        grad_scale = 1.0
+        if ppo.dist is not None:
+            ppo.dist.all_reduce(self.flat_g)
+            grad_scale = 1.0 / ppo.dist.get_world_size()
+        o = self.optimizer
+        chk(lib.lgx_adam_clip(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n, _vp(self.norm_parts),
+                              self.norm_parts.numel(), grad_scale, ppo.max_grad_norm, _vp(o.lr_dev), _vp(o.step_dev),
+                              o.betas[0], o.betas[1], o.eps, stream), "adam")

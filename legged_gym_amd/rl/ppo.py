@@ -13,6 +13,7 @@ import torch.nn as nn
 import torch.optim as optim
 
 from .actor_critic import ActorCritic
+from .fused_ppo import FusedPPOUpdate
 from .storage import RolloutStorage
 
 
@@ -26,7 +27,7 @@ class PPO:
 
     def __init__(self, actor_critic, num_learning_epochs=1, num_mini_batches=1, clip_param=0.2, gamma=0.998, lam=0.95,
                  value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
-                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu"):
+                 use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu", use_fused_update=True):
         self.device = device
         self.desired_kl = desired_kl
         self.schedule = schedule
@@ -46,6 +47,10 @@ class PPO:
         self.max_grad_norm = max_grad_norm
         self.use_clipped_value_loss = use_clipped_value_loss
         self.dist = _dist()
+        self._fused = None
+        if fused and use_fused_update and FusedPPOUpdate.supported(self.actor_critic):
+            self._fused = FusedPPOUpdate(self)       # parameters become views of its flat buffer
+            self.optimizer = self._fused.optimizer
         if self.dist is not None:
             self._broadcast_params()
 
@@ -118,6 +123,12 @@ class PPO:
             off += n
 
     def update(self):
+        if self._fused is not None:
+            out = self._fused.update()
+            self.storage.clear()
+            if hasattr(self.actor_critic, "invalidate_fused"):
+                self.actor_critic.invalidate_fused()
+            return out
         mean_value_loss = 0.0
         mean_surrogate_loss = 0.0
         gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)

@@ -100,6 +100,23 @@ class LgxMlpDesc(C.Structure):
                 ("weights", C.c_void_p * 6), ("biases", C.c_void_p * 6)]
 
 
+class LgxPpoLossArgs(C.Structure):
+    _fields_ = [("rows", i64), ("num_actions", i32), ("use_clipped_value_loss", i32), ("clip_param", C.c_float),
+                ("value_loss_coef", C.c_float), ("entropy_coef", C.c_float)] + [
+        (n, C.c_void_p) for n in ("idx", "mu_raw", "v_raw", "b4a", "b4c", "std", "actions", "old_logp", "old_mu",
+                                  "old_sigma", "advantages", "target_values", "returns", "d_mu", "d_v", "partials",
+                                  "g_std", "g_b4a", "g_b4c", "stats")]
+
+
+class LgxReduceJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("n", i64), ("job_stride", i64), ("slice_stride", i64),
+                ("dst_stride", i64), ("slices", i32), ("count", i32)]
+
+
+PPO_MAX_ACTIONS = 16
+MAX_REDUCE_JOBS = 8
+
+
 def declare(lib, prefix="lgx"):
     """Attach argtypes/restypes of the product C-ABI to a loaded CDLL."""
     vp = C.c_void_p
@@ -124,6 +141,21 @@ def declare(lib, prefix="lgx"):
         "mlp_forward_batch": (C.c_int, [C.POINTER(LgxMlpDesc), i32, vp]),
         "profile_collect": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
     }
+    if prefix == "lgx":  # PPO update entry points: product library only
+        sigs.update({
+            "ppo_gather_rows": (C.c_int, [vp, vp, vp, i64, i32, vp]),
+            "bias_act": (C.c_int, [vp, vp, i64, i32, i32, i32, vp]),
+            "ppo_loss_partials_floats": (i64, [i64, i32]),
+            "ppo_loss": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp]),
+            "ppo_adapt_lr": (C.c_int, [vp, C.c_float, vp, C.c_double, vp]),
+            "head_bwd_partials_floats": (i64, [i64, i32, i32]),
+            "head_bwd": (C.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp]),
+            "colsum_partials_floats": (i64, [i64, i32, i32]),
+            "elu_bwd_colsum": (C.c_int, [vp, vp, i64, i32, i32, vp, vp]),
+            "reduce_slices": (C.c_int, [C.POINTER(LgxReduceJob), i32, vp]),
+            "adam_clip": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
+                                    C.c_float, C.c_float, vp]),
+        })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}")
         fn.restype = res
@@ -134,12 +166,18 @@ def declare(lib, prefix="lgx"):
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
             "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
-            "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch"]
+            "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
+            "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
+            "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
+            "lgx_reduce_slices", "lgx_adam_clip"]
 
 
-def check_layout(sizes_fn):
-    out = (C.c_int64 * 3)()
+def check_layout(sizes_fn, n=6):
+    """Compare the library's sizeof() of every ABI struct with these mirrors (the oracle
+    reports the first 3)."""
+    out = (C.c_int64 * 6)()
     sizes_fn(out)
-    mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers))
-    if tuple(out) != mine:
-        raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)} vs bindings {mine}")
+    mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers), C.sizeof(LgxMlpDesc),
+            C.sizeof(LgxPpoLossArgs), C.sizeof(LgxReduceJob))[:n]
+    if tuple(out)[:n] != mine:
+        raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)[:n]} vs bindings {mine}")

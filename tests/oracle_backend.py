@@ -43,7 +43,7 @@ def load_oracle():
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    abi.check_layout(lib.lgxo_struct_sizes)
+    abi.check_layout(lib.lgxo_struct_sizes, n=3)
     _LIB = lib
     return lib
 
