@@ -211,6 +211,7 @@ class FusedPPOUpdate:
         self.njobs = len(jobs)
 
     # ------------------------------------------------------------------ update
+    @torch.no_grad()
     def update(self):
         ppo = self.ppo
         st = ppo.storage
@@ -274,6 +275,7 @@ class FusedPPOUpdate:
         self._minibatch(idx, obs, cobs, self._loss_args(storage), stream, apply=apply)
         return self.flat_g.clone()
 
+    @torch.no_grad()
     def _minibatch(self, idx, obs, cobs, args, stream, apply=True):
         lib, chk = self.lib, self.check
         ppo = self.ppo
