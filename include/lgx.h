@@ -199,8 +199,9 @@ const char* lgx_last_error(void);
 int lgx_version(void);
 
 /* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers), sizeof(lgx_mlp_desc),
- * sizeof(lgx_ppo_loss_args), sizeof(lgx_reduce_job): lets bindings verify layout */
-void lgx_struct_sizes(int64_t out[6]);
+ * sizeof(lgx_ppo_loss_args), sizeof(lgx_reduce_job), sizeof(lgx_ppo_act_args),
+ * sizeof(lgx_ppo_store_args): lets bindings verify layout */
+void lgx_struct_sizes(int64_t out[8]);
 
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
@@ -285,6 +286,42 @@ int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, con
 #define LGX_PPO_MAX_ACTIONS 16
 #define LGX_MAX_REDUCE_JOBS 8
 
+/* PPO.act + RolloutStorage.add_transitions of one env step: actions = mu + std * noise,
+ * log-prob, storage row (st_* point at row t of the [T, N, .] storage tensors). */
+typedef struct lgx_ppo_act_args {
+  int64_t num_envs;
+  int32_t num_actions, num_obs, num_cobs, pad;
+  const float* mu;              /* [N,A] actor mean (rollout MLP output) */
+  const float* value;           /* [N]   critic value */
+  const float* std;             /* [A] */
+  const float* noise;           /* [N,A] standard-normal draws */
+  const float* obs;             /* [N,num_obs] */
+  const float* cobs;            /* [N,num_cobs] privileged obs or NULL */
+  float* actions_out;           /* [N,A] */
+  float* st_obs;
+  float* st_cobs;               /* NULL iff cobs is NULL */
+  float* st_actions;
+  float* st_values;
+  float* st_logp;
+  float* st_mu;
+  float* st_sigma;
+} lgx_ppo_act_args;
+int lgx_ppo_act(const lgx_ppo_act_args* args, void* stream);
+
+/* PPO.process_env_step: st_rew = rew + gamma * st_values * time_outs; st_dones = reset */
+typedef struct lgx_ppo_store_args {
+  int64_t num_envs;
+  float gamma;
+  int32_t pad;
+  const float* rew;
+  const uint8_t* reset;
+  const uint8_t* time_outs;     /* NULL: no time-out bootstrap */
+  const float* st_values;
+  float* st_rew;
+  uint8_t* st_dones;
+} lgx_ppo_store_args;
+int lgx_ppo_store(const lgx_ppo_store_args* args, void* stream);
+
 /* dst[r, :] = src[idx[r], :] for r < rows (minibatch gather of storage rows) */
 int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width, void* stream);
 
@@ -327,7 +364,7 @@ int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream);
 /* adaptive schedule on the device: lr (double) from KL = kl_sum[0] * kl_scale */
 int lgx_ppo_adapt_lr(const float* kl_sum, float kl_scale, double* lr, double desired_kl, void* stream);
 
-/* output layers backward: partials per 64-row chunk [A*H dW4a | H dW4c | 2H db3];
+/* output layers backward: partials per 64-row chunk [A*H dW4a | H dW4c | 2H db3] (H <= 1024);
  * A3 [2,M,H] (post-ELU) is overwritten by dZ3 */
 int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_actions, int32_t hidden);
 int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3, int64_t rows,

@@ -42,6 +42,7 @@ int lgx_hip_status(const char* what);  // LGX_OK or LGX_EHIP from hipGetLastErro
 // a batch of reduction jobs passed by value to one launch (lgx_reduce_slices)
 struct lgx_reduce_jobs {
   lgx_reduce_job job[LGX_MAX_REDUCE_JOBS];
+  int32_t tile_start[LGX_MAX_REDUCE_JOBS];  // first 64-output tile of each job in the flat grid
 };
 
 // scratch layout (floats): [blocks][LGX_MAX_TERMS + 2] reduction partials

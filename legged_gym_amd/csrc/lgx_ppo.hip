@@ -42,6 +42,65 @@ gather_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, const
   for (int c = lane; c < width; c += 64) d[c] = s[c];
 }
 
+// ---------------------------------------------------------------------------------------- rollout
+// PPO.act + RolloutStorage.add_transitions for one env step (rsl_rl v1.0.x): actions =
+// mu + std * eps (Normal.sample with the caller's standard-normal draws), log-prob, and the
+// storage row t (obs, critic obs, actions, value, log-prob, mu, sigma).  64 envs per workgroup:
+// the obs rows of those envs are one contiguous range, copied coalesced by all 256 lanes.
+__global__ void __launch_bounds__(TPB)
+ppo_act_kernel(lgx_ppo_act_args a) {
+  const int64_t n0 = (int64_t)blockIdx.x * 64;
+  const int64_t nn = min((int64_t)64, a.num_envs - n0);
+  {
+    const int64_t cnt = nn * a.num_obs;
+    const float* src = a.obs + n0 * a.num_obs;
+    float* dst = a.st_obs + n0 * a.num_obs;
+    for (int64_t i = threadIdx.x; i < cnt; i += TPB) dst[i] = src[i];
+    if (a.cobs && a.st_cobs) {
+      const int64_t cc = nn * a.num_cobs;
+      const float* cs = a.cobs + n0 * a.num_cobs;
+      float* cd = a.st_cobs + n0 * a.num_cobs;
+      for (int64_t i = threadIdx.x; i < cc; i += TPB) cd[i] = cs[i];
+    }
+  }
+  const int A = a.num_actions;
+  for (int64_t k = threadIdx.x; k < nn * A; k += TPB) {  // coalesced [env, action] elements
+    const int64_t e = n0 * A + k;
+    const int j = (int)(k % A);
+    const float sd = a.std[j];
+    const float mu = a.mu[e];
+    const float act = mu + sd * a.noise[e];
+    a.actions_out[e] = act;
+    a.st_actions[e] = act;
+    a.st_mu[e] = mu;
+    a.st_sigma[e] = sd;
+  }
+  __syncthreads();
+  if (threadIdx.x < nn) {
+    const int64_t n = n0 + threadIdx.x;
+    const float half_log_2pi = 0.91893853320467274178f;
+    float logp = 0.f;
+    for (int j = 0; j < A; ++j) {
+      float sd = a.std[j];
+      float d = a.st_actions[n * A + j] - a.mu[n * A + j];
+      logp += -(d * d) / (2.f * sd * sd) - logf(sd) - half_log_2pi;
+    }
+    a.st_logp[n] = logp;
+    a.st_values[n] = a.value[n];
+  }
+}
+
+// PPO.process_env_step: r += gamma * V * time_out (time-out bootstrap), dones stored as bytes
+__global__ void __launch_bounds__(TPB)
+ppo_store_kernel(lgx_ppo_store_args a) {
+  const int64_t n = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (n >= a.num_envs) return;
+  float r = a.rew[n];
+  if (a.time_outs) r += a.gamma * (a.st_values[n] * (a.time_outs[n] ? 1.f : 0.f));
+  a.st_rew[n] = r;
+  a.st_dones[n] = a.reset[n] ? 1 : 0;
+}
+
 // ---------------------------------------------------------------------------------------- bias + act
 __global__ void __launch_bounds__(TPB)
 bias_act_kernel(float* __restrict__ z, const float* __restrict__ b, int64_t rows, int32_t cols, int32_t nets,
@@ -177,55 +236,54 @@ __global__ void adapt_lr_kernel(const float* __restrict__ kl_sum, float kl_scale
 // ---------------------------------------------------------------------------------------- head bwd
 // per 64-row chunk: dW4 partial = [dMU | dV]^T [A3a | A3c], dZ3 = (dMU W4a | dV w4c) * elu'(A3)
 // written over A3, db3 partial = column sums of dZ3.  Partials row: [A*H (dW4a), H (dW4c), 2H (db3)].
+// Thread = (net, column c): one coalesced pass over the chunk's rows keeps the head-weight column
+// and the dW4 column accumulators in registers; dMU rows are LDS broadcasts.
+template <int MAXA>
 __global__ void __launch_bounds__(TPB)
 head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, const float* __restrict__ W4a,
                 const float* __restrict__ W4c, float* __restrict__ A3, int64_t rows, int32_t A, int32_t H,
                 float* __restrict__ partials) {
-  extern __shared__ float sm[];
-  float* a3 = sm;                       // [2][CHUNK][H]
-  float* dmu = a3 + 2 * CHUNK * H;      // [CHUNK][A+1]  (last column = dV)
-  float* w4 = dmu + CHUNK * (A + 1);    // [(A+1)][H]
+  __shared__ float dmu[CHUNK][MAXA + 1];
   const int64_t r0 = (int64_t)blockIdx.x * CHUNK;
   const int nr = (int)min((int64_t)CHUNK, rows - r0);
-  const int t = threadIdx.x;
-  for (int i = t; i < 2 * CHUNK * H; i += TPB) {
-    int net = i / (CHUNK * H), rem = i % (CHUNK * H), rr = rem / H, c = rem % H;
-    a3[i] = rr < nr ? A3[(int64_t)net * rows * H + (r0 + rr) * H + c] : 0.f;
-  }
-  for (int i = t; i < CHUNK * (A + 1); i += TPB) {
+  for (int i = threadIdx.x; i < CHUNK * (A + 1); i += TPB) {
     int rr = i / (A + 1), j = i % (A + 1);
     float v = 0.f;
     if (rr < nr) v = j < A ? d_mu[(r0 + rr) * A + j] : d_v[r0 + rr];
-    dmu[i] = v;
+    dmu[rr][j] = v;
   }
-  for (int i = t; i < (A + 1) * H; i += TPB) w4[i] = i < A * H ? W4a[i] : W4c[i - A * H];
   __syncthreads();
-  const int NPr = (A + 1) * H + 2 * H;
-  float* P = partials + (int64_t)blockIdx.x * NPr;
-  // dW4 partial: output (j, c); j < A: actor rows against A3a, j == A: critic against A3c
-  for (int o = t; o < (A + 1) * H; o += TPB) {
-    int j = o / H, c = o % H;
-    const float* col = a3 + (j < A ? 0 : CHUNK * H) + c;
-    float s = 0.f;
-    for (int rr = 0; rr < CHUNK; ++rr) s += dmu[rr * (A + 1) + j] * col[rr * H];
-    P[o] = s;
-  }
-  // dZ3 + db3 partial: thread per (net, column)
-  for (int o = t; o < 2 * H; o += TPB) {
-    int net = o / H, c = o % H;
+  float* P = partials + (int64_t)blockIdx.x * ((A + 1) * H + 2 * H);
+  for (int o = threadIdx.x; o < 2 * H; o += TPB) {
+    const int net = o / H, c = o % H;
+    float w[MAXA], acc[MAXA];
+    const int nj = net == 0 ? A : 1;
+#pragma unroll
+    for (int j = 0; j < MAXA; ++j) {
+      w[j] = j < nj ? (net == 0 ? W4a[j * H + c] : W4c[c]) : 0.f;
+      acc[j] = 0.f;
+    }
+    const int jo = net == 0 ? 0 : A;  // dMU column block of this net
+    float* col = A3 + (int64_t)net * rows * H + r0 * H + c;
     float cs = 0.f;
     for (int rr = 0; rr < nr; ++rr) {
-      float dA;
-      if (net == 0) {
-        dA = 0.f;
-        for (int j = 0; j < A; ++j) dA += dmu[rr * (A + 1) + j] * w4[j * H + c];
-      } else {
-        dA = dmu[rr * (A + 1) + A] * w4[A * H + c];
+      float y = col[(int64_t)rr * H];
+      float dA = 0.f;
+#pragma unroll
+      for (int j = 0; j < MAXA; ++j) {
+        if (j < nj) {
+          float d = dmu[rr][jo + j];
+          acc[j] += d * y;
+          dA += d * w[j];
+        }
       }
-      float dz = dA * elu_grad_from_out(a3[net * CHUNK * H + rr * H + c]);
-      A3[(int64_t)net * rows * H + (r0 + rr) * H + c] = dz;
+      float dz = dA * elu_grad_from_out(y);
+      col[(int64_t)rr * H] = dz;
       cs += dz;
     }
+#pragma unroll
+    for (int j = 0; j < MAXA; ++j)
+      if (j < nj) P[(jo + j) * H + c] = acc[j];
     P[(A + 1) * H + o] = cs;
   }
 }
@@ -254,17 +312,33 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
 }
 
 // ---------------------------------------------------------------------------------------- reductions
-// job: dst[j][i] = sum_s src[j*job_stride + s*slice_stride + i] for s < S, i < n, j < count
+// job: dst[j][i] = sum_s src[j*job_stride + s*slice_stride + i] for s < S, i < n, j < count.
+// Workgroup = one 64-output tile of one job; its 4 waves split the slices (s = wave, wave+4,
+// ...) and combine in LDS in a fixed order: long slice loops (hundreds of chunk partials)
+// run 4-wide with independent loads in flight instead of one serial chain per output.
 __global__ void __launch_bounds__(TPB)
-reduce_slices_kernel(lgx_reduce_jobs jobs) {
-  const lgx_reduce_job& jb = jobs.job[blockIdx.y];
+reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs) {
+  __shared__ float red[4][64];
+  int b = blockIdx.x, ji = 0;
+  while (ji + 1 < njobs && b >= jobs.tile_start[ji + 1]) ++ji;
+  const lgx_reduce_job& jb = jobs.job[ji];
+  const int64_t o = (int64_t)(b - jobs.tile_start[ji]) * 64 + (threadIdx.x & 63);
+  const int w = threadIdx.x >> 6;
   const int64_t total = (int64_t)jb.count * jb.n;
-  for (int64_t o = (int64_t)blockIdx.x * TPB + threadIdx.x; o < total; o += (int64_t)gridDim.x * TPB) {
-    int64_t j = o / jb.n, i = o % jb.n;
+  float acc = 0.f;
+  int64_t j = 0, i = 0;
+  if (o < total) {
+    j = o / jb.n;
+    i = o % jb.n;
     const float* s = jb.src + j * jb.job_stride + i;
-    float acc = 0.f;
-    for (int k = 0; k < jb.slices; ++k) acc += s[(int64_t)k * jb.slice_stride];
-    jb.dst[j * jb.dst_stride + i] = acc;
+#pragma unroll 8
+    for (int k = w; k < jb.slices; k += 4) acc += s[(int64_t)k * jb.slice_stride];
+  }
+  red[w][threadIdx.x & 63] = acc;
+  __syncthreads();
+  if (w == 0 && o < total) {
+    int l = threadIdx.x;
+    jb.dst[j * jb.dst_stride + i] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
   }
 }
 
@@ -346,6 +420,27 @@ extern "C" int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* 
   return lgx_hip_status("lgx_ppo_gather_rows");
 }
 
+extern "C" int lgx_ppo_act(const lgx_ppo_act_args* args, void* stream) {
+  if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_act: null args");
+  const lgx_ppo_act_args& a = *args;
+  if (a.num_envs <= 0 || a.num_actions <= 0 || a.num_obs <= 0 || !a.mu || !a.value || !a.std || !a.noise || !a.obs ||
+      !a.actions_out || !a.st_obs || !a.st_actions || !a.st_values || !a.st_logp || !a.st_mu || !a.st_sigma ||
+      ((a.cobs != nullptr) != (a.st_cobs != nullptr)))
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_act: bad args");
+  hipLaunchKernelGGL(ppo_act_kernel, dim3((unsigned)((a.num_envs + 63) / 64)), dim3(TPB), 0, LGX_STREAM(stream), a);
+  return lgx_hip_status("lgx_ppo_act");
+}
+
+extern "C" int lgx_ppo_store(const lgx_ppo_store_args* args, void* stream) {
+  if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_store: null args");
+  const lgx_ppo_store_args& a = *args;
+  if (a.num_envs <= 0 || !a.rew || !a.reset || !a.st_values || !a.st_rew || !a.st_dones)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_store: bad args");
+  hipLaunchKernelGGL(ppo_store_kernel, dim3((unsigned)((a.num_envs + TPB - 1) / TPB)), dim3(TPB), 0,
+                     LGX_STREAM(stream), a);
+  return lgx_hip_status("lgx_ppo_store");
+}
+
 extern "C" int lgx_bias_act(float* z, const float* b, int64_t rows, int32_t cols, int32_t nets, int32_t act,
                             void* stream) {
   if (!z || !b || rows < 0 || cols <= 0 || cols % 4 || nets <= 0 || act < 0 || act > 2)
@@ -388,13 +483,15 @@ extern "C" int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_action
 extern "C" int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3,
                             int64_t rows, int32_t num_actions, int32_t hidden, float* partials, void* stream) {
   if (!d_mu || !d_v || !W4a || !W4c || !A3 || !partials || rows <= 0 || num_actions <= 0 ||
-      num_actions > LGX_PPO_MAX_ACTIONS || hidden <= 0 || hidden > 256)
-    return lgx_fail(LGX_EINVAL, "lgx_head_bwd: bad args (hidden <= 256)");
-  size_t lds = sizeof(float) * (2 * CHUNK * hidden + CHUNK * (num_actions + 1) + (num_actions + 1) * hidden);
-  if (lds > 160 * 1024) return lgx_fail(LGX_EINVAL, "lgx_head_bwd: LDS budget exceeded");
+      num_actions > LGX_PPO_MAX_ACTIONS || hidden <= 0 || hidden > 1024)
+    return lgx_fail(LGX_EINVAL, "lgx_head_bwd: bad args");
   int blocks = (int)((rows + CHUNK - 1) / CHUNK);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(blocks), dim3(TPB), lds, LGX_STREAM(stream), d_mu, d_v, W4a, W4c, A3, rows,
-                     num_actions, hidden, partials);
+  if (num_actions <= 12)
+    hipLaunchKernelGGL(head_bwd_kernel<12>, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), d_mu, d_v, W4a, W4c, A3,
+                       rows, num_actions, hidden, partials);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<LGX_PPO_MAX_ACTIONS>, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), d_mu, d_v,
+                       W4a, W4c, A3, rows, num_actions, hidden, partials);
   return lgx_hip_status("lgx_head_bwd");
 }
 
@@ -415,16 +512,17 @@ extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32
 extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream) {
   if (!jobs || njobs <= 0 || njobs > LGX_MAX_REDUCE_JOBS) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job count");
   lgx_reduce_jobs J;
-  int64_t biggest = 0;
+  int64_t tiles = 0;
   for (int i = 0; i < njobs; ++i) {
     const lgx_reduce_job& j = jobs[i];
     if (!j.src || !j.dst || j.n <= 0 || j.slices <= 0 || j.count <= 0)
       return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job");
     J.job[i] = j;
-    biggest = std::max<int64_t>(biggest, (int64_t)j.count * j.n);
+    J.tile_start[i] = (int32_t)tiles;
+    tiles += ((int64_t)j.count * j.n + 63) / 64;
   }
-  int blocks = (int)std::min<int64_t>((biggest + TPB - 1) / TPB, 2048);
-  hipLaunchKernelGGL(reduce_slices_kernel, dim3(blocks, njobs), dim3(TPB), 0, LGX_STREAM(stream), J);
+  if (tiles > (1 << 30)) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: too large");
+  hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs);
   return lgx_hip_status("lgx_reduce_slices");
 }
 

@@ -207,6 +207,14 @@ class ActorCritic(nn.Module):
             return self.distribution.sample(), value
         return self.act(observations), self.evaluate(critic_observations)
 
+    def rollout_forward(self, observations, critic_observations):
+        """(actor mean, critic value) in one fused MFMA launch, or None when the fused kernel does
+        not apply (CPU, non-ELU/tanh stacks, widths > 512)."""
+        if self._fused_ok(observations, self._fused_actor) and self._fused_critic.ok:
+            mean, value = run_fused([(self._fused_actor, observations), (self._fused_critic, critic_observations)])
+            return mean, value
+        return None
+
     def evaluate(self, critic_observations, **kwargs):
         if self._fused_ok(critic_observations, self._fused_critic):
             return self._fused_critic(critic_observations)

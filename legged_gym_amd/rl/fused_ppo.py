@@ -99,7 +99,7 @@ class FusedPPOUpdate:
             return False
         ha = [l.out_features for l in la[:-1]]
         hc = [l.out_features for l in lc[:-1]]
-        return (ha == hc and all(h % 4 == 0 for h in ha) and ha[-1] <= 256 and lc[-1].out_features == 1
+        return (ha == hc and all(h % 4 == 0 for h in ha) and ha[-1] <= 1024 and lc[-1].out_features == 1
                 and la[-1].out_features <= abi.PPO_MAX_ACTIONS and ac.std.dim() == 1)
 
     def __init__(self, ppo):

@@ -21,6 +21,7 @@ class RolloutStorage:
             self.action_mean = None
             self.action_sigma = None
             self.hidden_states = None
+            self.in_storage = False   # row already written by the fused rollout kernel
 
         def clear(self):
             self.__init__()

@@ -113,6 +113,17 @@ class LgxReduceJob(C.Structure):
                 ("dst_stride", i64), ("slices", i32), ("count", i32)]
 
 
+class LgxPpoActArgs(C.Structure):
+    _fields_ = [("num_envs", i64), ("num_actions", i32), ("num_obs", i32), ("num_cobs", i32), ("pad", i32)] + [
+        (n, C.c_void_p) for n in ("mu", "value", "std", "noise", "obs", "cobs", "actions_out", "st_obs", "st_cobs",
+                                  "st_actions", "st_values", "st_logp", "st_mu", "st_sigma")]
+
+
+class LgxPpoStoreArgs(C.Structure):
+    _fields_ = [("num_envs", i64), ("gamma", C.c_float), ("pad", i32)] + [
+        (n, C.c_void_p) for n in ("rew", "reset", "time_outs", "st_values", "st_rew", "st_dones")]
+
+
 PPO_MAX_ACTIONS = 16
 MAX_REDUCE_JOBS = 8
 
@@ -144,6 +155,8 @@ def declare(lib, prefix="lgx"):
     if prefix == "lgx":  # PPO update entry points: product library only
         sigs.update({
             "ppo_gather_rows": (C.c_int, [vp, vp, vp, i64, i32, vp]),
+            "ppo_act": (C.c_int, [C.POINTER(LgxPpoActArgs), vp]),
+            "ppo_store": (C.c_int, [C.POINTER(LgxPpoStoreArgs), vp]),
             "bias_act": (C.c_int, [vp, vp, i64, i32, i32, i32, vp]),
             "ppo_loss_partials_floats": (i64, [i64, i32]),
             "ppo_loss": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp]),
@@ -169,15 +182,16 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
-            "lgx_reduce_slices", "lgx_adam_clip"]
+            "lgx_reduce_slices", "lgx_adam_clip", "lgx_ppo_act", "lgx_ppo_store"]
 
 
-def check_layout(sizes_fn, n=6):
+def check_layout(sizes_fn, n=8):
     """Compare the library's sizeof() of every ABI struct with these mirrors (the oracle
     reports the first 3)."""
-    out = (C.c_int64 * 6)()
+    out = (C.c_int64 * 8)()
     sizes_fn(out)
     mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers), C.sizeof(LgxMlpDesc),
-            C.sizeof(LgxPpoLossArgs), C.sizeof(LgxReduceJob))[:n]
+            C.sizeof(LgxPpoLossArgs), C.sizeof(LgxReduceJob), C.sizeof(LgxPpoActArgs),
+            C.sizeof(LgxPpoStoreArgs))[:n]
     if tuple(out)[:n] != mine:
         raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)[:n]} vs bindings {mine}")

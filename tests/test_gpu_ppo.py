@@ -118,3 +118,37 @@ def test_fused_checkpoint_roundtrip(gpu, tmp_path):
     for a, b in zip(fus.actor_critic.parameters(), fus2.actor_critic.parameters()):
         assert torch.equal(a, b)
     assert torch.equal(fus.optimizer.m, fus2.optimizer.m) and torch.equal(fus.optimizer.v, fus2.optimizer.v)
+
+
+def test_fused_rollout_act_and_store(gpu):
+    """lgx_ppo_act / lgx_ppo_store == PPO.act + process_env_step + add_transitions (torch)."""
+    from torch.distributions import Normal
+    _, fus = make_pair()
+    st = fus.storage
+    st.clear()
+    g = torch.Generator(device="cuda:0").manual_seed(7)
+    obs = torch.randn(N, OBS, device="cuda:0", generator=g)
+    with torch.inference_mode():
+        torch.manual_seed(5)
+        actions = fus.act(obs, obs).clone()
+        assert fus.transition.in_storage
+        rew = torch.randn(N, device="cuda:0", generator=g)
+        dones = torch.rand(N, device="cuda:0", generator=g) < 0.2
+        time_outs = (torch.rand(N, device="cuda:0", generator=g) < 0.5) & dones
+        fus.process_env_step(rew, dones, {"time_outs": time_outs})
+        assert st.step == 1
+        ac = fus.actor_critic
+        mean, value = ac.actor(obs), ac.critic(obs)
+        torch.manual_seed(5)
+        noise = torch.randn_like(mean)
+    ref_a = mean + ac.std * noise
+    ref_logp = Normal(mean, ac.std.expand_as(mean)).log_prob(ref_a).sum(-1)
+    assert torch.allclose(actions, ref_a, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(st.actions[0], actions)
+    assert torch.allclose(st.actions_log_prob[0, :, 0], ref_logp, atol=1e-3, rtol=1e-5)
+    assert torch.allclose(st.values[0, :, 0], value[:, 0], atol=1e-4, rtol=1e-4)
+    assert torch.equal(st.observations[0], obs)
+    assert torch.allclose(st.mu[0], mean, atol=1e-4, rtol=1e-4) and torch.equal(st.sigma[0], ac.std.expand_as(mean))
+    ref_r = rew + fus.gamma * st.values[0, :, 0] * time_outs.float()
+    assert torch.allclose(st.rewards[0, :, 0], ref_r, atol=1e-6, rtol=1e-6)
+    assert torch.equal(st.dones[0, :, 0], dones.byte())
