@@ -218,6 +218,11 @@ int lgx_sim_destroy(lgx_sim* sim);
  * `common_step_counter` is the host counter value AFTER this step's increment. */
 int lgx_step(lgx_sim* sim, int64_t common_step_counter, void* stream);
 
+/* Re-point the observation output (device float[N, num_obs]) for the next calls.  The reference
+ * rebinds obs_buf every step (`self.obs_buf = torch.cat(...)`, legged_robot.py:218), so rsl_rl
+ * keeps the previous step's tensor alive across env.step(); callers double-buffer with this. */
+int lgx_rebind_obs(lgx_sim* sim, float* obs);
+
 /* Physics only: `n` substeps with the currently bound dof_targets (gym.simulate x n). */
 int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
 

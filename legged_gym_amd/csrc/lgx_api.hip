@@ -170,6 +170,12 @@ int lgx_set_draws(lgx_sim* s, const float* draws) {
   return 0;
 }
 
+int lgx_rebind_obs(lgx_sim* s, float* obs) {
+  if (!s || !obs) return fail(LGX_EINVAL, "lgx_rebind_obs: null argument");
+  s->bufs.obs = obs;
+  return 0;
+}
+
 int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
   if (!s || n < 0) return fail(LGX_EINVAL, "lgx_simulate: bad arguments");
   if (n == 0) return 0;

@@ -63,6 +63,9 @@ class LgxBackend:
         self._check(self.lib.lgx_reset_idx(self.handle, C.c_void_p(ids_i32.data_ptr()), ids_i32.numel(), counter,
                                            int(init_done), self.stream()), "lgx_reset_idx")
 
+    def rebind_obs(self, obs):
+        self._check(self.lib.lgx_rebind_obs(self.handle, C.c_void_p(obs.data_ptr())), "lgx_rebind_obs")
+
     def set_draws(self, draws):
         self._check(self.lib.lgx_set_draws(self.handle, C.c_void_p(draws.data_ptr()) if draws is not None else None),
                     "lgx_set_draws")
@@ -97,6 +100,7 @@ class LeggedRobot(BaseTask):
     def step(self, actions):
         """legged_robot.py:79-107 as one C-ABI call (lgx_step)."""
         self.actions.copy_(actions)            # clipped in place by the kernel (:85-86)
+        self._next_obs_buffer()
         self.common_step_counter += 1
         self._backend.step(self.common_step_counter)
         self._publish_extras()
@@ -104,6 +108,7 @@ class LeggedRobot(BaseTask):
 
     def post_physics_step(self):
         """legged_robot.py:109-141 on the current physics state (no physics)."""
+        self._next_obs_buffer()
         self.common_step_counter += 1
         self._backend.post_physics(self.common_step_counter)
         self._publish_extras()
@@ -119,6 +124,16 @@ class LeggedRobot(BaseTask):
         ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).contiguous()
         self._backend.reset_idx(ids, self.common_step_counter, self.init_done)
         self._publish_extras()
+
+    def _next_obs_buffer(self):
+        """Alternate between two observation buffers: the reference returns a fresh obs tensor per
+        step (legged_robot.py:218), and rsl_rl keeps the previous one until process_env_step."""
+        self._obs_slot ^= 1
+        ob = self._obs_bufs[self._obs_slot]
+        self._lgx_bufs.obs = _ptr(ob)
+        if hasattr(self._backend, "rebind_obs"):
+            self._backend.rebind_obs(ob)
+        self.obs_buf = ob
 
     def compute_observations(self):
         raise NotImplementedError("observations are produced inside lgx_step/lgx_post_physics")
@@ -456,6 +471,8 @@ class LeggedRobot(BaseTask):
             b.hf_rows, b.hf_cols = self.height_samples.shape
         self._actuator_setup(p, b)
         self._lgx_params, self._lgx_bufs = p, b
+        self._obs_bufs = [self.obs_buf, torch.zeros_like(self.obs_buf)]
+        self._obs_slot = 0
         self._backend = self._make_backend(self._lgx_model, p, b)
 
     def _scratch_floats(self):

@@ -144,6 +144,7 @@ def declare(lib, prefix="lgx"):
         "post_physics": (C.c_int, [vp, i64, vp]),
         "reset_idx": (C.c_int, [vp, vp, i32, i64, i32, vp]),
         "set_draws": (C.c_int, [vp, vp]),
+        "rebind_obs": (C.c_int, [vp, vp]),
         "actuator_mlp": (C.c_int, [vp, vp, i64, vp, vp, vp]),
         "actuator_lstm": (C.c_int, [vp, vp, vp, vp, i64, vp, vp]),
         "mlp_forward": (C.c_int, [vp, vp, i64, i32, C.POINTER(i32), C.POINTER(vp), C.POINTER(vp), i32, vp]),
@@ -177,7 +178,7 @@ def declare(lib, prefix="lgx"):
 
 
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
-            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws",
+            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",

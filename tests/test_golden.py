@@ -26,14 +26,14 @@ def load(name):
     return dict(np.load(os.path.join(GOLD, name + ".npz"), allow_pickle=False))
 
 
-def build(name, g):
-    env = make_env(CASES[name], num_envs=int(g["num_envs"]), device="cpu", backend="oracle")
+def build(name, g, device="cpu", backend="oracle"):
+    env = make_env(CASES[name], num_envs=int(g["num_envs"]), device=device, backend=backend)
     if "height_samples" in g:
         assert tuple(env.height_samples.shape) == g["height_samples"].shape
         env.height_samples.copy_(torch.from_numpy(g["height_samples"]))
         env.terrain_origins.copy_(torch.from_numpy(g["terrain_origins"]))
         env.terrain_types.copy_(torch.from_numpy(g["terrain_types"]))
-    st = lambda k: torch.from_numpy(np.asarray(g["init_" + k]))
+    st = lambda k: torch.from_numpy(np.asarray(g["init_" + k])).to(device)
     env.root_states.copy_(st("root_states"))
     env.dof_state.copy_(st("dof_state"))
     env.commands.copy_(st("commands"))

@@ -141,8 +141,8 @@ def test_fused_rollout_act_and_store(gpu):
         mean, value = ac.actor(obs), ac.critic(obs)
         torch.manual_seed(5)
         noise = torch.randn_like(mean)
-    ref_a = mean + ac.std * noise
-    ref_logp = Normal(mean, ac.std.expand_as(mean)).log_prob(ref_a).sum(-1)
+        ref_a = mean + ac.std * noise
+        ref_logp = Normal(mean, ac.std.expand_as(mean)).log_prob(ref_a).sum(-1)
     assert torch.allclose(actions, ref_a, atol=1e-4, rtol=1e-4)
     assert torch.allclose(st.actions[0], actions)
     assert torch.allclose(st.actions_log_prob[0, :, 0], ref_logp, atol=1e-3, rtol=1e-5)

@@ -139,3 +139,16 @@ def test_rough_terrain_contact_follows_heightfield():
     h = env.root_states[:, 2] - ground
     assert torch.isfinite(env.root_states).all()
     assert (h > 0.0).float().mean() > 0.8
+
+
+def test_returned_obs_survive_the_next_step():
+    """The reference returns a fresh obs tensor every step (legged_robot.py:218); rsl_rl stores the
+    transition's obs after the following env.step, so that tensor must not be overwritten."""
+    env = fresh(n=4)
+    env.reset()
+    obs0, *_ = env.step(torch.zeros(4, 12))
+    keep = obs0.clone()
+    obs1, *_ = env.step(torch.ones(4, 12) * 0.3)
+    assert obs1.data_ptr() != obs0.data_ptr()
+    assert torch.equal(obs0, keep)
+    assert torch.equal(env.get_observations(), obs1)
