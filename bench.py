@@ -32,6 +32,15 @@ PHYS_PMC_TRAFFIC_BYTES = int((2 * 6592.1 + 19206.3) * 1024)
 from legged_gym_amd.sim.flops import physics_flop_per_env_substep  # noqa: E402
 
 
+BASELINE_METRIC = "env-steps/sec (whole node), Go1 rough-terrain 4096 envs/GPU at 1/2/4/8 GPUs"
+WORKLOADS = {
+    "go1_rough": "C3 go1_rough: Go1 trimesh curriculum terrain + 187-point height scan, actuator-net history+MLP",
+    "go1_flat_bench": "C2 go1_flat_bench: Go1 flat, PD drive, no domain randomisation",
+    "anymal_c_rough": "C5 anymal_c_rough: ANYmal-C trimesh curriculum terrain + 187-point height scan, friction/mass "
+                      "randomisation, pushes",
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -148,12 +157,13 @@ def main():
     kernels = {n: {"avg_ms": round(a, 4), "launches": int(c), "share_of_iteration": round(m / args.steps / it_ms, 4)}
                for n, a, c, m in zip(names, avg, cnt, ms)}
     out = {
-        "metric": "env-steps/sec (whole node), Go1 rough-terrain 4096 envs/GPU",
+        "metric": (BASELINE_METRIC if (args.task == "go1_rough" and N == 4096)
+                   else f"env-steps/sec (whole node), {args.task} {N} envs/GPU"),
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": it_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (procedural curriculum terrain, random-init policy)",
-        "config": {"workload": f"C3 {args.task}: Go1 trimesh curriculum terrain + 187-point height scan, "
-                               f"actuator-net history+MLP, PPO 24 steps x {N} envs/GPU, 5 epochs x 4 minibatches",
+        "config": {"workload": WORKLOADS.get(args.task, args.task) + f", PPO {steps_per_iter} steps x {N} envs/GPU, "
+                               f"{runner.alg.num_learning_epochs} epochs x {runner.alg.num_mini_batches} minibatches",
                    "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
         "roofline": roof,
         "roofline_secondary": roof2,

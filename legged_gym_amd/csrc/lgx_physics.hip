@@ -230,6 +230,7 @@ template <int PP>
 LGX_DEV float psum(float v) {
   if (PP >= 2) v += __shfl_xor(v, 4);
   if (PP >= 4) v += __shfl_xor(v, 8);
+  if (PP >= 8) v += __shfl_xor(v, 16);
   return v;
 }
 
@@ -656,7 +657,9 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
   const char* force = getenv("LGX_PHYS_PP");  // A/B switch for measurements
   const int ppx = force ? atoi(force) : pp;
   const int blocks = (n_envs + 15) / 16;       // 16 envs per workgroup of 64*PP lanes
-  if (ppx == 4)
+  if (ppx == 8)
+    hipLaunchKernelGGL(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions);
+  else if (ppx == 4)
     hipLaunchKernelGGL(lgx_physics_kernel<4>, dim3(blocks), dim3(256), 0, stream, dm, dp, b, nsub, from_actions);
   else if (ppx == 2)
     hipLaunchKernelGGL(lgx_physics_kernel<2>, dim3(blocks), dim3(128), 0, stream, dm, dp, b, nsub, from_actions);

@@ -1,0 +1,92 @@
+"""GPU: the data-parallel fused PPO update (KL all-reduce before the device-side adaptive LR,
+flat-gradient all-reduce scaled inside lgx_adam_clip, global advantage statistics) with two
+ranks sharing cuda:0 over gloo, against one process holding both ranks' envs.
+
+Full-batch minibatches (num_mini_batches = 1) so both runs see the same sample sets; same
+tolerance rule as test_gpu_ppo.py (Adam normalises gradients at rounding level).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+T, B, OBS, ACT = 4, 512, 235, 12
+
+
+def _data():
+    g = torch.Generator().manual_seed(3)
+    return dict(obs=torch.randn(T, 2 * B, OBS, generator=g), act=torch.randn(T, 2 * B, ACT, generator=g),
+                rew=torch.randn(T, 2 * B, 1, generator=g), done=(torch.rand(T, 2 * B, 1, generator=g) < 0.1).byte(),
+                val=torch.randn(T, 2 * B, 1, generator=g), logp=torch.randn(T, 2 * B, 1, generator=g) * 0.3 - 17,
+                mu=torch.randn(T, 2 * B, ACT, generator=g) * 0.1, sigma=torch.rand(T, 2 * B, ACT, generator=g) * .5 + .75,
+                last=torch.randn(2 * B, 1, generator=g))
+
+
+def _make(n_envs, sl):
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    from legged_gym_amd.rl.ppo import PPO
+    torch.manual_seed(0)
+    ac = ActorCritic(OBS, OBS, ACT, [512, 256, 128], [512, 256, 128])
+    ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=1, learning_rate=1e-3, gamma=0.99, lam=0.95,
+              schedule="adaptive", entropy_coef=0.01, device="cuda:0")
+    assert ppo._fused is not None
+    ppo.init_storage(n_envs, T, [OBS], [None], [ACT])
+    d = _data()
+    st = ppo.storage
+    for name, key in (("observations", "obs"), ("actions", "act"), ("rewards", "rew"), ("dones", "done"),
+                      ("values", "val"), ("actions_log_prob", "logp"), ("mu", "mu"), ("sigma", "sigma")):
+        getattr(st, name).copy_(d[key][:, sl])
+    st.step = T
+    st.compute_returns(d["last"][sl].cuda(), 0.99, 0.95, reduce_stats=ppo._adv_stats)
+    return ppo
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ppo = _make(B, slice(rank * B, (rank + 1) * B))
+        vl, sl = ppo.update()
+        if rank == 0:
+            q.put([p.detach().cpu().numpy() for p in ppo.actor_critic.parameters()] + [ppo.learning_rate])
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_fused_update_two_ranks_equal_one_process(gpu):
+    ref = _make(2 * B, slice(0, 2 * B))
+    ref.update()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert got[-1] == ref.learning_rate
+    big = total = 0
+    for a, b in zip(got[:-1], ref.actor_critic.parameters()):
+        d = np.abs(a - b.detach().cpu().numpy())
+        assert d.max() <= 2 * 2 * 1e-3
+        big += int((d > 1e-5).sum())
+        total += d.size
+    assert big <= 1e-3 * total, (big, total)

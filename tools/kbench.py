@@ -73,11 +73,28 @@ def phys_ab():
     for task in ("go1_flat_bench", "go1_rough"):
         env = make_env(task, num_envs=4096, device="cuda:0", backend="lgx")
         env.reset()
-        for pp in ("1", "2", "4", "1", "2", "4"):
+        for pp in ("2", "4", "8", "4", "8"):
             os.environ["LGX_PHYS_PP"] = pp
             ms = timeit(lambda: env.simulate(4), iters=20)
             print(f"{task} physics 4 substeps N=4096 PP={pp}: {ms*1e3:.1f} us")
         os.environ.pop("LGX_PHYS_PP")
+
+
+def mlp_ab():
+    """A/B the wide (policy) MLP tile height: rollout actor+critic on 4096 rows."""
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    ac = ActorCritic(235, 235, 12, [512, 256, 128], [512, 256, 128]).cuda()
+    x = torch.randn(4096, 235, device="cuda:0")
+    f = 2 * 4096 * 2 * (235 * 512 + 512 * 256 + 256 * 128 + 128 * 6.5)
+    with torch.inference_mode():
+        ref = (ac.actor(x), ac.critic(x))
+        for rs in ("1", "1"):
+            os.environ["LGX_MLP_WIDE_RS"] = rs
+            m, v = ac.rollout_forward(x, x)
+            err = max((m - ref[0]).abs().max().item(), (v - ref[1]).abs().max().item())
+            ms = timeit(lambda: ac.rollout_forward(x, x), iters=50)
+            print(f"rollout MLP RS={rs}: {ms*1e3:.1f} us {f/ms/1e9:.1f} TFLOP/s  max|err| {err:.2e}")
+    os.environ.pop("LGX_MLP_WIDE_RS")
 
 
 def phys_run(task="go1_rough", n=4096, steps=10):
@@ -99,6 +116,8 @@ if __name__ == "__main__":
         env_bench()
     if "phys" in what:
         phys_ab()
+    if "mlpab" in what:
+        mlp_ab()
     if "physrun" in what:
         phys_run()
 
