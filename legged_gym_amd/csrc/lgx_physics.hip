@@ -160,27 +160,30 @@ struct LegSys {     // lane-private pieces of the arrowhead system
   float rl[3];      // leg rhs
 };
 
-// adds J^T W J and J^T f for a point P on leg body `k` (k = -1: base), W = wt*I + (wn - wt) n n^T
+// adds J^T W J and J^T f for a point P on leg body `k` (k = -1: base), W = wt*I + (wn - wt) n n^T.
+// Column j of W J is formed on the fly (3 floats live instead of 27).
 LGX_DEV void add_contact(LegSys& L, f3 P, f3 n, float wn, float wt, f3 f, int k, const sv* S) {
   f3 Jc[9];  // 6 base + up to 3 leg columns
 #pragma unroll
   for (int c = 0; c < 6; ++c) Jc[c] = jb_col(c, P);
 #pragma unroll
   for (int j = 0; j < 3; ++j) Jc[6 + j] = (j <= k) ? cross(S[j].a, P) + S[j].l : mk3(0.f, 0.f, 0.f);
-  f3 WJ[9];
-  float dw = wn - wt;
+  const float dw = wn - wt;
 #pragma unroll
-  for (int c = 0; c < 9; ++c) WJ[c] = wt * Jc[c] + (dw * dot(n, Jc[c])) * n;
+  for (int j = 0; j < 9; ++j) {
+    const f3 wj = wt * Jc[j] + (dw * dot(n, Jc[j])) * n;
+    if (j < 6) {
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
+      for (int i = 0; i <= j; ++i) L.Ap[sidx(i, j)] += dot(Jc[i], wj);
+    } else {
+      const int jl = j - 6;
 #pragma unroll
-    for (int j = i; j < 6; ++j) L.Ap[sidx(i, j)] += dot(Jc[i], WJ[j]);
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) L.B[i][j] += dot(Jc[i], WJ[6 + j]);
-  L.D[0] += dot(Jc[6], WJ[6]); L.D[1] += dot(Jc[7], WJ[7]); L.D[2] += dot(Jc[8], WJ[8]);
-  L.D[3] += dot(Jc[6], WJ[7]); L.D[4] += dot(Jc[6], WJ[8]); L.D[5] += dot(Jc[7], WJ[8]);
+      for (int i = 0; i < 6; ++i) L.B[i][jl] += dot(Jc[i], wj);
+      if (jl == 0) L.D[0] += dot(Jc[6], wj);
+      if (jl == 1) { L.D[1] += dot(Jc[7], wj); L.D[3] += dot(Jc[6], wj); }
+      if (jl == 2) { L.D[2] += dot(Jc[8], wj); L.D[4] += dot(Jc[6], wj); L.D[5] += dot(Jc[7], wj); }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 6; ++i) L.rb[i] += dot(Jc[i], f);
 #pragma unroll
@@ -223,6 +226,9 @@ LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon,
 }  // namespace
 
 #define MAX_LANE_PTS 32
+#ifndef LGX_PHYS_WAVES_PER_SIMD
+#define LGX_PHYS_WAVES_PER_SIMD 1
+#endif
 #define HIST_STRIDE 31
 
 // sum over the PP lanes that share a leg (lane bits 2..): contact terms were split across them
@@ -240,15 +246,22 @@ LGX_DEV float psum(float v) {
 // shuffles, so the serial contact work per lane shrinks PP-fold while the chip gets PP x
 // more waves (4096 envs x 16 lanes = 1024 waves for PP = 4: all 4 SIMDs of every CU busy).
 template <int PP>
-__global__ void __launch_bounds__(64 * PP)
+__global__ void __launch_bounds__(64 * PP, LGX_PHYS_WAVES_PER_SIMD)
 lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* __restrict__ P, lgx_buffers B,
                    int32_t nsub, int32_t from_actions) {
   constexpr int PHYS_BLOCK = 64 * PP;               // 16 envs per workgroup
   constexpr int LPE = 4 * PP;                       // lanes per env
   constexpr int SLOTS = (MAX_LANE_PTS + PP - 1) / PP;
+  constexpr int ENVS = 16;                          // envs per workgroup
   __shared__ lgx_dev_model smodel;                  // model tables staged once per workgroup
   __shared__ float4 slot_state[PHYS_BLOCK][SLOTS];  // per own candidate: status, fslide.xyz
-  __shared__ float hist_lds[PHYS_BLOCK * HIST_STRIDE]; // Go1 actuator history of the lane's leg
+  __shared__ float hist_lds[ENVS * 4 * HIST_STRIDE];  // Go1 actuator history per (env, leg)
+  // Per-leg / per-env quantities that every lane of the leg / env holds identically are kept
+  // in LDS instead of VGPRs (all those lanes store the same values, so no cross-lane ordering
+  // is needed): register pressure decides the occupancy of this latency-bound kernel.
+  __shared__ float leg_kin[ENVS * 4][3][12];        // body frames of the leg: R (9), origin (3)
+  __shared__ float leg_sys[ENVS * 4][36];           // contact-free leg system: B 18, D 6, rb 6, rl 3
+  __shared__ float env_com[ENVS][40];               // base block 21, its rhs 6, base rotation 9
   {
     const int4* src = reinterpret_cast<const int4*>(DMg);
     int4* dst = reinterpret_cast<int4*>(&smodel);
@@ -261,6 +274,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   const int gl = blockIdx.x * PHYS_BLOCK + tid;
   const int e = gl / LPE;
   const int lie = gl % LPE;
+  const int eb = tid / LPE;                         // env within the workgroup
   const int leg = lie & 3;
   const int pl = lie >> 2;                          // lane index within the leg group
   const bool lane0 = leg == 0;
@@ -286,7 +300,11 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   for (int k = 0; k < 3; ++k) mscale[1 + k] = B.body_mass_scale[(int64_t)ec * 13 + 1 + 3 * leg + k];
   const float mu = 0.5f * ((B.friction ? B.friction[ec] : 1.0f) + M->ground_friction);
   const int ctrl = P->control_type;
-  float* hist = hist_lds + threadIdx.x * HIST_STRIDE;
+  const int lg = eb * 4 + leg;                      // (env, leg) slot in the workgroup
+  float* hist = hist_lds + lg * HIST_STRIDE;
+  float* kin = &leg_kin[lg][0][0];
+  float* lsys = leg_sys[lg];
+  float* ecom = env_com[eb];
   const bool use_hist = from_actions && P->use_actuator_history;
   if (from_actions) {  // clip (legged_robot.py:85-86) fused into the load
     const float* a = B.actions + (int64_t)ec * 12 + leg * 3;
@@ -355,6 +373,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     m33 Rb[3];
     f3 ob[3];
     sv S[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) ecom[27 + i] = R0.a[i];
     {
       m33 Rp = R0;
       f3 op = mk3(0, 0, 0);
@@ -370,6 +390,9 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         f3 aw = mul(Rjf, ax);
         Rb[k] = mul(Rjf, axis_angle(ax, th[k]));
         ob[k] = oj;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) kin[k * 12 + i] = Rb[k].a[i];
+        kin[k * 12 + 9] = oj.x; kin[k * 12 + 10] = oj.y; kin[k * 12 + 11] = oj.z;
         S[k] = sv{aw, cross(oj, aw)};
         Rp = Rb[k];
         op = oj;
@@ -418,6 +441,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       tot = si_add(tot, Ibase);
       si_to_sym6(tot, Acom);
     }
+#pragma unroll
+    for (int i = 0; i < 21; ++i) ecom[i] = Acom[i];
     // H u and bias: rb = A u_b - dt f_base + sum_l (B_l qd_l - dt F0_l);  rl = B^T u_b + D qd + dt(g - C)
     float ub[6] = {wang.x, wang.y, wang.z, vlin.x, vlin.y, vlin.z};
     float rbcom[6];
@@ -427,6 +452,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 #pragma unroll
       for (int j = 0; j < 6; ++j) s2 += Acom[sidx(i, j)] * ub[j];
       rbcom[i] = s2 - dt * sv_get(fbase, i);
+      ecom[21 + i] = rbcom[i];
     }
     float rb0[6];
 #pragma unroll
@@ -471,6 +497,13 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       rl0[k] += dt * g;
     }
     L0.D[0] += Dimp[0]; L0.D[1] += Dimp[1]; L0.D[2] += Dimp[2];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      lsys[3 * i] = L0.B[i][0]; lsys[3 * i + 1] = L0.B[i][1]; lsys[3 * i + 2] = L0.B[i][2];
+      lsys[18 + i] = L0.D[i];
+      lsys[24 + i] = rb0[i];
+    }
+    lsys[30] = rl0[0]; lsys[31] = rl0[1]; lsys[32] = rl0[2];
     // ---- contacts: two passes (pass 0 implicit stick, pass 1 with slide / drop decisions)
     const float kn = M->contact_k, cn = M->contact_c, ct = M->friction_c;
     const float wn = dt * (cn + dt * kn);
@@ -487,17 +520,21 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       L.rl[0] = L.rl[1] = L.rl[2] = 0.f;
       for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
         if (c >= npts) break;
+        float4 st = slot_state[tid][sl];
+        if (pass == 1 && st.x == 0.f) continue;  // separated in pass 0: same geometry, no contact
         int pi = DM->lane_pts[leg][c];
         int db = M->point_dyn[pi];
         int k = db == 0 ? -1 : (db - 1) % 3;
-        m33 R = db == 0 ? R0 : sel3(k, Rb[0], Rb[1], Rb[2]);
-        f3 ol = db == 0 ? mk3(0, 0, 0) : sel3(k, ob[0], ob[1], ob[2]);
+        const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;   // body rotation (+ origin) in LDS
+        m33 R;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
+        f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
         f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
         f3 n;
         float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
         float rad = M->point_radius[pi];
         float depth = (h - (Pp.z + pos.z)) * n.z + rad;
-        float4 st = slot_state[tid][sl];
         if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[tid][sl] = st; }
         if (depth <= 0.f || st.x == 0.f) continue;
         f3 Pc = Pp - rad * n;
@@ -511,14 +548,14 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       for (int i = 0; i < 21; ++i) L.Ap[i] = psum<PP>(L.Ap[i]);
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
-        L.rb[i] = psum<PP>(L.rb[i]) + rb0[i];
+        L.rb[i] = psum<PP>(L.rb[i]) + lsys[24 + i];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) L.B[i][k] = psum<PP>(L.B[i][k]) + L0.B[i][k];
-        L.D[i] = psum<PP>(L.D[i]) + L0.D[i];
+        for (int k = 0; k < 3; ++k) L.B[i][k] = psum<PP>(L.B[i][k]) + lsys[3 * i + k];
+        L.D[i] = psum<PP>(L.D[i]) + lsys[18 + i];
       }
 #pragma unroll
-      for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + rl0[k];
-      arrow_solve(L, Acom, rbcom, lane0, xb, xl);
+      for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + lsys[30 + k];
+      arrow_solve(L, ecom, ecom + 21, lane0, xb, xl);
       // contact status (after pass 0) / reported forces (after pass 1, last substep)
       const bool report = pass == 1 && s == nsub - 1;
       if (pass == 0 || report) {
@@ -534,8 +571,11 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
           int pi = DM->lane_pts[leg][c];
           int db = M->point_dyn[pi];
           int k = db == 0 ? -1 : (db - 1) % 3;
-          m33 R = db == 0 ? R0 : sel3(k, Rb[0], Rb[1], Rb[2]);
-          f3 ol = db == 0 ? mk3(0, 0, 0) : sel3(k, ob[0], ob[1], ob[2]);
+          const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;
+          m33 R;
+#pragma unroll
+          for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
+          f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
           f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
           f3 n;
           float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);

@@ -53,8 +53,9 @@ def physics_flop_per_env_substep(num_candidates, active_contacts=4.0, heightfiel
     free = (QUAT_TO_MAT + 12 * KIN_PER_JOINT + 13 * BODY_SI + 12 * RNEA_PER_JOINT + legs * RNEA_LEG_SUMS + FBASE
             + legs * CRBA_PER_LEG + ACOM + RBCOM + legs * (RB0_PER_LEG + RL0_PER_LEG) + 12 * DRIVE_PER_JOINT
             + 2 * (legs * ARROW_PER_LEG + ARROW_PER_ENV) + legs * STATUS_VL_PER_LEG + INTEGRATE)
-    cand = 2 * num_candidates * (CAND_TRANSFORM + (HEIGHT_FIELD if heightfield else HEIGHT_PLANE))
-    act = active_contacts * (2 * ACTIVE_PER_PASS + ACTIVE_STATUS)
+    geo = CAND_TRANSFORM + (HEIGHT_FIELD if heightfield else HEIGHT_PLANE)
+    cand = num_candidates * geo                       # pass 0 classifies every primitive
+    act = active_contacts * (geo + 2 * ACTIVE_PER_PASS + ACTIVE_STATUS)   # pass 1 revisits contacts only
     return free + cand + act
 
 
