@@ -254,7 +254,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   constexpr int SLOTS = (MAX_LANE_PTS + PP - 1) / PP;
   constexpr int ENVS = 16;                          // envs per workgroup
   __shared__ lgx_dev_model smodel;                  // model tables staged once per workgroup
-  __shared__ float4 slot_state[PHYS_BLOCK][SLOTS];  // per own candidate: status, fslide.xyz
+  __shared__ float4 slot_state[SLOTS][PHYS_BLOCK];  // per own candidate: status, fslide.xyz (lane-minor: no bank conflicts)
   __shared__ float hist_lds[ENVS * 4 * HIST_STRIDE];  // Go1 actuator history per (env, leg)
   // Per-leg / per-env quantities that every lane of the leg / env holds identically are kept
   // in LDS instead of VGPRs (all those lanes store the same values, so no cross-lane ordering
@@ -520,7 +520,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       L.rl[0] = L.rl[1] = L.rl[2] = 0.f;
       for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
         if (c >= npts) break;
-        float4 st = slot_state[tid][sl];
+        float4 st = slot_state[sl][tid];
         if (pass == 1 && st.x == 0.f) continue;  // separated in pass 0: same geometry, no contact
         int pi = DM->lane_pts[leg][c];
         int db = M->point_dyn[pi];
@@ -535,7 +535,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
         float rad = M->point_radius[pi];
         float depth = (h - (Pp.z + pos.z)) * n.z + rad;
-        if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[tid][sl] = st; }
+        if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[sl][tid] = st; }
         if (depth <= 0.f || st.x == 0.f) continue;
         f3 Pc = Pp - rad * n;
         float wt = (pass == 0 || st.x == 1.f) ? dt * ct : 0.f;
@@ -566,7 +566,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         Vl[2] = add(Vl[1], scale(xl.z, S[2]));
         for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
           if (c >= npts) break;
-          float4 st = slot_state[tid][sl];
+          float4 st = slot_state[sl][tid];
           if (st.x == 0.f) continue;
           int pi = DM->lane_pts[leg][c];
           int db = M->point_dyn[pi];
@@ -594,7 +594,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
               float sc = -mu * fn / vtn;
               st = make_float4(2.f, sc * vt.x, sc * vt.y, sc * vt.z);
             } else st.x = 1.f;
-            slot_state[tid][sl] = st;
+            slot_state[sl][tid] = st;
           } else {
             fn = fmaxf(fn, 0.f);
             f3 ft = st.x == 1.f ? (-ct) * vt : mk3(st.y, st.z, st.w);
