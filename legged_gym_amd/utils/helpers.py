@@ -171,8 +171,19 @@ def get_args(argv=None):
 
 
 def export_policy_as_jit(actor_critic, path):
-    """helpers.py:180-190: TorchScript export of the actor MLP."""
+    """helpers.py:180-190: TorchScript export of the actor MLP (as plain nn.Linear layers, so the
+    exported module has no dependency on this package)."""
     import torch
+    import torch.nn as nn
     os.makedirs(path, exist_ok=True)
-    model = copy.deepcopy(actor_critic.actor).to("cpu")
-    torch.jit.script(model).save(os.path.join(path, "policy_1.pt"))
+    layers = []
+    for m in actor_critic.actor:
+        if isinstance(m, nn.Linear):
+            lin = nn.Linear(m.in_features, m.out_features)
+            with torch.no_grad():
+                lin.weight.copy_(m.weight.detach().cpu())
+                lin.bias.copy_(m.bias.detach().cpu())
+            layers.append(lin)
+        else:
+            layers.append(copy.deepcopy(m).to("cpu"))
+    torch.jit.script(nn.Sequential(*layers)).save(os.path.join(path, "policy_1.pt"))

@@ -159,3 +159,14 @@ def test_runner_learns_on_oracle_env_and_checkpoints(tmp_path):
     with torch.inference_mode():
         a = pol(env.get_observations())
     assert a.shape == (8, 12) and torch.isfinite(a).all()
+
+
+def test_policy_export_is_plain_torchscript(tmp_path):
+    """helpers.py:180-190: the exported actor is a TorchScript module of plain layers."""
+    from legged_gym_amd.utils import export_policy_as_jit
+    torch.manual_seed(0)
+    ac = ActorCritic(OBS, OBS, ACT, [16, 8], [16, 8])
+    export_policy_as_jit(ac, str(tmp_path))
+    pol = torch.jit.load(str(tmp_path / "policy_1.pt"))
+    x = torch.randn(5, OBS)
+    assert torch.allclose(pol(x), ac.actor(x), atol=1e-6)
