@@ -1,0 +1,111 @@
+"""GPU at the benchmark size (C3: go1_rough, 4096 envs): size-independent properties of a
+rollout, oracle parity of a strided env subset taken from the full-size run, and the
+every-env-resets-at-once edge case.
+
+Tolerances as test_gpu_parity.py (physics model identical, algorithms differ: dense vs Schur).
+"""
+import pytest
+import torch
+
+from oracle_backend import make_env
+from test_gpu_parity import close, randomize_state, sync
+
+pytestmark = pytest.mark.gpu
+
+N = 4096
+
+
+@pytest.fixture(scope="module")
+def big(gpu):
+    env = make_env("go1_rough", num_envs=N, device="cuda:0", backend="lgx", overrides=_no_noise)
+    env.reset()
+    return env
+
+
+def _no_noise(cfg):
+    cfg.noise.add_noise = False
+
+
+def test_full_size_rollout_properties(big):
+    env = big
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    resets = 0
+    len0 = env._episode_length_buf.clone()
+    for t in range(60):
+        a = torch.randn(N, 12, device="cuda:0", generator=g) * 0.5
+        obs, _, rew, done, infos = env.step(a)
+        assert torch.isfinite(obs).all() and obs.abs().max() <= env.cfg.normalization.clip_observations
+        assert torch.isfinite(rew).all() and torch.isfinite(env.root_states).all()
+        assert torch.isfinite(env.contact_forces).all() and torch.isfinite(env.dof_state).all()
+        assert (env.torques.abs() <= 23.7 + 1e-3).all()
+        resets += int(done.sum())
+        # episode counters: +1 per step, 0 after a reset
+        exp = torch.where(done, torch.zeros_like(len0), len0 + 1)
+        assert torch.equal(env._episode_length_buf, exp)
+        len0 = env._episode_length_buf.clone()
+        keys = {"rew_" + k for k in env.episode_sums} | ({"terrain_level"} if env.cfg.terrain.curriculum else set())
+        assert set(infos["episode"]) == keys
+    assert resets < 0.5 * N * 60
+
+
+def test_full_size_subset_matches_oracle(big):
+    """Envs 0, 64, 128, ... of the 4096-env device state, stepped by the 64-env oracle.  Draws
+    are keyed by env index, so observation noise is off (both envs) and only non-resetting envs
+    are compared in full."""
+    dev = big
+    idx = torch.arange(0, N, N // 64)
+    ora = make_env("go1_rough", num_envs=64, device="cpu", backend="oracle", overrides=_no_noise)
+    if not torch.equal(ora.height_samples, dev.height_samples.cpu()):
+        pytest.skip("heightfield depends on num_envs")
+    gen = torch.Generator().manual_seed(5)
+    ora.dof_state.view(64, 12, 2).copy_(dev.dof_state.view(N, 12, 2)[idx.cuda()].cpu())
+    for name in ("root_states", "actions", "last_actions", "last_dof_vel", "last_root_vel", "commands",
+                 "feet_air_time", "_episode_length_buf", "env_origins", "terrain_levels", "terrain_types",
+                 "body_mass_scale", "friction_coeffs", "target_poses"):
+        getattr(ora, name).copy_(getattr(dev, name)[idx.cuda()].cpu())
+    ora._episode_sums_buf.copy_(dev._episode_sums_buf[:, idx.cuda()].cpu())
+    if hasattr(dev, "actuator_history"):
+        ora.actuator_history.copy_(dev.actuator_history[idx.cuda()].cpu())
+    ora.common_step_counter = dev.common_step_counter = 100
+    a_sub = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+    a_full = torch.zeros(N, 12)
+    a_full[idx] = a_sub
+    ora.step(a_sub)
+    dev.step(a_full.cuda())
+    torch.cuda.synchronize()
+    rd = dev.reset_buf[idx.cuda()].cpu()
+    assert torch.equal(rd, ora.reset_buf)
+    keep = ~rd
+    ok, e = close(dev.root_states[idx.cuda()][keep.cuda()], ora.root_states[keep], 2e-3, 2e-3)
+    assert ok, f"root max err {e}"
+    ok, e = close(dev.dof_state.view(N, 12, 2)[idx.cuda()][keep.cuda()], ora.dof_state.view(64, 12, 2)[keep], 5e-3, 2e-3)
+    assert ok, f"dof max err {e}"
+    ok, e = close(dev.rew_buf[idx.cuda()][keep.cuda()], ora.rew_buf[keep], 1e-4, 1e-3)
+    assert ok, f"rew max err {e}"
+    ok, e = close(dev.obs_buf[idx.cuda()][keep.cuda()], ora.obs_buf[keep], 5e-3, 5e-3)
+    assert ok, f"obs max err {e}"
+
+
+def test_all_envs_reset_in_one_step(gpu):
+    """Every env times out in the same step (episode_length_buf = max_episode_length)."""
+    ora = make_env("go1_rough", num_envs=64, device="cpu", backend="oracle")
+    dev = make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
+    gen = torch.Generator().manual_seed(9)
+    randomize_state(ora, gen)
+    ora._episode_length_buf[:] = int(ora.max_episode_length)
+    sync(ora, dev)
+    dev.terrain_types.copy_(ora.terrain_types)
+    ora.common_step_counter = dev.common_step_counter = 20
+    a = (torch.rand(64, 12, generator=gen) - 0.5)
+    ora.step(a)
+    dev.step(a.cuda())
+    torch.cuda.synchronize()
+    assert ora.reset_buf.all() and ora.time_out_buf.all()
+    assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf) and torch.equal(dev.time_out_buf.cpu(), ora.time_out_buf)
+    assert torch.equal(dev._episode_length_buf.cpu(), ora._episode_length_buf)
+    for name in ("root_states", "dof_state", "commands", "env_origins", "_extras_buf", "_episode_sums_buf"):
+        ok, e = close(getattr(dev, name), getattr(ora, name), 1e-4, 1e-5)
+        assert ok, f"{name} max err {e}"
+    assert torch.equal(dev.terrain_levels.cpu(), ora.terrain_levels)
+    ok, e = close(dev.obs_buf, ora.obs_buf, 5e-3, 5e-3)
+    assert ok, f"obs max err {e}"

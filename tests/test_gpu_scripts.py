@@ -20,7 +20,8 @@ def test_train_then_play(gpu, tmp_path):
     root = os.path.join(LEGGED_GYM_ROOT_DIR, "logs", exp)
     runs = os.listdir(root)
     assert len(runs) == 1 and "model_2.pt" in os.listdir(os.path.join(root, runs[0]))
-    finished = play(get_args(common), steps=60)
+    # go1_config.py pins load_run to the authors' run; point it at ours
+    finished = play(get_args(common + ["--load_run", runs[0]]), steps=60)
     assert os.path.exists(os.path.join(root, "exported", "policies", "policy_1.pt"))
     pol = torch.jit.load(os.path.join(root, "exported", "policies", "policy_1.pt"))
     assert pol(torch.zeros(1, 48)).shape == (1, 12)
