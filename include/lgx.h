@@ -369,7 +369,7 @@ int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream);
 /* adaptive schedule on the device: lr (double) from KL = kl_sum[0] * kl_scale */
 int lgx_ppo_adapt_lr(const float* kl_sum, float kl_scale, double* lr, double desired_kl, void* stream);
 
-/* output layers backward: partials per 64-row chunk [A*H dW4a | H dW4c | 2H db3] (H <= 1024);
+/* output layers backward: partials per 32-row chunk [A*H dW4a | H dW4c | 2H db3] (H <= 1024);
  * A3 [2,M,H] (post-ELU) is overwritten by dZ3 */
 int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_actions, int32_t hidden);
 int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3, int64_t rows,

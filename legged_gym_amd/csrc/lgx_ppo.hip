@@ -25,6 +25,7 @@ namespace {
 
 constexpr int TPB = 256;
 constexpr int CHUNK = 64;  // rows per workgroup in the backward epilogues
+constexpr int HEAD_CHUNK = 32;  // rows per workgroup in the output-layer backward
 
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
@@ -204,21 +205,33 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
 }
 
 // one workgroup: reduce the loss partials, write d std / d b4a / d b4c into the flat gradient,
-// the KL mean and the running loss sums
+// the KL mean and the running loss sums.  Thread (g, k): value k over partial blocks g, g+8, ...
+// then a fixed-order combine of the 8 groups.
 __global__ void __launch_bounds__(TPB)
 ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) {
   const int A = a.num_actions;
-  const int NP = 2 * A + 4;
-  const int k = threadIdx.x;
-  if (k >= NP) return;
+  const int NP = 2 * A + 4;               // <= 36
+  __shared__ float red[8][2 * LGX_PPO_MAX_ACTIONS + 4];
+  const int grp = threadIdx.x / 32;
+  {
+    for (int kk = threadIdx.x % 32; kk < NP; kk += 32) {
+      float s = 0.f;
+      for (int b = grp; b < nblocks; b += 8) s += a.partials[(int64_t)b * NP + kk];
+      red[grp][kk] = s;
+    }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= NP) return;
   float s = 0.f;
-  for (int b = 0; b < nblocks; ++b) s += a.partials[(int64_t)b * NP + k];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) s += red[g][t];
   const float invM = 1.0f / (float)a.rows;
-  if (k < A) a.g_std[k] = s - a.entropy_coef / a.std[k];   // entropy: -c_e mean(sum_j log std_j + c)
-  else if (k < 2 * A) a.g_b4a[k - A] = s;
-  else if (k == 2 * A) a.g_b4c[0] = s;
-  else if (k == 2 * A + 1) a.stats[0] = s * invM;          // KL mean of this minibatch (local)
-  else if (k == 2 * A + 2) a.stats[1] += s * invM;         // running surrogate-loss sum
+  if (t < A) a.g_std[t] = s - a.entropy_coef / a.std[t];   // entropy: -c_e mean(sum_j log std_j + c)
+  else if (t < 2 * A) a.g_b4a[t - A] = s;
+  else if (t == 2 * A) a.g_b4c[0] = s;
+  else if (t == 2 * A + 1) a.stats[0] = s * invM;          // KL mean of this minibatch (local)
+  else if (t == 2 * A + 2) a.stats[1] += s * invM;         // running surrogate-loss sum
   else a.stats[2] += s * invM;                             // running value-loss sum
 }
 
@@ -234,7 +247,7 @@ __global__ void adapt_lr_kernel(const float* __restrict__ kl_sum, float kl_scale
 }
 
 // ---------------------------------------------------------------------------------------- head bwd
-// per 64-row chunk: dW4 partial = [dMU | dV]^T [A3a | A3c], dZ3 = (dMU W4a | dV w4c) * elu'(A3)
+// per 32-row chunk: dW4 partial = [dMU | dV]^T [A3a | A3c], dZ3 = (dMU W4a | dV w4c) * elu'(A3)
 // written over A3, db3 partial = column sums of dZ3.  Partials row: [A*H (dW4a), H (dW4c), 2H (db3)].
 // Thread = (net, column c): one coalesced pass over the chunk's rows keeps the head-weight column
 // and the dW4 column accumulators in registers; dMU rows are LDS broadcasts.
@@ -243,10 +256,10 @@ __global__ void __launch_bounds__(TPB)
 head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, const float* __restrict__ W4a,
                 const float* __restrict__ W4c, float* __restrict__ A3, int64_t rows, int32_t A, int32_t H,
                 float* __restrict__ partials) {
-  __shared__ float dmu[CHUNK][MAXA + 1];
-  const int64_t r0 = (int64_t)blockIdx.x * CHUNK;
-  const int nr = (int)min((int64_t)CHUNK, rows - r0);
-  for (int i = threadIdx.x; i < CHUNK * (A + 1); i += TPB) {
+  __shared__ float dmu[HEAD_CHUNK][MAXA + 1];
+  const int64_t r0 = (int64_t)blockIdx.x * HEAD_CHUNK;
+  const int nr = (int)min((int64_t)HEAD_CHUNK, rows - r0);
+  for (int i = threadIdx.x; i < HEAD_CHUNK * (A + 1); i += TPB) {
     int rr = i / (A + 1), j = i % (A + 1);
     float v = 0.f;
     if (rr < nr) v = j < A ? d_mu[(r0 + rr) * A + j] : d_v[r0 + rr];
@@ -290,7 +303,7 @@ head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, c
 
 // ---------------------------------------------------------------------------------------- elu bwd
 // dA [nets, rows, H] -> dZ = dA * elu'(Y) in place; partial column sums per 64-row chunk:
-// partials[chunk][net*H + c]
+// partials[chunk][net*H + c].  Thread = 4 consecutive columns (16-B loads and stores).
 __global__ void __launch_bounds__(TPB)
 elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64_t rows, int32_t H, int32_t nets,
                       float* __restrict__ partials) {
@@ -299,15 +312,34 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
   const int nr = (int)min((int64_t)CHUNK, rows - r0);
   const int64_t base = (int64_t)net * rows * H + r0 * H;
   float* P = partials + (int64_t)blockIdx.x * nets * H + net * H;
-  for (int c = threadIdx.x; c < H; c += TPB) {
-    float cs = 0.f;
-    for (int rr = 0; rr < nr; ++rr) {
-      int64_t i = base + (int64_t)rr * H + c;
-      float dz = dA[i] * elu_grad_from_out(Y[i]);
-      dA[i] = dz;
-      cs += dz;
+  const int H4 = H >> 2;
+  // TPB threads = (row lane, column quad): rows are split over TPB / H4 lanes
+  const int lanes_per_row = H4 < TPB ? H4 : TPB;
+  const int row_groups = TPB / lanes_per_row;
+  const int cq = threadIdx.x % lanes_per_row, rg = threadIdx.x / lanes_per_row;
+  __shared__ float4 red[TPB];
+  for (int c4 = cq; c4 < H4; c4 += lanes_per_row) {
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int rr = rg; rr < nr; rr += row_groups) {
+      int64_t i = (base + (int64_t)rr * H) / 4 + c4;
+      float4 d = reinterpret_cast<float4*>(dA)[i];
+      float4 y = reinterpret_cast<const float4*>(Y)[i];
+      d.x *= elu_grad_from_out(y.x); d.y *= elu_grad_from_out(y.y);
+      d.z *= elu_grad_from_out(y.z); d.w *= elu_grad_from_out(y.w);
+      reinterpret_cast<float4*>(dA)[i] = d;
+      cs.x += d.x; cs.y += d.y; cs.z += d.z; cs.w += d.w;
     }
-    P[c] = cs;
+    red[threadIdx.x] = cs;
+    __syncthreads();
+    if (rg == 0) {
+      float4 t = red[cq];
+      for (int g = 1; g < row_groups; ++g) {
+        float4 u = red[g * lanes_per_row + cq];
+        t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+      }
+      reinterpret_cast<float4*>(P)[c4] = t;
+    }
+    __syncthreads();
   }
 }
 
@@ -477,7 +509,7 @@ extern "C" int lgx_ppo_adapt_lr(const float* kl_sum, float kl_scale, double* lr,
 }
 
 extern "C" int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_actions, int32_t hidden) {
-  return ((rows + CHUNK - 1) / CHUNK) * ((int64_t)(num_actions + 1) * hidden + 2 * (int64_t)hidden);
+  return ((rows + HEAD_CHUNK - 1) / HEAD_CHUNK) * ((int64_t)(num_actions + 1) * hidden + 2 * (int64_t)hidden);
 }
 
 extern "C" int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3,
@@ -485,7 +517,7 @@ extern "C" int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4
   if (!d_mu || !d_v || !W4a || !W4c || !A3 || !partials || rows <= 0 || num_actions <= 0 ||
       num_actions > LGX_PPO_MAX_ACTIONS || hidden <= 0 || hidden > 1024)
     return lgx_fail(LGX_EINVAL, "lgx_head_bwd: bad args");
-  int blocks = (int)((rows + CHUNK - 1) / CHUNK);
+  int blocks = (int)((rows + HEAD_CHUNK - 1) / HEAD_CHUNK);
   if (num_actions <= 12)
     hipLaunchKernelGGL(head_bwd_kernel<12>, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), d_mu, d_v, W4a, W4c, A3,
                        rows, num_actions, hidden, partials);
@@ -501,8 +533,9 @@ extern "C" int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int3
 
 extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32_t hidden, int32_t nets,
                                   float* partials, void* stream) {
-  if (!dA || !Y || !partials || rows <= 0 || hidden <= 0 || nets <= 0 || nets > 2)
-    return lgx_fail(LGX_EINVAL, "lgx_elu_bwd_colsum: bad args");
+  if (!dA || !Y || !partials || rows <= 0 || hidden <= 0 || hidden % 4 || nets <= 0 || nets > 2 ||
+      (hidden / 4 < TPB && TPB % (hidden / 4)) || (hidden / 4 > TPB && (hidden / 4) % TPB))
+    return lgx_fail(LGX_EINVAL, "lgx_elu_bwd_colsum: bad args (hidden % 4, hidden/4 must divide or be a multiple of 256)");
   int chunks = (int)((rows + CHUNK - 1) / CHUNK);
   hipLaunchKernelGGL(elu_bwd_colsum_kernel, dim3(chunks, nets), dim3(TPB), 0, LGX_STREAM(stream), dA, Y, rows, hidden,
                      nets, partials);

@@ -184,7 +184,6 @@ class FusedPPOUpdate:
     def _build_reduce_jobs(self):
         M, S, h, A = self.M, self.S, self.hidden, self.A
         g = self.flat_g
-        chunks = (M + 63) // 64
         jobs = []
 
         def job(src, dst_off, n, count, job_stride, slices, slice_stride, dst_stride):
@@ -200,11 +199,13 @@ class FusedPPOUpdate:
             nk = h[k] * h[k - 1]
             job(self.P[k], self.Wg[k], nk, 2, S * nk, S, nk, nk)                    # dW_k stacked
         nh = (A + 1) * h[-1] + 2 * h[-1]
-        job(self.head_parts, self.Wg[self.L], (A + 1) * h[-1], 1, 0, chunks, nh, 0)  # dW head (actor | critic)
+        hchunks = self.head_parts.numel() // nh                                     # per-chunk partial rows
+        job(self.head_parts, self.Wg[self.L], (A + 1) * h[-1], 1, 0, hchunks, nh, 0)  # dW head (actor | critic)
         hp_b = self.head_parts[(A + 1) * h[-1]:]
-        job(hp_b, self.bo[self.L - 1], 2 * h[-1], 1, 0, chunks, nh, 0)              # db of the last hidden layer
+        job(hp_b, self.bo[self.L - 1], 2 * h[-1], 1, 0, hchunks, nh, 0)              # db of the last hidden layer
         for k in range(self.L - 1):
-            job(self.col_parts[k], self.bo[k], 2 * h[k], 1, 0, chunks, 2 * h[k], 0)  # db_k
+            cchunks = self.col_parts[k].numel() // (2 * h[k])
+            job(self.col_parts[k], self.bo[k], 2 * h[k], 1, 0, cchunks, 2 * h[k], 0)  # db_k
         if len(jobs) > abi.MAX_REDUCE_JOBS:
             raise RuntimeError("too many reduction jobs for one launch")
         self.jobs = (abi.LgxReduceJob * len(jobs))(*jobs)
