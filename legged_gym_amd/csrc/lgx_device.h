@@ -90,9 +90,12 @@ LGX_DEV float quad_sum(float v) {
   return v;
 }
 
-// triangulated heightfield (diagonal (i,j)-(i+1,j+1), isaacgym terrain_utils trimesh)
+// triangulated heightfield (diagonal (i,j)-(i+1,j+1), isaacgym terrain_utils trimesh).
+// Optional LDS patch: samples (i, j) with 0 <= i - pi0, j - pj0 < LGX_HF_PATCH are read from
+// `patch` (a copy of the same int16 samples), others from H: identical values either way.
+#define LGX_HF_PATCH 24
 LGX_DEV float ground_height(const lgx_env_params* __restrict__ P, const int16_t* __restrict__ H, int rows, int cols,
-                            float x, float y, f3* n) {
+                            float x, float y, f3* n, const int16_t* patch = nullptr, int pi0 = 0, int pj0 = 0) {
   if (P->terrain_kind == 0 || H == nullptr) { *n = mk3(0.f, 0.f, 1.f); return 0.0f; }
   float hs = P->horizontal_scale, vs = P->vertical_scale;
   float u = (x + P->border_size) / hs, v = (y + P->border_size) / hs;
@@ -100,8 +103,15 @@ LGX_DEV float ground_height(const lgx_env_params* __restrict__ P, const int16_t*
   i = min(max(i, 0), rows - 2);
   j = min(max(j, 0), cols - 2);
   float fu = clampf(u - (float)i, 0.f, 1.f), fv = clampf(v - (float)j, 0.f, 1.f);
-  float h00 = H[i * cols + j] * vs, h10 = H[(i + 1) * cols + j] * vs;
-  float h01 = H[i * cols + j + 1] * vs, h11 = H[(i + 1) * cols + j + 1] * vs;
+  float h00, h10, h01, h11;
+  const int li = i - pi0, lj = j - pj0;
+  if (patch && (unsigned)li < LGX_HF_PATCH - 1 && (unsigned)lj < LGX_HF_PATCH - 1) {
+    const int16_t* q = patch + li * LGX_HF_PATCH + lj;
+    h00 = q[0] * vs; h10 = q[LGX_HF_PATCH] * vs; h01 = q[1] * vs; h11 = q[LGX_HF_PATCH + 1] * vs;
+  } else {
+    h00 = H[i * cols + j] * vs; h10 = H[(i + 1) * cols + j] * vs;
+    h01 = H[i * cols + j + 1] * vs; h11 = H[(i + 1) * cols + j + 1] * vs;
+  }
   float gx, gy, h;
   if (fu >= fv) { gx = (h10 - h00) / hs; gy = (h11 - h10) / hs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
   else          { gx = (h11 - h01) / hs; gy = (h01 - h00) / hs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }

@@ -201,27 +201,41 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
   __shared__ float part[LGX_ENV_BLOCK][LGX_PARTIAL_STRIDE];
 
-  // ---- phase A: height scan (legged_robot.py:818-854), pre-reset base pose
+  // ---- phase A: height scan (legged_robot.py:818-854), pre-reset base pose.  The per-env yaw
+  // rotation and base xy are staged in LDS; the (env, point) loop is unrolled so several
+  // heightfield gathers are in flight per lane.
   if (P->measure_heights) {
-    const int np = P->num_height_points;
-    const int total = LGX_ENV_BLOCK * np;
-    for (int idx = tid; idx < total; idx += ENV_THREADS) {
-      int le = idx / np, i = idx - le * np;
-      int e = e0 + le;
-      if (e >= N) break;
-      float* mh = B.measured_heights + (int64_t)e * np + i;
-      if (P->terrain_kind == 0) { *mh = 0.f; continue; }
+    __shared__ float4 base_xy_yaw[LGX_ENV_BLOCK];
+    if (tid < LGX_ENV_BLOCK) {
+      const int e = min(e0 + tid, N - 1);
       const float* rs = B.root_states + (int64_t)e * 13;
       float z = rs[5], w = rs[6];
       float nrm = fmaxf(sqrtf(z * z + w * w), 1e-9f);
-      f3 o = quat_apply(0.f, 0.f, z / nrm, w / nrm, mk3(P->height_points[i][0], P->height_points[i][1], 0.f));
-      float x = o.x + rs[0] + P->border_size, y = o.y + rs[1] + P->border_size;
-      int64_t px = (int64_t)(x / P->horizontal_scale), py = (int64_t)(y / P->horizontal_scale);
-      px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
-      py = py < 0 ? 0 : (py > B.hf_cols - 2 ? B.hf_cols - 2 : py);
-      const int16_t* H = B.height_samples;
-      int h1 = H[px * B.hf_cols + py], h2 = H[(px + 1) * B.hf_cols + py], h3 = H[px * B.hf_cols + py + 1];
-      *mh = (float)min(min(h1, h2), h3) * P->vertical_scale;
+      base_xy_yaw[tid] = make_float4(rs[0] + P->border_size, rs[1] + P->border_size, z / nrm, w / nrm);
+    }
+    __syncthreads();
+    const int np = P->num_height_points;
+    const int total = LGX_ENV_BLOCK * np;
+    const int16_t* H = B.height_samples;
+#pragma unroll 4
+    for (int idx = tid; idx < total; idx += ENV_THREADS) {
+      const int le = idx / np, i = idx - le * np;
+      const int e = e0 + le;
+      if (e < N) {
+        float* mh = B.measured_heights + (int64_t)e * np + i;
+        if (P->terrain_kind == 0) {
+          *mh = 0.f;
+        } else {
+          const float4 b = base_xy_yaw[le];
+          f3 o = quat_apply(0.f, 0.f, b.z, b.w, mk3(P->height_points[i][0], P->height_points[i][1], 0.f));
+          float x = o.x + b.x, y = o.y + b.y;
+          int64_t px = (int64_t)(x / P->horizontal_scale), py = (int64_t)(y / P->horizontal_scale);
+          px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
+          py = py < 0 ? 0 : (py > B.hf_cols - 2 ? B.hf_cols - 2 : py);
+          int h1 = H[px * B.hf_cols + py], h2 = H[(px + 1) * B.hf_cols + py], h3 = H[px * B.hf_cols + py + 1];
+          *mh = (float)min(min(h1, h2), h3) * P->vertical_scale;
+        }
+      }
     }
     __syncthreads();
   }

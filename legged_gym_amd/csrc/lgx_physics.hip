@@ -262,6 +262,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   __shared__ float leg_kin[ENVS * 4][3][12];        // body frames of the leg: R (9), origin (3)
   __shared__ float leg_sys[ENVS * 4][36];           // contact-free leg system: B 18, D 6, rb 6, rl 3
   __shared__ float env_com[ENVS][40];               // base block 21, its rhs 6, base rotation 9
+  __shared__ int16_t hf_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];  // terrain around each base
+  __shared__ int32_t hf_org[ENVS][2];
   {
     const int4* src = reinterpret_cast<const int4*>(DMg);
     int4* dst = reinterpret_cast<int4*>(&smodel);
@@ -325,6 +327,27 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 #pragma unroll
     for (int i = 0; i < 30; ++i) hist[i] = h[i];
   }
+  // heightfield patch of each env (rough terrain): LGX_HF_PATCH^2 samples centred on the base at
+  // the start of the launch; contact queries inside it read LDS instead of gathering from HBM
+  const bool use_patch = P->terrain_kind != 0 && B.height_samples != nullptr && B.hf_rows >= LGX_HF_PATCH &&
+                         B.hf_cols >= LGX_HF_PATCH;
+  if (use_patch) {
+    if (lie == 0) {
+      const float hs = P->horizontal_scale;
+      int ci = (int)floorf((pos.x + P->border_size) / hs), cj = (int)floorf((pos.y + P->border_size) / hs);
+      hf_org[eb][0] = min(max(ci - LGX_HF_PATCH / 2, 0), B.hf_rows - LGX_HF_PATCH);
+      hf_org[eb][1] = min(max(cj - LGX_HF_PATCH / 2, 0), B.hf_cols - LGX_HF_PATCH);
+    }
+    __syncthreads();
+    for (int q = tid; q < ENVS * LGX_HF_PATCH * LGX_HF_PATCH; q += PHYS_BLOCK) {
+      const int ee = q / (LGX_HF_PATCH * LGX_HF_PATCH), r = q % (LGX_HF_PATCH * LGX_HF_PATCH);
+      const int li = r / LGX_HF_PATCH, lj = r % LGX_HF_PATCH;
+      hf_patch[ee][r] = B.height_samples[(int64_t)(hf_org[ee][0] + li) * B.hf_cols + hf_org[ee][1] + lj];
+    }
+    __syncthreads();
+  }
+  const int16_t* patch = use_patch ? hf_patch[eb] : nullptr;
+  const int pi0 = use_patch ? hf_org[eb][0] : 0, pj0 = use_patch ? hf_org[eb][1] : 0;
   const int npts = DM->lane_npts[leg];
   const int maxpts = DM->max_lane_npts;
   f3 cf_leg[4] = {mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0)};
@@ -532,7 +555,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
         f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
         f3 n;
-        float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
+        float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n, patch, pi0, pj0);
         float rad = M->point_radius[pi];
         float depth = (h - (Pp.z + pos.z)) * n.z + rad;
         if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[sl][tid] = st; }
@@ -578,7 +601,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
           f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
           f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
           f3 n;
-          float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n);
+          float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n, patch, pi0, pj0);
           float rad = M->point_radius[pi];
           float depth = (h - (Pp.z + pos.z)) * n.z + rad;
           f3 Pc = Pp - rad * n;

@@ -146,6 +146,9 @@ class FusedPPOUpdate:
             else:
                 self.W.append(self.flat_p[o:o + 2 * la[k].weight.numel()].view(2, *la[k].weight.shape))
         self.Wg = [self.off[id(la[k].weight)] for k in range(self.L + 1)]
+        if self.num_obs == self.num_cobs:
+            o = self.Wg[0]
+            self.W1s = self.flat_p[o:o + 2 * la[0].weight.numel()].view(2, *la[0].weight.shape)
         self.bo = [self.off[id(la[k].bias)] for k in range(self.L + 1)]
         self.std_off = self.off[id(ac.std)]
         params = list(ac.parameters())
@@ -288,8 +291,11 @@ class FusedPPOUpdate:
             Xc = self.Xc
         # ---- forward
         wa, wc = self.W[0]
-        torch.mm(self.X, wa.t(), out=self.Y[0][0])
-        torch.mm(Xc, wc.t(), out=self.Y[0][1])
+        if cobs is None:   # shared input: one batched GEMM over {actor, critic} with a stride-0 input
+            torch.bmm(self.X.unsqueeze(0).expand(2, M, self.num_obs), self.W1s.transpose(1, 2), out=self.Y[0])
+        else:
+            torch.mm(self.X, wa.t(), out=self.Y[0][0])
+            torch.mm(Xc, wc.t(), out=self.Y[0][1])
         fp = self.flat_p
         chk(lib.lgx_bias_act(_vp(self.Y[0]), C.c_void_p(fp.data_ptr() + 4 * self.bo[0]), M, h[0], 2, 1, stream), "bias")
         for k in range(1, L):
