@@ -26,7 +26,8 @@ MI355X_F32_PEAK_TFLOPS = 157.3      # vector FP32 == f32 MFMA peak (MI355X_MICRO
 MI355X_HBM_PEAK_GBS = 8000.0
 # HBM bytes per physics launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE
 # counts half of wide reads), rocprofv3 --pmc passes in profiles/r01_pmc_env_kernels.json
-PHYS_PMC_TRAFFIC_BYTES = int((2 * 6592.1 + 19206.3) * 1024)
+PHYS_PMC_TRAFFIC_BYTES = int((2 * 4508.4 + 11584.0) * 1024)
+ACT_PMC_TRAFFIC_BYTES = int((2 * 4521.6 + 768.0) * 1024)    # actuator MLP launch, same passes
 
 
 from legged_gym_amd.sim.flops import physics_flop_per_env_substep  # noqa: E402
@@ -133,7 +134,7 @@ def main():
     value = steps_per_iter * N * world * args.steps / elapsed
 
     # roofline of the dominant lgx kernel (HIP-event durations over the timed region)
-    names = ["lgx_physics_kernel", "lgx_mlp_forward_kernel(actuator)", "lgx_post_physics_kernel"]
+    names = ["lgx_physics_kernel", "lgx_actuator_ws_kernel", "lgx_post_physics_kernel"]
     avg = [ms[i] / cnt[i] if cnt[i] else 0.0 for i in range(3)]
     dom = max(range(3), key=lambda i: ms[i])
     decim = env.cfg.control.decimation
@@ -148,8 +149,10 @@ def main():
                      "from legged_gym_amd/sim/flops.py x envs x substeps; traffic = FETCH_SIZE*2 + WRITE_SIZE "
                      "per launch from profiles/r01_pmc_env_kernels.json; latency-bound, see DESIGN.md 4.1")}
     act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
-    roof2 = {"kernel": names[1], "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-             "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None}
+    roof2 = {"kernel": "lgx_actuator_ws_kernel", "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None,
+             "traffic": ACT_PMC_TRAFFIC_BYTES if (N == 4096 and args.task == "go1_rough") else None,
+             "algorithmic_per_launch": act_flop}
     for r in (roof, roof2):
         if r["achieved"] is not None:
             r["frac"] = r["achieved"] / r["peak"]
