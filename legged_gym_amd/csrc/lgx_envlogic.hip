@@ -4,16 +4,16 @@
 // with no host synchronisation (the reference's reset_buf.nonzero() and per-term launches
 // are replaced by per-env predication and a deterministic two-stage reduction for extras).
 //
-// Block = 256 threads owns 16 envs (256 workgroups at 4096 envs).  Phases:
-//   A  (all 256 lanes) height scan: (env, point) pairs, coalesced int16 gathers
-//   B  (lanes 0..15)   one env per lane: scalar logic, rewards, reset
-//   C  (all 256 lanes) observation rows: (env, obs index) pairs, coalesced stores
+// Block = 16 lanes per env x LGX_ENV_BLOCK envs.  Phases:
+//   A  (all lanes) height scan: (env, point) pairs, coalesced int16 gathers
+//   B  (one lane per env) scalar env logic: scalar logic, rewards, reset
+//   C  (all lanes) observation rows: (env, obs index) pairs, coalesced stores
 // Extras (episode means over reset envs) are reduced per block in LDS, then by a one-block
 // finalize kernel in fixed order (bitwise reproducible).
 #include "lgx_device.h"
 #include "lgx_internal.h"
 
-#define ENV_THREADS 256
+#define ENV_THREADS (16 * LGX_ENV_BLOCK)
 
 namespace {
 
@@ -240,6 +240,24 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
     __syncthreads();
   }
 
+  // ---- stage the per-env rows the reward terms read (coalesced, all lanes) into LDS: the
+  // term loop below re-reads them many times from a single lane per env
+  constexpr int SROW = 24 + 12 + LGX_MAX_BODIES * 3 + 12 + 12 + 12;  // ds tq cf act la ldv
+  __shared__ float srow[LGX_ENV_BLOCK][SROW + 1];
+  for (int idx = tid; idx < LGX_ENV_BLOCK * SROW; idx += ENV_THREADS) {
+    const int le = idx / SROW, c = idx - le * SROW;
+    const int e = min(e0 + le, N - 1);
+    float v;
+    if (c < 24) v = B.dof_state[(int64_t)e * 24 + c];
+    else if (c < 36) v = B.torques[(int64_t)e * 12 + c - 24];
+    else if (c < 36 + LGX_MAX_BODIES * 3) v = B.contact_forces[(int64_t)e * LGX_MAX_BODIES * 3 + c - 36];
+    else if (c < 48 + LGX_MAX_BODIES * 3) v = B.actions[(int64_t)e * 12 + c - 36 - LGX_MAX_BODIES * 3];
+    else if (c < 60 + LGX_MAX_BODIES * 3) v = B.last_actions[(int64_t)e * 12 + c - 48 - LGX_MAX_BODIES * 3];
+    else v = B.last_dof_vel[(int64_t)e * 12 + c - 60 - LGX_MAX_BODIES * 3];
+    srow[le][c] = v;
+  }
+  __syncthreads();
+
   // ---- phase B: one env per lane
   if (tid < LGX_ENV_BLOCK) {
     const int e = e0 + tid;
@@ -266,12 +284,12 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
         rs[7] = (mv - -mv) * D(e, LGX_DRAW_PUSH, step, 0u) + -mv;
         rs[8] = (mv - -mv) * D(e, LGX_DRAW_PUSH + 1, step, 0u) + -mv;
       }
-      v.ds = B.dof_state + (int64_t)e * 24;
-      v.tq = B.torques + (int64_t)e * 12;
-      v.cf = B.contact_forces + (int64_t)e * LGX_MAX_BODIES * 3;
-      v.act = B.actions + (int64_t)e * 12;
-      v.la = B.last_actions + (int64_t)e * 12;
-      v.ldv = B.last_dof_vel + (int64_t)e * 12;
+      v.ds = srow[tid];                    // pre-reset rows, staged above
+      v.tq = srow[tid] + 24;
+      v.cf = srow[tid] + 36;
+      v.act = srow[tid] + 36 + LGX_MAX_BODIES * 3;
+      v.la = srow[tid] + 48 + LGX_MAX_BODIES * 3;
+      v.ldv = srow[tid] + 60 + LGX_MAX_BODIES * 3;
       v.fat = B.feet_air_time + (int64_t)e * 4;
       v.rootz = rs[2];
       v.mh = B.measured_heights ? B.measured_heights + (int64_t)e * P->num_height_points : nullptr;
@@ -319,10 +337,11 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
 
   // ---- phase C: observations (:214-231) + noise + clip (:103-104)
   const int total = LGX_ENV_BLOCK * nobs;
+#pragma unroll 4
   for (int idx = tid; idx < total; idx += ENV_THREADS) {
     int le = idx / nobs, i = idx - le * nobs;
     int e = e0 + le;
-    if (e >= N) break;
+    if (e >= N) continue;
     float o;
     if (i < 3) o = B.base_lin_vel[(int64_t)e * 3 + i] * P->obs_scale_lin_vel;
     else if (i < 6) o = B.base_ang_vel[(int64_t)e * 3 + i - 3] * P->obs_scale_ang_vel;
@@ -381,28 +400,24 @@ __global__ void __launch_bounds__(256)
 lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks, int32_t level_scan) {
   const int N = P->num_envs;
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
-  __shared__ float red[256];
   __shared__ float sums[LGX_PARTIAL_STRIDE];
-  int t = threadIdx.x;
-  // 256 threads: each (row, block-slice) pair accumulates, fixed order -> reproducible
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave w reduces rows w, w+4, ...: lanes take blocks lane, lane+64, ... then a fixed-order
+  // butterfly (deterministic, no atomics)
   const int rows = T + 2;
-  for (int r = 0; r < rows; ++r) {
+  for (int r = wave; r < rows; r += 4) {
     float s = 0.f;
     if (r == T + 1 && level_scan) {
       if (P->curriculum)
-        for (int e = t; e < N; e += 256) s += (float)B.terrain_levels[e];
+        for (int e = lane; e < N; e += 64) s += (float)B.terrain_levels[e];
     } else {
-      for (int b = t; b < nblocks; b += 256) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + r];
+      for (int b = lane; b < nblocks; b += 64) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + r];
     }
-    red[t] = s;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (t < w) red[t] += red[t + w];
-      __syncthreads();
-    }
-    if (t == 0) sums[r] = red[0];
-    __syncthreads();
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) sums[r] = s;
   }
+  __syncthreads();
   float count = sums[T];
   if (count <= 0.f) return;  // reference keeps stale extras (legged_robot.py:160-161)
   if (t < T) B.extras[t] = (sums[t] / count) / P->max_episode_length_s;

@@ -46,5 +46,7 @@ struct lgx_reduce_jobs {
 };
 
 // scratch layout (floats): [blocks][LGX_MAX_TERMS + 2] reduction partials
-#define LGX_ENV_BLOCK 16
+#ifndef LGX_ENV_BLOCK
+#define LGX_ENV_BLOCK 16  // envs per post-physics workgroup (16 lanes each)
+#endif
 #define LGX_PARTIAL_STRIDE (LGX_MAX_TERMS + 2)

@@ -476,7 +476,7 @@ class LeggedRobot(BaseTask):
         self._backend = self._make_backend(self._lgx_model, p, b)
 
     def _scratch_floats(self):
-        blocks = (self.num_envs + abi.ENV_BLOCK - 1) // abi.ENV_BLOCK  # == lgx_scratch_floats()
+        blocks = (self.num_envs + abi.ENV_BLOCK - 1) // abi.ENV_BLOCK  # >= lgx_scratch_floats()
         return blocks * (abi.MAX_TERMS + 2) + 64
 
     def _make_backend(self, model, params, bufs):

@@ -13,7 +13,7 @@ MAX_POINTS = 128
 MAX_OBS = 256
 MAX_HEIGHT_POINTS = 192
 MAX_TERMS = 24
-ENV_BLOCK = 16   # envs per post-physics workgroup (scratch partial rows)
+ENV_BLOCK = 4    # smallest envs-per-workgroup the post-physics kernel is built with (sizes scratch)
 
 # reward term ids (enum lgx_reward_term) keyed by the reference's `_reward_<name>` suffix
 REWARD_IDS = {
