@@ -23,6 +23,25 @@ import torch.nn as nn
 from legged_gym_amd.sim import abi
 
 
+def _use_tuned_gemms():
+    """Load the GEMM solution table tuned on MI355X for the PPO-update shapes (torch TunableOp,
+    rocBLAS / hipBLASLt solutions; regenerate with tools/tune_gemms.sh).  Read-only: shapes that
+    are not in the table run the library default.  LGX_TUNED_GEMMS=0 disables."""
+    import os
+    if os.environ.get("LGX_TUNED_GEMMS", "1") == "0":
+        return
+    import torch.cuda.tunable as tunable
+    from legged_gym_amd import LEGGED_GYM_ROOT_DIR
+    path = os.path.join(LEGGED_GYM_ROOT_DIR, "resources", "tunableop", "ppo_gemms_gfx950.csv")
+    if not os.path.exists(path) or tunable.is_enabled():
+        return
+    tunable.enable(True)
+    tunable.tuning_enable(False)
+    tunable.record_untuned_enable(False)
+    tunable.set_filename(path, insert_device_ordinal=False)
+    tunable.read_file(path)
+
+
 def _vp(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -106,6 +125,7 @@ class FusedPPOUpdate:
         from legged_gym_amd.sim import lib as lgxlib
         self.lib = lgxlib.load()
         self.check = lgxlib.check
+        _use_tuned_gemms()
         self.ppo = ppo
         ac = ppo.actor_critic
         self.dev = next(ac.parameters()).device
