@@ -189,7 +189,17 @@ class LeggedRobot(BaseTask):
                                             device=self.device)
         self._get_env_origins()
         self._process_dof_props()
-        self._process_rigid_shape_props()
+        # the reference's per-env creation loop (legged_robot.py:707-728) draws each env's start
+        # pose offset (torch, on self.device; the pose itself is overwritten by the first reset)
+        # and builds the friction tables (CPU torch generator) right after env 0's draw: keep
+        # that consumption order so the same seed gives the same friction buckets
+        if str(self.device) == "cpu":
+            torch_rand_float(-1., 1., (2, 1), device=self.device)
+            self._process_rigid_shape_props()
+            for _ in range(1, self.num_envs):
+                torch_rand_float(-1., 1., (2, 1), device=self.device)
+        else:
+            self._process_rigid_shape_props()
         self._process_rigid_body_props()
         idx = lambda names: torch.tensor([body_names.index(n) for n in names], dtype=torch.long, device=self.device)
         self.feet_indices = idx(feet_names)
@@ -222,11 +232,19 @@ class LeggedRobot(BaseTask):
         masses = np.array([b["mass"] for b in rb], dtype=np.float64)
         rnd = np.tile(masses, (self.num_envs, 1))
         dr = self.cfg.domain_rand
-        if dr.randomize_base_mass:
-            rnd[:, 0] += np.random.uniform(dr.added_mass_range[0], dr.added_mass_range[1], self.num_envs)
-        if dr.randomize_limb_mass:
-            rnd[:, 1:] *= 1 + np.random.uniform(dr.added_limb_percentage[0], dr.added_limb_percentage[1],
-                                                (self.num_envs, len(rb) - 1))
+        # numpy draws in the reference's order: env-major, body 0 (base) then bodies 1.. (limbs);
+        # np.random.uniform(lo, hi) == lo + (hi - lo) * random_sample()
+        cols = ([0] if dr.randomize_base_mass else []) + (list(range(1, len(rb))) if dr.randomize_limb_mass else [])
+        if cols:
+            u = np.random.random_sample((self.num_envs, len(cols)))
+            for j, bi in enumerate(cols):
+                if bi == 0:
+                    lo, hi = dr.added_mass_range
+                    rnd[:, 0] += lo + (hi - lo) * u[:, j]
+                else:
+                    lo, hi = dr.added_limb_percentage
+                    rnd[:, bi] *= 1 + (lo + (hi - lo) * u[:, j])
+        self.body_masses = rnd   # [N, reporting bodies] after randomisation (float64, as set on the actor)
         dyn_mass = np.zeros((self.num_envs, abi.NUM_DYN))
         for i, b in enumerate(rb):
             dyn_mass[:, b["dyn_body"]] += rnd[:, i]

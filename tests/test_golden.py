@@ -63,7 +63,7 @@ def close(a, b, atol, rtol):
 @pytest.mark.parametrize("name", list(CASES))
 def test_setup_constants_match_reference(name):
     g = load(name)
-    env = make_env(CASES[name], num_envs=int(g["num_envs"]), device="cpu", backend="oracle")
+    env = make_env(CASES[name], num_envs=int(g["num_envs"]), device="cpu", backend="oracle", seed=int(g["seed"]))
     assert env.max_episode_length == float(g["max_episode_length"]) == 1001.0       # legged_robot.py:777
     assert env.dt == pytest.approx(float(g["dt"]), abs=0)
     assert env.cfg.domain_rand.push_interval == float(g["push_interval"])
@@ -76,6 +76,15 @@ def test_setup_constants_match_reference(name):
     assert env.penalised_contact_indices.tolist() == g["penalised_contact_indices"].tolist()
     assert env.termination_contact_indices.tolist() == g["termination_contact_indices"].tolist()
     assert list(env.episode_sums.keys()) == [str(x) for x in g["episode_keys"]]
+    # domain randomisation at creation (legged_robot.py:259-335) with the same seed: friction
+    # buckets (CPU torch generator) and per-env body masses (numpy) as the reference set them
+    if "dr_friction" in g:
+        np.testing.assert_array_equal(env.friction_coeffs.numpy(), g["dr_friction"])
+    np.testing.assert_allclose(env.body_masses, g["dr_body_masses"], rtol=1e-12, atol=0)
+    # terrain placement at creation (legged_robot.py:742-767): levels, types -> env origins
+    if "setup_terrain_levels" in g:
+        np.testing.assert_array_equal(env.terrain_levels.numpy(), g["setup_terrain_levels"])
+    np.testing.assert_allclose(env.env_origins.numpy(), g["setup_env_origins"], rtol=0, atol=1e-6)
 
 
 @pytest.mark.parametrize("name", list(CASES))

@@ -130,6 +130,7 @@ def make_isaacgym_stub(model):
 
         def __init__(self):
             self.n = 0
+            self.body_masses = []
             self.sim_calls = 0
             self.next_state = None
             self.decimation = 4
@@ -182,6 +183,9 @@ def make_isaacgym_stub(model):
 
         def get_actor_rigid_body_properties(self, e, h):
             return [Obj(mass=b["mass"]) for b in model["report_bodies"]]
+
+        def set_actor_rigid_body_properties(self, e, h, props, recomputeInertia=False):
+            self.body_masses.append([p.mass for p in props])   # domain-randomised masses per env
 
         def find_actor_rigid_body_handle(self, e, h, name):
             return model["body_names"].index(name)
@@ -360,6 +364,8 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
     stride = abi.DRAW_NOISE + env.num_obs
     gen = torch.Generator().manual_seed(seed + 100)
     instrument(env, stride)
+    setup_levels = env.terrain_levels.clone().numpy() if hasattr(env, "terrain_levels") else None
+    setup_origins = env.env_origins.clone().numpy()
     # initial reset() with injected draws
     DrawCtx.table = torch.rand(num_envs, stride, generator=gen)
     init_draws = DrawCtx.table.clone()
@@ -370,7 +376,14 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
     el[1::7] = 1000
     el[2::7] = 998
     env.common_step_counter = 748
-    rec = {"name": name, "num_envs": num_envs, "steps": steps, "stride": stride}
+    rec = {"name": name, "num_envs": num_envs, "steps": steps, "stride": stride, "seed": seed}
+    # domain randomisation at creation (legged_robot.py:259-335): friction buckets, body masses
+    rec["dr_body_masses"] = np.array(gym.body_masses, np.float64)
+    rec["setup_env_origins"] = setup_origins
+    if setup_levels is not None:
+        rec["setup_terrain_levels"] = setup_levels
+    if hasattr(env, "friction_coeffs"):
+        rec["dr_friction"] = env.friction_coeffs.reshape(-1).numpy().astype(np.float32)
     init_state = snapshot(env, REC_KEYS + ["terrain_levels"] if hasattr(env, "terrain_levels") else REC_KEYS)
     init_state["episode_sums"] = np.stack([env.episode_sums[k].numpy() for k in env.episode_sums])
     init_state["common_step_counter"] = np.array(env.common_step_counter)
