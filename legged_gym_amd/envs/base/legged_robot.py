@@ -385,7 +385,11 @@ class LeggedRobot(BaseTask):
         return None
 
     def _control_type(self):
-        # the reference step path drives joints through PhysX position drives (legged_robot.py:93-96)
+        # the reference step path drives joints through PhysX position drives (legged_robot.py:93-96);
+        # cfg.control.explicit_torques selects its commented-out explicit path, _compute_torques
+        # (legged_robot.py:90-91,370-392), with control_type P | V | T
+        if getattr(self.cfg.control, "explicit_torques", False):
+            return abi.CTRL[self.cfg.control.control_type]
         return abi.CTRL["POS_DRIVE"]
 
     def _build_lgx(self):

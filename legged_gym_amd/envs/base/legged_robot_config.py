@@ -64,6 +64,7 @@ class LeggedRobotCfg(BaseConfig):
 
     class control:  # ref :93-101
         control_type = 'P'          # P | V | T (explicit-torque path, _compute_torques)
+        explicit_torques = False    # lgx: True = _compute_torques instead of the PhysX position drive
         stiffness = {'joint_a': 10.0, 'joint_b': 15.}
         damping = {'joint_a': 1.0, 'joint_b': 1.5}
         action_scale = 0.5

@@ -307,3 +307,27 @@ def test_splitk_linear_gradients_match_torch(gpu):
     for a, b in ((lin.weight.grad, ref.weight.grad), (lin.bias.grad, ref.bias.grad), (x.grad, x2.grad)):
         ok, e = close(a, b, 1e-2, 1e-4)
         assert ok, f"split-K grad max err {e}"
+
+
+@pytest.mark.parametrize("ctrl", ["P", "V", "T"])
+def test_explicit_torque_control_matches_oracle(gpu, ctrl):
+    """_compute_torques (legged_robot.py:370-392) instead of the position drive: one env step."""
+    def ov(c):
+        c.control.explicit_torques = True
+        c.control.control_type = ctrl
+    ora = make_env("go1_flat_bench", num_envs=64, device="cpu", backend="oracle", overrides=ov)
+    dev = make_env("go1_flat_bench", num_envs=64, device="cuda:0", backend="lgx", overrides=ov)
+    gen = torch.Generator().manual_seed(21)
+    randomize_state(ora, gen)
+    sync(ora, dev)
+    a = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+    ora.step(a)
+    dev.step(a.cuda())
+    torch.cuda.synchronize()
+    ok, e = close(dev.torques, ora.torques, 1e-3, 1e-3)
+    assert ok, f"torques max err {e}"
+    assert (dev.torques.abs() <= dev.torque_limits + 1e-4).all()
+    ok, e = close(dev.dof_state, ora.dof_state, 5e-3, 2e-3)
+    assert ok, f"dof max err {e}"
+    ok, e = close(dev.obs_buf, ora.obs_buf, 5e-3, 5e-3)
+    assert ok, f"obs max err {e}"
