@@ -211,7 +211,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
       const float* rs = B.root_states + (int64_t)e * 13;
       float z = rs[5], w = rs[6];
       float nrm = fmaxf(sqrtf(z * z + w * w), 1e-9f);
-      base_xy_yaw[tid] = make_float4(rs[0] + P->border_size, rs[1] + P->border_size, z / nrm, w / nrm);
+      base_xy_yaw[tid] = make_float4(rs[0], rs[1], z / nrm, w / nrm);
     }
     __syncthreads();
     const int np = P->num_height_points;
@@ -228,7 +228,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
         } else {
           const float4 b = base_xy_yaw[le];
           f3 o = quat_apply(0.f, 0.f, b.z, b.w, mk3(P->height_points[i][0], P->height_points[i][1], 0.f));
-          float x = o.x + b.x, y = o.y + b.y;
+          float x = o.x + b.x + P->border_size, y = o.y + b.y + P->border_size;  // (p + root) + border, as :833-834
           int64_t px = (int64_t)(x / P->horizontal_scale), py = (int64_t)(y / P->horizontal_scale);
           px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
           py = py < 0 ? 0 : (py > B.hf_cols - 2 ? B.hf_cols - 2 : py);
