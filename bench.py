@@ -88,10 +88,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU (identity on a full node); LGX_DIST_BACKEND=gloo with more ranks than GPUs
+    # rehearses the data-parallel path on a single device
+    backend = os.environ.get("LGX_DIST_BACKEND", "nccl")
+    ngpu = torch.cuda.device_count() if backend != "nccl" else 0
+    if ngpu:
+        local = local % ngpu
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     device = f"cuda:{local}"
     import legged_gym_amd.envs  # noqa: F401
     from legged_gym_amd.sim import lib as lgxlib
