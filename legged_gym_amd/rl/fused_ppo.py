@@ -6,10 +6,10 @@ Per minibatch (M rows), on one stream, no host synchronisation:
   hidden layers: library GEMM (mm for layer 1, bmm over {actor, critic} after) + lgx_bias_act
   heads: mm; lgx_ppo_loss = log-prob / ratio / clipped surrogate / clipped value loss / entropy
          / KL and the analytic gradient w.r.t. mu, value, std, head biases
-  lgx_ppo_adapt_lr (device-side adaptive schedule; KL all-reduced first when data-parallel)
+  lgx_ppo_adapt_lr (device-side adaptive schedule; data-parallel: KL rides in the gradient all-reduce)
   backward: lgx_head_bwd, then per layer split-K bmm for dW, bmm for dA, lgx_elu_bwd_colsum
   lgx_reduce_slices: all split-K and bias partials -> flat gradient (one launch)
-  [all-reduce of the flat gradient over RCCL when data-parallel]
+  [ONE all-reduce over RCCL when data-parallel: flat gradient + the minibatch KL]
   lgx_adam_clip: clip_grad_norm_(max_grad_norm) + Adam on the flat buffers
 The module's nn.Parameters become views of the flat buffer, so state_dict / load_state_dict /
 the rollout's fused inference see the updated weights; the optimizer is `FlatAdam`, whose
@@ -145,7 +145,10 @@ class FusedPPOUpdate:
         order.append(ac.std)
         n = sum(p.numel() for p in order)
         self.flat_p = torch.zeros(n, device=self.dev)
-        self.flat_g = torch.zeros(n, device=self.dev)
+        # gradient buffer + one trailing slot: the minibatch KL rides in the same all-reduce as the
+        # gradient when data-parallel (one collective per minibatch)
+        self.g_comm = torch.zeros(n + 1, device=self.dev)
+        self.flat_g = self.g_comm[:n]
         self.off = {}
         off = 0
         with torch.no_grad():
@@ -328,12 +331,9 @@ class FusedPPOUpdate:
         # ---- loss, gradient at the heads, KL -> adaptive learning rate
         args.idx = idx.data_ptr()
         chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
-        kl_scale = 1.0
-        if ppo.dist is not None:
-            ppo.dist.all_reduce(self.stats[0:1])
-            kl_scale = 1.0 / ppo.dist.get_world_size()
-        if ppo.desired_kl is not None and ppo.schedule == "adaptive":
-            chk(lib.lgx_ppo_adapt_lr(_vp(self.stats), kl_scale, _vp(self.optimizer.lr_dev), ppo.desired_kl, stream),
+        adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"
+        if adaptive and ppo.dist is None:   # (data-parallel: after the joint all-reduce below)
+            chk(lib.lgx_ppo_adapt_lr(_vp(self.stats), 1.0, _vp(self.optimizer.lr_dev), ppo.desired_kl, stream),
                 "adapt_lr")
         # ---- backward
         chk(lib.lgx_head_bwd(_vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc), _vp(self.Y[L - 1]), M, A, h[-1],
@@ -354,8 +354,14 @@ class FusedPPOUpdate:
             return
         grad_scale = 1.0
         if ppo.dist is not None:
-            ppo.dist.all_reduce(self.flat_g)
+            # one collective: summed gradient + summed KL (rsl_rl adapts the LR before the step,
+            # only the optimizer step reads it, so adapting after the backward is equivalent)
+            self.g_comm[self.n:].copy_(self.stats[0:1])
+            ppo.dist.all_reduce(self.g_comm)
             grad_scale = 1.0 / ppo.dist.get_world_size()
+            if adaptive:
+                chk(lib.lgx_ppo_adapt_lr(C.c_void_p(self.g_comm.data_ptr() + 4 * self.n), grad_scale,
+                                         _vp(self.optimizer.lr_dev), ppo.desired_kl, stream), "adapt_lr")
         o = self.optimizer
         chk(lib.lgx_adam_clip(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n, _vp(self.norm_parts),
                               self.norm_parts.numel(), grad_scale, ppo.max_grad_norm, _vp(o.lr_dev), _vp(o.step_dev),
