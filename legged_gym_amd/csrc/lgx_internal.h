@@ -17,7 +17,6 @@ struct lgx_dev_model {
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                        int32_t nsub, int32_t from_actions, hipStream_t stream);
-int lgx_launch_clip_actions(float* a, int64_t n, float clip, hipStream_t stream);
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
                             int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
                             hipStream_t stream);

@@ -707,12 +707,6 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   }
 }
 
-// clip actions in place (legged_robot.py:85-86): one thread per element
-__global__ void lgx_clip_actions_kernel(float* a, int64_t n, float clip) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) a[i] = clampf(a[i], -clip, clip);
-}
-
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                        int32_t nsub, int32_t from_actions, hipStream_t stream) {
   // lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches
@@ -731,8 +725,3 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int lgx_launch_clip_actions(float* a, int64_t n, float clip, hipStream_t stream) {
-  int blocks = (int)((n + 255) / 256);
-  hipLaunchKernelGGL(lgx_clip_actions_kernel, dim3(blocks), dim3(256), 0, stream, a, n, clip);
-  return hipGetLastError() == hipSuccess ? 0 : -2;
-}
