@@ -11,6 +11,7 @@ torch.distributed.run (one rank per GPU, env vars RANK/LOCAL_RANK/WORLD_SIZE/MAS
 """
 import argparse
 import ctypes as C
+import gc
 import json
 import os
 import sys
@@ -45,8 +46,8 @@ WORKLOADS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--task", default="go1_rough")
     p.add_argument("--num_envs", type=int, default=4096)
     p.add_argument("--no_cpu_baseline", action="store_true")
@@ -120,6 +121,8 @@ def main():
     handle = env._backend.handle
 
     runner.learn(args.warmup)
+    gc.collect()
+    gc.disable()   # no collector pauses inside the timed region (host-side Python only)
     lib.lgx_profile_enable(handle, 1)
     if world > 1:
         dist.barrier()
@@ -130,6 +133,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     lib.lgx_profile_enable(handle, 0)
     ms = (C.c_double * 3)()
     cnt = (C.c_int64 * 3)()

@@ -41,7 +41,8 @@ int lgx_hip_status(const char* what);  // LGX_OK or LGX_EHIP from hipGetLastErro
 // a batch of reduction jobs passed by value to one launch (lgx_reduce_slices)
 struct lgx_reduce_jobs {
   lgx_reduce_job job[LGX_MAX_REDUCE_JOBS];
-  int32_t tile_start[LGX_MAX_REDUCE_JOBS];  // first 64-output tile of each job in the flat grid
+  int32_t tile_start[LGX_MAX_REDUCE_JOBS];    // first tile of each job in the flat grid
+  int32_t tile_outputs[LGX_MAX_REDUCE_JOBS];  // outputs per tile (16 or 64)
 };
 
 // scratch layout (floats): [blocks][LGX_MAX_TERMS + 2] reduction partials

@@ -46,24 +46,27 @@ gather_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, const
 // ---------------------------------------------------------------------------------------- rollout
 // PPO.act + RolloutStorage.add_transitions for one env step (rsl_rl v1.0.x): actions =
 // mu + std * eps (Normal.sample with the caller's standard-normal draws), log-prob, and the
-// storage row t (obs, critic obs, actions, value, log-prob, mu, sigma).  64 envs per workgroup:
-// the obs rows of those envs are one contiguous range, copied coalesced by all 256 lanes.
+// storage row t (obs, critic obs, actions, value, log-prob, mu, sigma).  16 envs per workgroup
+// (256 workgroups at 4096 envs): the obs rows of those envs are one contiguous range, copied
+// with 16-byte accesses when aligned.
+constexpr int ACT_ENVS = 16;
+
+__device__ __forceinline__ void copy_rows(const float* __restrict__ src, float* __restrict__ dst, int64_t cnt) {
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int64_t c4 = cnt >> 2;
+    for (int64_t i = threadIdx.x; i < c4; i += TPB)
+      reinterpret_cast<float4*>(dst)[i] = reinterpret_cast<const float4*>(src)[i];
+    for (int64_t i = 4 * c4 + threadIdx.x; i < cnt; i += TPB) dst[i] = src[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < cnt; i += TPB) dst[i] = src[i];
+  }
+}
 __global__ void __launch_bounds__(TPB)
 ppo_act_kernel(lgx_ppo_act_args a) {
-  const int64_t n0 = (int64_t)blockIdx.x * 64;
-  const int64_t nn = min((int64_t)64, a.num_envs - n0);
-  {
-    const int64_t cnt = nn * a.num_obs;
-    const float* src = a.obs + n0 * a.num_obs;
-    float* dst = a.st_obs + n0 * a.num_obs;
-    for (int64_t i = threadIdx.x; i < cnt; i += TPB) dst[i] = src[i];
-    if (a.cobs && a.st_cobs) {
-      const int64_t cc = nn * a.num_cobs;
-      const float* cs = a.cobs + n0 * a.num_cobs;
-      float* cd = a.st_cobs + n0 * a.num_cobs;
-      for (int64_t i = threadIdx.x; i < cc; i += TPB) cd[i] = cs[i];
-    }
-  }
+  const int64_t n0 = (int64_t)blockIdx.x * ACT_ENVS;
+  const int64_t nn = min((int64_t)ACT_ENVS, a.num_envs - n0);
+  copy_rows(a.obs + n0 * a.num_obs, a.st_obs + n0 * a.num_obs, nn * a.num_obs);
+  if (a.cobs && a.st_cobs) copy_rows(a.cobs + n0 * a.num_cobs, a.st_cobs + n0 * a.num_cobs, nn * a.num_cobs);
   const int A = a.num_actions;
   for (int64_t k = threadIdx.x; k < nn * A; k += TPB) {  // coalesced [env, action] elements
     const int64_t e = n0 * A + k;
@@ -345,17 +348,20 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
 
 // ---------------------------------------------------------------------------------------- reductions
 // job: dst[j][i] = sum_s src[j*job_stride + s*slice_stride + i] for s < S, i < n, j < count.
-// Workgroup = one 64-output tile of one job; its 4 waves split the slices (s = wave, wave+4,
-// ...) and combine in LDS in a fixed order: long slice loops (hundreds of chunk partials)
-// run 4-wide with independent loads in flight instead of one serial chain per output.
+// Workgroup = one tile of OT outputs of one job; its 256 / OT lane groups split the slices
+// (s = g, g + 256/OT, ...) and combine in LDS in a fixed order.  OT = 64 for short slice loops
+// (split-K partials, 8 slices), 16 for long ones (per-chunk bias / head partials, hundreds of
+// slices): independent loads in flight instead of one serial chain per output.
 __global__ void __launch_bounds__(TPB)
 reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs) {
-  __shared__ float red[4][64];
+  __shared__ float red[TPB];
   int b = blockIdx.x, ji = 0;
   while (ji + 1 < njobs && b >= jobs.tile_start[ji + 1]) ++ji;
   const lgx_reduce_job& jb = jobs.job[ji];
-  const int64_t o = (int64_t)(b - jobs.tile_start[ji]) * 64 + (threadIdx.x & 63);
-  const int w = threadIdx.x >> 6;
+  const int ot = jobs.tile_outputs[ji];
+  const int groups = TPB / ot;
+  const int t = threadIdx.x, oi = t % ot, g = t / ot;
+  const int64_t o = (int64_t)(b - jobs.tile_start[ji]) * ot + oi;
   const int64_t total = (int64_t)jb.count * jb.n;
   float acc = 0.f;
   int64_t j = 0, i = 0;
@@ -364,13 +370,14 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs) {
     i = o % jb.n;
     const float* s = jb.src + j * jb.job_stride + i;
 #pragma unroll 8
-    for (int k = w; k < jb.slices; k += 4) acc += s[(int64_t)k * jb.slice_stride];
+    for (int k = g; k < jb.slices; k += groups) acc += s[(int64_t)k * jb.slice_stride];
   }
-  red[w][threadIdx.x & 63] = acc;
+  red[t] = acc;
   __syncthreads();
-  if (w == 0 && o < total) {
-    int l = threadIdx.x;
-    jb.dst[j * jb.dst_stride + i] = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
+  if (g == 0 && o < total) {
+    float sum = red[oi];
+    for (int q = 1; q < groups; ++q) sum += red[q * ot + oi];
+    jb.dst[j * jb.dst_stride + i] = sum;
   }
 }
 
@@ -459,7 +466,8 @@ extern "C" int lgx_ppo_act(const lgx_ppo_act_args* args, void* stream) {
       !a.actions_out || !a.st_obs || !a.st_actions || !a.st_values || !a.st_logp || !a.st_mu || !a.st_sigma ||
       ((a.cobs != nullptr) != (a.st_cobs != nullptr)))
     return lgx_fail(LGX_EINVAL, "lgx_ppo_act: bad args");
-  hipLaunchKernelGGL(ppo_act_kernel, dim3((unsigned)((a.num_envs + 63) / 64)), dim3(TPB), 0, LGX_STREAM(stream), a);
+  hipLaunchKernelGGL(ppo_act_kernel, dim3((unsigned)((a.num_envs + ACT_ENVS - 1) / ACT_ENVS)), dim3(TPB), 0,
+                     LGX_STREAM(stream), a);
   return lgx_hip_status("lgx_ppo_act");
 }
 
@@ -552,7 +560,8 @@ extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void
       return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job");
     J.job[i] = j;
     J.tile_start[i] = (int32_t)tiles;
-    tiles += ((int64_t)j.count * j.n + 63) / 64;
+    J.tile_outputs[i] = j.slices > 32 ? 16 : 64;
+    tiles += ((int64_t)j.count * j.n + J.tile_outputs[i] - 1) / J.tile_outputs[i];
   }
   if (tiles > (1 << 30)) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: too large");
   hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs);
