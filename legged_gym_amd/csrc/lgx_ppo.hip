@@ -26,6 +26,7 @@ namespace {
 constexpr int TPB = 256;
 constexpr int CHUNK = 64;  // rows per workgroup in the backward epilogues
 constexpr int HEAD_CHUNK = 32;  // rows per workgroup in the output-layer backward
+constexpr int LOSS_TPB = 64;    // rows per loss workgroup (384 workgroups per 24576-row minibatch)
 
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
@@ -130,13 +131,13 @@ bias_act_kernel(float* __restrict__ z, const float* __restrict__ b, int64_t rows
 //   [A, 2A)     d loss / d b4a_j          (= sum of dMU over rows)
 //   2A          d loss / d b4c            (= sum of dV)
 //   2A+1        KL sum, 2A+2 surrogate sum, 2A+3 value-loss sum
-__global__ void __launch_bounds__(TPB)
+__global__ void __launch_bounds__(LOSS_TPB)
 ppo_loss_kernel(lgx_ppo_loss_args a) {
   constexpr int MAXA = LGX_PPO_MAX_ACTIONS;
   const int A = a.num_actions;
   const int NP = 2 * A + 4;
-  __shared__ float red[TPB][2 * MAXA + 4 + 1];
-  const int64_t r = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  __shared__ float red[LOSS_TPB][2 * MAXA + 4 + 1];
+  const int64_t r = (int64_t)blockIdx.x * LOSS_TPB + threadIdx.x;
   float* my = red[threadIdx.x];
   for (int k = 0; k < NP; ++k) my[k] = 0.f;
   if (r < a.rows) {
@@ -202,7 +203,7 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
   __syncthreads();
   if (threadIdx.x < NP) {
     float s = 0.f;
-    for (int t = 0; t < TPB; ++t) s += red[t][threadIdx.x];
+    for (int t = 0; t < LOSS_TPB; ++t) s += red[t][threadIdx.x];
     a.partials[(int64_t)blockIdx.x * NP + threadIdx.x] = s;
   }
 }
@@ -218,9 +219,16 @@ ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) {
   const int grp = threadIdx.x / 32;
   {
     for (int kk = threadIdx.x % 32; kk < NP; kk += 32) {
-      float s = 0.f;
-      for (int b = grp; b < nblocks; b += 8) s += a.partials[(int64_t)b * NP + kk];
-      red[grp][kk] = s;
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;   // 4 independent chains, fixed order
+      int b = grp;
+      for (; b + 24 < nblocks; b += 32) {
+        s0 += a.partials[(int64_t)b * NP + kk];
+        s1 += a.partials[(int64_t)(b + 8) * NP + kk];
+        s2 += a.partials[(int64_t)(b + 16) * NP + kk];
+        s3 += a.partials[(int64_t)(b + 24) * NP + kk];
+      }
+      for (; b < nblocks; b += 8) s0 += a.partials[(int64_t)b * NP + kk];
+      red[grp][kk] = (s0 + s1) + (s2 + s3);
     }
   }
   __syncthreads();
@@ -259,7 +267,8 @@ __global__ void __launch_bounds__(TPB)
 head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, const float* __restrict__ W4a,
                 const float* __restrict__ W4c, float* __restrict__ A3, int64_t rows, int32_t A, int32_t H,
                 float* __restrict__ partials) {
-  __shared__ float dmu[HEAD_CHUNK][MAXA + 1];
+  constexpr int DS = ((MAXA + 1 + 3) / 4) * 4;  // dMU row (+ dV) padded for 16-byte LDS reads
+  __shared__ __align__(16) float dmu[HEAD_CHUNK][DS];
   const int64_t r0 = (int64_t)blockIdx.x * HEAD_CHUNK;
   const int nr = (int)min((int64_t)HEAD_CHUNK, rows - r0);
   for (int i = threadIdx.x; i < HEAD_CHUNK * (A + 1); i += TPB) {
@@ -284,14 +293,23 @@ head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, c
     float cs = 0.f;
     for (int rr = 0; rr < nr; ++rr) {
       float y = col[(int64_t)rr * H];
-      float dA = 0.f;
+      float drow[DS];
 #pragma unroll
-      for (int j = 0; j < MAXA; ++j) {
-        if (j < nj) {
-          float d = dmu[rr][jo + j];
-          acc[j] += d * y;
-          dA += d * w[j];
-        }
+      for (int q = 0; q < DS / 4; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(&dmu[rr][4 * q]);
+        drow[4 * q] = v.x; drow[4 * q + 1] = v.y; drow[4 * q + 2] = v.z; drow[4 * q + 3] = v.w;
+      }
+      float dA = 0.f;
+      if (net == 0) {
+#pragma unroll
+        for (int j = 0; j < MAXA; ++j)
+          if (j < nj) { acc[j] += drow[j] * y; dA += drow[j] * w[j]; }
+      } else {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j <= MAXA; ++j) d = (j == A) ? drow[j] : d;   // dV column
+        acc[0] += d * y;
+        dA = d * w[0];
       }
       float dz = dA * elu_grad_from_out(y);
       col[(int64_t)rr * H] = dz;
@@ -493,7 +511,7 @@ extern "C" int lgx_bias_act(float* z, const float* b, int64_t rows, int32_t cols
 }
 
 extern "C" int64_t lgx_ppo_loss_partials_floats(int64_t rows, int32_t num_actions) {
-  return ((rows + TPB - 1) / TPB) * (2 * (int64_t)num_actions + 4);
+  return ((rows + LOSS_TPB - 1) / LOSS_TPB) * (2 * (int64_t)num_actions + 4);
 }
 
 extern "C" int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream) {
@@ -504,8 +522,8 @@ extern "C" int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream) {
       !a.target_values || !a.returns || !a.d_mu || !a.d_v || !a.partials || !a.g_std || !a.g_b4a || !a.g_b4c ||
       !a.stats)
     return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: bad args");
-  int blocks = (int)((a.rows + TPB - 1) / TPB);
-  hipLaunchKernelGGL(ppo_loss_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), a);
+  int blocks = (int)((a.rows + LOSS_TPB - 1) / LOSS_TPB);
+  hipLaunchKernelGGL(ppo_loss_kernel, dim3(blocks), dim3(LOSS_TPB), 0, LGX_STREAM(stream), a);
   hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
   return lgx_hip_status("lgx_ppo_loss");
 }

@@ -9,7 +9,7 @@ if [[ $STEP == all || $STEP == tests ]]; then
   tail -3 gpurun_out/gpu_tests.log
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
-  timeout -k 10 900 python bench.py --steps ${BENCH_STEPS:-5} --warmup ${BENCH_WARMUP:-2} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed rc=$?"; tail -30 gpurun_out/bench.err; exit 1; }
+  timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed rc=$?"; tail -30 gpurun_out/bench.err; exit 1; }
   cat gpurun_out/bench.json
 fi
 if [[ $STEP == all || $STEP == prof ]]; then
