@@ -84,9 +84,29 @@ LGX_DEV f3 quat_apply(float qx, float qy, float qz, float qw, f3 v) {
 LGX_DEV float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 
 // quad (4-lane) all-reduce: lanes 4e..4e+3 own one env
+// Cross-lane moves on the DPP path (a VALU modifier) instead of ds_bpermute (the LDS crossbar):
+// dpp_mov<CTRL> returns the value of the lane selected by the DPP control word.
+template <int CTRL>
+LGX_DEV float dpp_mov(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, v), __builtin_bit_cast(int, v),
+                                                              CTRL, 0xF, 0xF, false));
+}
+LGX_DEV float lane_xor1(float v) { return dpp_mov<0xB1>(v); }   // quad_perm [1,0,3,2]
+LGX_DEV float lane_xor2(float v) { return dpp_mov<0x4E>(v); }   // quad_perm [2,3,0,1]
+// xor 4 / xor 8 inside a 16-lane row: row_shl:n (from lane + n) or row_shr:n (from lane - n)
+LGX_DEV float lane_xor4(float v) {
+  const float up = dpp_mov<0x104>(v), dn = dpp_mov<0x114>(v);
+  return (threadIdx.x & 4) ? dn : up;
+}
+LGX_DEV float lane_xor8(float v) {
+  const float up = dpp_mov<0x108>(v), dn = dpp_mov<0x118>(v);
+  return (threadIdx.x & 8) ? dn : up;
+}
+
+// sum over the 4 lanes of a quad; every lane gets the bitwise-identical ((a+b)+(c+d)) order
 LGX_DEV float quad_sum(float v) {
-  v += __shfl_xor(v, 1);
-  v += __shfl_xor(v, 2);
+  v += lane_xor1(v);
+  v += lane_xor2(v);
   return v;
 }
 

@@ -234,8 +234,8 @@ LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon,
 // sum over the PP lanes that share a leg (lane bits 2..): contact terms were split across them
 template <int PP>
 LGX_DEV float psum(float v) {
-  if (PP >= 2) v += __shfl_xor(v, 4);
-  if (PP >= 4) v += __shfl_xor(v, 8);
+  if (PP >= 2) v += lane_xor4(v);
+  if (PP >= 4) v += lane_xor8(v);
   if (PP >= 8) v += __shfl_xor(v, 16);
   return v;
 }
