@@ -336,3 +336,28 @@ def test_explicit_torque_control_matches_oracle(gpu, ctrl):
     assert ok, f"dof max err {e}"
     ok, e = close(dev.obs_buf, ora.obs_buf, 5e-3, 5e-3)
     assert ok, f"obs max err {e}"
+
+
+@pytest.mark.parametrize("task", ["a1", "a1_src", "aliengo", "anymal_b"])
+def test_other_robots_step_matches_oracle(gpu, task):
+    """The remaining registered quadrupeds (model JSONs from their URDFs): one full env step
+    from a randomised state, HIP path vs oracle."""
+    ora = make_env(task, num_envs=64, device="cpu", backend="oracle")
+    dev = make_env(task, num_envs=64, device="cuda:0", backend="lgx")
+    gen = torch.Generator().manual_seed(21)
+    randomize_state(ora, gen)
+    sync(ora, dev)
+    dev.terrain_types.copy_(ora.terrain_types)
+    ora.common_step_counter = dev.common_step_counter = 5
+    a = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+    ora.step(a)
+    dev.step(a.cuda())
+    torch.cuda.synchronize()
+    assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf)
+    keep = ~ora.reset_buf
+    ok, e = close(dev.root_states.cpu()[keep], ora.root_states[keep], 2e-3, 2e-3)
+    assert ok, f"root max err {e}"
+    ok, e = close(dev.obs_buf.cpu()[keep], ora.obs_buf[keep], 5e-3, 5e-3)
+    assert ok, f"obs max err {e}"
+    ok, e = close(dev.rew_buf.cpu()[keep], ora.rew_buf[keep], 1e-4, 1e-3)
+    assert ok, f"rew max err {e}"
