@@ -123,7 +123,8 @@ def main():
     runner.learn(args.warmup)
     gc.collect()
     gc.disable()   # no collector pauses inside the timed region (host-side Python only)
-    lib.lgx_profile_enable(handle, 1)
+    timing_period = int(os.environ.get("LGX_BENCH_KERNEL_TIMING", "1"))   # time every k-th env step (0: off)
+    lib.lgx_profile_enable(handle, timing_period)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

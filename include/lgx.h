@@ -218,10 +218,22 @@ int lgx_sim_destroy(lgx_sim* sim);
  * `common_step_counter` is the host counter value AFTER this step's increment. */
 int lgx_step(lgx_sim* sim, int64_t common_step_counter, void* stream);
 
+/* lgx_step with the policy's raw actions read from `actions` (device float[N,12], row-major)
+ * instead of the bound actions buffer; the clipped actions are still written to the bound
+ * buffer (self.actions = clip(actions), legged_robot.py:85-86) -- no host-side copy. */
+int lgx_step_from(lgx_sim* sim, const float* actions, int64_t common_step_counter, void* stream);
+
 /* Re-point the observation output (device float[N, num_obs]) for the next calls.  The reference
  * rebinds obs_buf every step (`self.obs_buf = torch.cat(...)`, legged_robot.py:218), so rsl_rl
  * keeps the previous step's tensor alive across env.step(); callers double-buffer with this. */
 int lgx_rebind_obs(lgx_sim* sim, float* obs);
+
+/* Per-call copy of the episode extras (device float[T + 2], lgx_buffers.extras layout) written by
+ * the next lgx_step / lgx_post_physics / lgx_reset_idx, stale values included.  The reference
+ * publishes fresh tensors in extras["episode"] (legged_robot.py:182-189) that consumers keep
+ * (rsl_rl's ep_infos); binding a fresh snapshot per call gives the same semantics without a
+ * separate copy.  NULL disables the copy. */
+int lgx_rebind_extras(lgx_sim* sim, float* snapshot);
 
 /* Physics only: `n` substeps with the currently bound dof_targets (gym.simulate x n). */
 int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
@@ -271,12 +283,13 @@ typedef struct lgx_mlp_desc {
 } lgx_mlp_desc;
 int lgx_mlp_forward_batch(const lgx_mlp_desc* descs, int32_t count, void* stream);
 
-/* In-library kernel timing for the measurement harness (bench.py): when enabled, every
- * lgx_step records hipEvents on the launch stream around each kernel class
- * (0 physics, 1 actuator MLP, 2 post-physics incl. extras finalize).  lgx_profile_collect
- * synchronises those events (call it OUTSIDE timed regions), writes per class the summed
- * milliseconds and launch count to ms[3] / count[3], and clears the record. */
-int lgx_profile_enable(lgx_sim* sim, int32_t on);
+/* In-library kernel timing for the measurement harness (bench.py): with `period` = k > 0, every
+ * k-th lgx_step dispatches its kernels through hipExtLaunchKernelGGL with a (start, stop)
+ * hipEvent pair per kernel class (0 physics, 1 actuator MLP, 2 post-physics kernel); 0 turns
+ * timing off.  lgx_profile_collect synchronises those events (call it OUTSIDE timed regions),
+ * writes per class the summed milliseconds and launch count to ms[3] / count[3], and clears
+ * the record. */
+int lgx_profile_enable(lgx_sim* sim, int32_t period);
 int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
 
 /* Generalised advantage estimation (rsl_rl RolloutStorage.compute_returns, before the

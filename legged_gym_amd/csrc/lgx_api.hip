@@ -38,8 +38,10 @@ struct lgx_sim {
   lgx_dev_model* d_model;
   lgx_env_params* d_params;
   const float* draws;
+  float* extras_snapshot;  // lgx_rebind_extras (NULL: no per-call copy)
   int32_t n_term_rows;
-  bool profiling;
+  int32_t profiling;     // 0 = off, k = time every k-th lgx_step
+  int64_t prof_calls;
   std::vector<hipEvent_t> ev[3];  // (start, stop) pairs per kernel class
   std::vector<hipEvent_t> pool;
 };
@@ -47,15 +49,21 @@ struct lgx_sim {
 static hipEvent_t take_event(lgx_sim* s) {
   if (!s->pool.empty()) { hipEvent_t e = s->pool.back(); s->pool.pop_back(); return e; }
   hipEvent_t e = nullptr;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  // no system-scope fences: the timestamps are only read back through hipEventElapsedTime
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
   return e;
 }
-static void mark(lgx_sim* s, int cls, hipStream_t st) {
-  if (!s->profiling) return;
-  hipEvent_t e = take_event(s);
-  if (!e) return;
-  (void)hipEventRecord(e, st);
-  s->ev[cls].push_back(e);
+thread_local lgx_timing_slot lgx_timing;
+
+// arm the kernel-tight event pair for the next launch of kernel class `cls` (see LGX_LAUNCH)
+static void arm(lgx_sim* s, int cls, bool sample) {
+  lgx_timing = lgx_timing_slot{};
+  if (!sample) return;
+  hipEvent_t e0 = take_event(s), e1 = take_event(s);
+  if (!e0 || !e1) return;
+  s->ev[cls].push_back(e0);
+  s->ev[cls].push_back(e1);
+  lgx_timing = lgx_timing_slot{e0, e1};
 }
 
 extern "C" {
@@ -141,7 +149,9 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   s->params = *params;
   s->bufs = *bufs;
   s->draws = nullptr;
-  s->profiling = false;
+  s->extras_snapshot = nullptr;
+  s->profiling = 0;
+  s->prof_calls = 0;
   s->n_term_rows = params->num_terms + (params->termination_slot >= 0 ? 1 : 0);
   if ((rc = hip_check(hipMalloc(&s->d_model, sizeof(lgx_dev_model)), "hipMalloc(model)"))) { delete s; return rc; }
   if ((rc = hip_check(hipMalloc(&s->d_params, sizeof(lgx_env_params)), "hipMalloc(params)"))) {
@@ -176,48 +186,59 @@ int lgx_rebind_obs(lgx_sim* s, float* obs) {
   return 0;
 }
 
+int lgx_rebind_extras(lgx_sim* s, float* snapshot) {
+  if (!s) return fail(LGX_EINVAL, "lgx_rebind_extras: null sim");
+  s->extras_snapshot = snapshot;
+  return 0;
+}
+
 int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
   if (!s || n < 0) return fail(LGX_EINVAL, "lgx_simulate: bad arguments");
   if (n == 0) return 0;
-  return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, n, 0, (hipStream_t)stream),
+  return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, n, 0, nullptr,
+                                         (hipStream_t)stream),
                       "lgx_simulate: physics launch");
 }
 
 int lgx_post_physics(lgx_sim* s, int64_t step, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_post_physics: null sim");
   return launch_check(lgx_launch_post_physics(s->d_params, s->bufs, s->params.num_envs, s->params.num_obs, s->n_term_rows,
-                                              s->params.measure_heights, step, s->draws, (hipStream_t)stream),
+                                              s->params.measure_heights, step, s->draws, s->extras_snapshot,
+                                              (hipStream_t)stream),
                       "lgx_post_physics: launch");
 }
 
-int lgx_step(lgx_sim* s, int64_t step, void* stream) {
+int lgx_step(lgx_sim* s, int64_t step, void* stream) { return lgx_step_from(s, nullptr, step, stream); }
+
+int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_step: null sim");
   hipStream_t st = (hipStream_t)stream;
   const lgx_env_params& p = s->params;
-  // action clipping is fused into the physics kernel's action load
-  mark(s, 0, st);
-  int rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, st),
+  const bool sample = s->profiling > 0 && (s->prof_calls++ % s->profiling) == 0;
+  // action clipping is fused into the physics kernel's action load (raw actions from `actions`
+  // or, when NULL, from the bound actions buffer; the clipped copy lands in the bound buffer)
+  arm(s, 0, sample);
+  int rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, actions, st),
                     "lgx_step: physics launch");
-  mark(s, 0, st);
   if (rc) return rc;
   if (p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel) {
     // UniNet on every (substep, env, leg) row of this step's model_ins; result = dVel
-    mark(s, 1, st);
+    arm(s, 1, sample);
     rc = launch_check(lgx_launch_actuator_mlp(s->bufs.model_ins, s->bufs.act_dvel, (int64_t)p.decimation * p.num_envs * 4,
                                               s->bufs.act_net_w, s->bufs.act_net_scale, st),
                       "lgx_step: actuator mlp launch");
-    mark(s, 1, st);
     if (rc) return rc;
   }
-  mark(s, 2, st);
+  arm(s, 2, sample);
   rc = lgx_post_physics(s, step, stream);
-  mark(s, 2, st);
+  lgx_timing = lgx_timing_slot{};
   return rc;
 }
 
 int lgx_profile_enable(lgx_sim* s, int32_t on) {
   if (!s) return fail(LGX_EINVAL, "lgx_profile_enable: null sim");
-  s->profiling = on != 0;
+  s->profiling = on > 0 ? on : 0;
+  s->prof_calls = 0;
   return 0;
 }
 
@@ -248,7 +269,7 @@ int lgx_reset_idx(lgx_sim* s, const int32_t* env_ids, int32_t n, int64_t step, i
   if (!s || n < 0 || (n > 0 && !env_ids)) return fail(LGX_EINVAL, "lgx_reset_idx: bad arguments");
   if (n > s->params.num_envs) return fail(LGX_EINVAL, "lgx_reset_idx: more ids than envs");
   return launch_check(lgx_launch_reset_idx(s->d_params, s->bufs, s->params.num_envs, s->n_term_rows, env_ids, n, step,
-                                           init_done, s->draws, (hipStream_t)stream),
+                                           init_done, s->draws, s->extras_snapshot, (hipStream_t)stream),
                       "lgx_reset_idx: launch");
 }
 

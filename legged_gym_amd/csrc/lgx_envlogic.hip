@@ -397,7 +397,8 @@ lgx_reset_idx_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, const 
 // extras finalize: deterministic sum of block partials; publish only if >= 1 env reset.
 // level_scan: sum terrain levels over all envs here (reset_idx path) instead of partials.
 __global__ void __launch_bounds__(256)
-lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks, int32_t level_scan) {
+lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks, int32_t level_scan,
+                           float* __restrict__ snapshot) {
   const int N = P->num_envs;
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
   __shared__ float sums[LGX_PARTIAL_STRIDE];
@@ -418,35 +419,41 @@ lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, 
     if (lane == 0) sums[r] = s;
   }
   __syncthreads();
-  float count = sums[T];
-  if (count <= 0.f) return;  // reference keeps stale extras (legged_robot.py:160-161)
-  if (t < T) B.extras[t] = (sums[t] / count) / P->max_episode_length_s;
-  if (t == 0) {
-    if (P->curriculum) B.extras[T] = sums[T + 1] / (float)N;
-    B.extras[T + 1] = count;
+  const float count = sums[T];
+  const bool update = count > 0.f;  // else the reference keeps stale extras (legged_robot.py:160-161)
+  if (t < rows) {
+    float v = B.extras[t];
+    if (update) {
+      if (t < T) v = (sums[t] / count) / P->max_episode_length_s;
+      else if (t == T + 1) v = count;
+      else if (P->curriculum) v = sums[T + 1] / (float)N;
+      B.extras[t] = v;
+    }
+    if (snapshot) snapshot[t] = v;  // this step's published copy (lgx_rebind_extras)
   }
+  if (!update) return;
   if (P->send_timeouts)
     for (int e = t; e < N; e += 256) B.extras_time_outs[e] = B.time_out[e];
 }
 
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
                             int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
-                            hipStream_t stream) {
+                            float* extras_snapshot, hipStream_t stream) {
   (void)num_obs; (void)n_term_rows; (void)measure_heights;
   int blocks = (n_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
-  hipLaunchKernelGGL(lgx_post_physics_kernel, dim3(blocks), dim3(ENV_THREADS), 0, stream, dp, b, step, draws);
-  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 0);
+  LGX_LAUNCH(lgx_post_physics_kernel, dim3(blocks), dim3(ENV_THREADS), 0, stream, dp, b, step, draws);
+  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 0, extras_snapshot);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
                          const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
-                         hipStream_t stream) {
+                         float* extras_snapshot, hipStream_t stream) {
   (void)n_envs; (void)n_term_rows;
   if (n <= 0) return 0;
   int blocks = (n + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
   hipLaunchKernelGGL(lgx_reset_idx_kernel, dim3(blocks), dim3(LGX_ENV_BLOCK), 0, stream, dp, b, ids, n, step,
                      init_done, draws);
-  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 1);
+  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 1, extras_snapshot);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

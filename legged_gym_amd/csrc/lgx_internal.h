@@ -1,5 +1,6 @@
 // Internal (non-ABI) declarations shared by the lgx HIP translation units.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "../../include/lgx.h"
@@ -16,13 +17,13 @@ struct lgx_dev_model {
 };
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
-                       int32_t nsub, int32_t from_actions, hipStream_t stream);
+                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream);
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
                             int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
-                            hipStream_t stream);
+                            float* extras_snapshot, hipStream_t stream);
 int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
                          const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
-                         hipStream_t stream);
+                         float* extras_snapshot, hipStream_t stream);
 int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
                             hipStream_t stream);
 int lgx_launch_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m, const float* w,
@@ -33,6 +34,22 @@ int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, c
 int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t stream);
 int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream);
+
+// Kernel-tight timing for lgx_profile_*: when the caller arms a (start, stop) event pair, the
+// next LGX_LAUNCH on this thread is dispatched with hipExtLaunchKernelGGL, which records the
+// events on the kernel's own dispatch (no host launch latency inside the interval).
+struct lgx_timing_slot { hipEvent_t start = nullptr, stop = nullptr; };
+extern thread_local lgx_timing_slot lgx_timing;
+#define LGX_LAUNCH(kern, grid, block, shmem, stream, ...)                                          \
+  do {                                                                                           \
+    if (lgx_timing.start) {                                                                      \
+      hipExtLaunchKernelGGL(kern, grid, block, shmem, stream, lgx_timing.start, lgx_timing.stop, 0, \
+                            __VA_ARGS__);                                                        \
+      lgx_timing = lgx_timing_slot{};                                                            \
+    } else {                                                                                     \
+      hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                         \
+    }                                                                                            \
+  } while (0)
 
 // error reporting shared by the translation units (thread-local message, lgx_last_error)
 int lgx_fail(int code, const char* msg);

@@ -231,11 +231,11 @@ static int launch_batch(const MlpBatch& b, int count, hipStream_t stream) {
   int64_t grid = tiles < 2048 ? tiles : 2048;
   dim3 g((unsigned)grid, (unsigned)count);
   if (narrow)
-    hipLaunchKernelGGL((lgx_mlp_forward_kernel<2, 264, 2>), g, dim3(MLP_THREADS), 0, stream, b);
+    LGX_LAUNCH((lgx_mlp_forward_kernel<2, 264, 2>), g, dim3(MLP_THREADS), 0, stream, b);
   else if (actw <= 776)
-    hipLaunchKernelGGL((lgx_mlp_forward_kernel<1, 776, 8>), g, dim3(MLP_THREADS), 0, stream, b);
+    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 776, 8>), g, dim3(MLP_THREADS), 0, stream, b);
   else
-    hipLaunchKernelGGL((lgx_mlp_forward_kernel<1, 1032, 8>), g, dim3(MLP_THREADS), 0, stream, b);
+    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 1032, 8>), g, dim3(MLP_THREADS), 0, stream, b);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -411,7 +411,7 @@ int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const flo
     WsArgs wa{in, out, rows, w, out_scale};
     const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
     const int grid = (int)std::min<int64_t>(tiles, 512);  // 2 persistent workgroups per CU
-    hipLaunchKernelGGL(lgx_actuator_ws_kernel, dim3(grid), dim3(256), 0, stream, wa);
+    LGX_LAUNCH(lgx_actuator_ws_kernel, dim3(grid), dim3(256), 0, stream, wa);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }
   MlpBatch b{};

@@ -248,7 +248,7 @@ LGX_DEV float psum(float v) {
 template <int PP>
 __global__ void __launch_bounds__(64 * PP, LGX_PHYS_WAVES_PER_SIMD)
 lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* __restrict__ P, lgx_buffers B,
-                   int32_t nsub, int32_t from_actions) {
+                   int32_t nsub, int32_t from_actions, const float* __restrict__ act_src) {
   constexpr int PHYS_BLOCK = 64 * PP;               // 16 envs per workgroup
   constexpr int LPE = 4 * PP;                       // lanes per env
   constexpr int SLOTS = (MAX_LANE_PTS + PP - 1) / PP;
@@ -309,7 +309,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   float* ecom = env_com[eb];
   const bool use_hist = from_actions && P->use_actuator_history;
   if (from_actions) {  // clip (legged_robot.py:85-86) fused into the load
-    const float* a = B.actions + (int64_t)ec * 12 + leg * 3;
+    const float* a = act_src + (int64_t)ec * 12 + leg * 3;  // raw actions (B.actions or lgx_step_from's input)
 #pragma unroll
     for (int k = 0; k < 3; ++k) act[k] = clampf(a[k], -P->clip_actions, P->clip_actions);
   }
@@ -708,20 +708,21 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 }
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
-                       int32_t nsub, int32_t from_actions, hipStream_t stream) {
+                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream) {
+  if (!act_src) act_src = b.actions;
   // lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches
   const int pp = n_envs >= 16384 ? 1 : (n_envs >= 8192 ? 2 : 4);
   const char* force = getenv("LGX_PHYS_PP");  // A/B switch for measurements
   const int ppx = force ? atoi(force) : pp;
   const int blocks = (n_envs + 15) / 16;       // 16 envs per workgroup of 64*PP lanes
   if (ppx == 8)
-    hipLaunchKernelGGL(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions);
+    LGX_LAUNCH(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions, act_src);
   else if (ppx == 4)
-    hipLaunchKernelGGL(lgx_physics_kernel<4>, dim3(blocks), dim3(256), 0, stream, dm, dp, b, nsub, from_actions);
+    LGX_LAUNCH(lgx_physics_kernel<4>, dim3(blocks), dim3(256), 0, stream, dm, dp, b, nsub, from_actions, act_src);
   else if (ppx == 2)
-    hipLaunchKernelGGL(lgx_physics_kernel<2>, dim3(blocks), dim3(128), 0, stream, dm, dp, b, nsub, from_actions);
+    LGX_LAUNCH(lgx_physics_kernel<2>, dim3(blocks), dim3(128), 0, stream, dm, dp, b, nsub, from_actions, act_src);
   else
-    hipLaunchKernelGGL(lgx_physics_kernel<1>, dim3(blocks), dim3(64), 0, stream, dm, dp, b, nsub, from_actions);
+    LGX_LAUNCH(lgx_physics_kernel<1>, dim3(blocks), dim3(64), 0, stream, dm, dp, b, nsub, from_actions, act_src);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -34,6 +34,7 @@ def _ptr(t, ctype=abi.PF):
 
 class LgxBackend:
     """Thin owner of one `lgx_sim` (product path: HIP only, no fallback)."""
+    takes_actions = True   # step(counter, actions) reads the policy's tensor directly (lgx_step_from)
 
     def __init__(self, env, model, params, bufs):
         from legged_gym_amd.sim import lib as lgxlib
@@ -50,8 +51,12 @@ class LgxBackend:
     def stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def step(self, counter):
-        self._check(self.lib.lgx_step(self.handle, counter, self.stream()), "lgx_step")
+    def step(self, counter, actions=None):
+        if actions is None:
+            self._check(self.lib.lgx_step(self.handle, counter, self.stream()), "lgx_step")
+        else:
+            self._check(self.lib.lgx_step_from(self.handle, C.c_void_p(actions.data_ptr()), counter, self.stream()),
+                        "lgx_step_from")
 
     def simulate(self, n):
         self._check(self.lib.lgx_simulate(self.handle, n, self.stream()), "lgx_simulate")
@@ -65,6 +70,9 @@ class LgxBackend:
 
     def rebind_obs(self, obs):
         self._check(self.lib.lgx_rebind_obs(self.handle, C.c_void_p(obs.data_ptr())), "lgx_rebind_obs")
+
+    def rebind_extras(self, snapshot):
+        self._check(self.lib.lgx_rebind_extras(self.handle, C.c_void_p(snapshot.data_ptr())), "lgx_rebind_extras")
 
     def set_draws(self, draws):
         self._check(self.lib.lgx_set_draws(self.handle, C.c_void_p(draws.data_ptr()) if draws is not None else None),
@@ -99,19 +107,24 @@ class LeggedRobot(BaseTask):
     # ------------------------------------------------------------------ step path
     def step(self, actions):
         """legged_robot.py:79-107 as one C-ABI call (lgx_step)."""
-        self.actions.copy_(actions)            # clipped in place by the kernel (:85-86)
         self._next_obs_buffer()
+        snap = self._next_extras_snapshot()
         self.common_step_counter += 1
-        self._backend.step(self.common_step_counter)
-        self._publish_extras()
+        if self._direct_actions(actions):      # kernel reads the policy's tensor, clips into self.actions
+            self._backend.step(self.common_step_counter, actions)
+        else:
+            self.actions.copy_(actions)        # clipped in place by the kernel (:85-86)
+            self._backend.step(self.common_step_counter)
+        self._publish_extras(snap)
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 
     def post_physics_step(self):
         """legged_robot.py:109-141 on the current physics state (no physics)."""
         self._next_obs_buffer()
+        snap = self._next_extras_snapshot()
         self.common_step_counter += 1
         self._backend.post_physics(self.common_step_counter)
-        self._publish_extras()
+        self._publish_extras(snap)
 
     def simulate(self, n=1):
         """n physics substeps with the current `target_poses` (gym.simulate x n)."""
@@ -122,8 +135,9 @@ class LeggedRobot(BaseTask):
         if len(env_ids) == 0:
             return
         ids = torch.as_tensor(env_ids, device=self.device).to(torch.int32).contiguous()
+        snap = self._next_extras_snapshot()
         self._backend.reset_idx(ids, self.common_step_counter, self.init_done)
-        self._publish_extras()
+        self._publish_extras(snap)
 
     def _next_obs_buffer(self):
         """Alternate between two observation buffers: the reference returns a fresh obs tensor per
@@ -138,11 +152,27 @@ class LeggedRobot(BaseTask):
     def compute_observations(self):
         raise NotImplementedError("observations are produced inside lgx_step/lgx_post_physics")
 
-    def _publish_extras(self):
+    def _direct_actions(self, actions):
+        return (getattr(self._backend, "takes_actions", False) and isinstance(actions, torch.Tensor)
+                and actions.device == self.actions.device and actions.dtype == torch.float32
+                and actions.shape == self.actions.shape and actions.is_contiguous())
+
+    def _next_extras_snapshot(self):
+        """A fresh [T + 2] tensor the kernels fill with this call's extras (lgx_rebind_extras);
+        None when the backend has no such output (then _publish_extras clones)."""
+        if not hasattr(self._backend, "rebind_extras"):
+            return None
+        snap = torch.empty_like(self._extras_buf)
+        self._backend.rebind_extras(snap)
+        return snap
+
+    def _publish_extras(self, snap=None):
         """extras["episode"] / ["time_outs"] (legged_robot.py:182-193).  The device keeps the
-        reference's stale-until-next-reset semantics; a snapshot is taken per call so that
-        consumers that keep references (rsl_rl ep_infos) see per-step values."""
-        snap = self._extras_buf.clone()
+        reference's stale-until-next-reset semantics; every call publishes its own snapshot
+        (written by the finalize kernel, or cloned) so that consumers that keep references
+        (rsl_rl ep_infos) see per-step values."""
+        if snap is None:
+            snap = self._extras_buf.clone()
         ep = {}
         for key, row in self._extras_rows:
             ep[key] = snap[row]

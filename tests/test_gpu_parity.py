@@ -361,3 +361,29 @@ def test_other_robots_step_matches_oracle(gpu, task):
     assert ok, f"obs max err {e}"
     ok, e = close(dev.rew_buf.cpu()[keep], ora.rew_buf[keep], 1e-4, 1e-3)
     assert ok, f"rew max err {e}"
+
+
+def test_direct_actions_and_extras_snapshots(gpu):
+    """lgx_step_from (policy tensor read in place) == copy-then-lgx_step, the caller's tensor is not
+    clipped in place, and every step publishes its own extras snapshot (kernel-written) that
+    stays valid after later steps, as the reference's fresh tensors do."""
+    a_env = make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
+    b_env = make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
+    a_env.reset()
+    b_env.reset()
+    gen = torch.Generator(device="cuda:0").manual_seed(3)
+    kept, expect = [], []
+    for _ in range(30):
+        act = torch.randn(64, 12, device="cuda:0", generator=gen) * 150.0   # beyond clip_actions
+        raw = act.clone()
+        assert a_env._direct_actions(act) and not b_env._direct_actions(act.t().contiguous().t())
+        oa, _, ra, da, ia = a_env.step(act)
+        ob, _, rb, db, ib = b_env.step(act.t().contiguous().t())
+        assert torch.equal(act, raw)
+        assert torch.equal(a_env.actions, b_env.actions) and a_env.actions.abs().max() <= 100.0
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
+        kept.append(ia["episode"])
+        expect.append(a_env._extras_buf.clone())
+    for ep, ref in zip(kept, expect):
+        for key, row in a_env._extras_rows:
+            assert torch.equal(ep[key], ref[row]), key
