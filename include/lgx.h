@@ -235,6 +235,12 @@ int lgx_rebind_obs(lgx_sim* sim, float* obs);
  * separate copy.  NULL disables the copy. */
 int lgx_rebind_extras(lgx_sim* sim, float* snapshot);
 
+/* The Go1 actuator net of lgx_step runs on an internal stream (its output, actuator dVel, is
+ * not consumed by the step: go1.py:71-73) and overlaps post-physics and the caller's next
+ * work; the next lgx_step / lgx_simulate orders itself after it.  Make `stream` wait for that
+ * work before reading act_dvel on it. */
+int lgx_sync_aux(lgx_sim* sim, void* stream);
+
 /* Physics only: `n` substeps with the currently bound dof_targets (gym.simulate x n). */
 int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
 
@@ -310,7 +316,7 @@ typedef struct lgx_ppo_act_args {
   int64_t num_envs;
   int32_t num_actions, num_obs, num_cobs, pad;
   const float* mu;              /* [N,A] actor mean (rollout MLP output) */
-  const float* value;           /* [N]   critic value */
+  const float* value;           /* [N]   critic value, or NULL when the critic wrote st_values itself */
   const float* std;             /* [A] */
   const float* noise;           /* [N,A] standard-normal draws */
   const float* obs;             /* [N,num_obs] */

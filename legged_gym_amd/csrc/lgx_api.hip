@@ -39,6 +39,12 @@ struct lgx_sim {
   lgx_env_params* d_params;
   const float* draws;
   float* extras_snapshot;  // lgx_rebind_extras (NULL: no per-call copy)
+  // Go1 actuator net off the critical path: its output (dVel) is not read by the step
+  // (go1.py:71-73), so it runs on an auxiliary stream concurrently with post-physics and the
+  // next policy forward; the next physics launch (which rewrites model_ins) waits for it.
+  hipStream_t aux;
+  hipEvent_t aux_in, aux_done;  // physics done (aux waits) / actuator done (main waits)
+  bool aux_pending;
   int32_t n_term_rows;
   int32_t profiling;     // 0 = off, k = time every k-th lgx_step
   int64_t prof_calls;
@@ -150,6 +156,9 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   s->bufs = *bufs;
   s->draws = nullptr;
   s->extras_snapshot = nullptr;
+  s->aux = nullptr;
+  s->aux_in = s->aux_done = nullptr;
+  s->aux_pending = false;
   s->profiling = 0;
   s->prof_calls = 0;
   s->n_term_rows = params->num_terms + (params->termination_slot >= 0 ? 1 : 0);
@@ -166,6 +175,12 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
 
 int lgx_sim_destroy(lgx_sim* s) {
   if (!s) return 0;
+  if (s->aux) {
+    (void)hipStreamSynchronize(s->aux);
+    (void)hipStreamDestroy(s->aux);
+    (void)hipEventDestroy(s->aux_in);
+    (void)hipEventDestroy(s->aux_done);
+  }
   for (auto& v : s->ev) for (hipEvent_t e : v) (void)hipEventDestroy(e);
   for (hipEvent_t e : s->pool) (void)hipEventDestroy(e);
   (void)hipFree(s->d_model);
@@ -192,9 +207,26 @@ int lgx_rebind_extras(lgx_sim* s, float* snapshot) {
   return 0;
 }
 
+// make `st` wait for the outstanding auxiliary-stream work (the actuator net of the last step)
+static int join_aux(lgx_sim* s, hipStream_t st) {
+  if (!s->aux_pending) return 0;
+  return hip_check(hipStreamWaitEvent(st, s->aux_done, 0), "hipStreamWaitEvent(aux)");
+}
+
+static int aux_enabled() {
+  const char* e = getenv("LGX_ACT_OVERLAP");  // A/B switch: 0 = actuator net on the caller's stream
+  return e ? atoi(e) : 1;
+}
+
+int lgx_sync_aux(lgx_sim* s, void* stream) {
+  if (!s) return fail(LGX_EINVAL, "lgx_sync_aux: null sim");
+  return join_aux(s, (hipStream_t)stream);
+}
+
 int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
   if (!s || n < 0) return fail(LGX_EINVAL, "lgx_simulate: bad arguments");
   if (n == 0) return 0;
+  if (int rc = join_aux(s, (hipStream_t)stream)) return rc;
   return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, n, 0, nullptr,
                                          (hipStream_t)stream),
                       "lgx_simulate: physics launch");
@@ -217,17 +249,37 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
   const bool sample = s->profiling > 0 && (s->prof_calls++ % s->profiling) == 0;
   // action clipping is fused into the physics kernel's action load (raw actions from `actions`
   // or, when NULL, from the bound actions buffer; the clipped copy lands in the bound buffer)
+  int rc = join_aux(s, st);  // the last actuator net still reads model_ins
+  if (rc) return rc;
   arm(s, 0, sample);
-  int rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, actions, st),
+  rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, actions, st),
                     "lgx_step: physics launch");
   if (rc) return rc;
   if (p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel) {
     // UniNet on every (substep, env, leg) row of this step's model_ins; result = dVel
+    hipStream_t ast = st;
+    if (aux_enabled()) {
+      if (!s->aux) {
+        rc = hip_check(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking), "hipStreamCreate(aux)");
+        if (!rc) rc = hip_check(hipEventCreateWithFlags(&s->aux_in, hipEventDisableTiming), "hipEventCreate(aux)");
+        if (!rc) rc = hip_check(hipEventCreateWithFlags(&s->aux_done, hipEventDisableTiming), "hipEventCreate(aux)");
+        if (rc) return rc;
+      }
+      rc = hip_check(hipEventRecord(s->aux_in, st), "hipEventRecord(aux_in)");
+      if (!rc) rc = hip_check(hipStreamWaitEvent(s->aux, s->aux_in, 0), "hipStreamWaitEvent(aux_in)");
+      if (rc) return rc;
+      ast = s->aux;
+    }
     arm(s, 1, sample);
     rc = launch_check(lgx_launch_actuator_mlp(s->bufs.model_ins, s->bufs.act_dvel, (int64_t)p.decimation * p.num_envs * 4,
-                                              s->bufs.act_net_w, s->bufs.act_net_scale, st),
+                                              s->bufs.act_net_w, s->bufs.act_net_scale, ast, ast != st ? 1 : 2),
                       "lgx_step: actuator mlp launch");
     if (rc) return rc;
+    if (ast != st) {
+      rc = hip_check(hipEventRecord(s->aux_done, ast), "hipEventRecord(aux_done)");
+      if (rc) return rc;
+      s->aux_pending = true;
+    }
   }
   arm(s, 2, sample);
   rc = lgx_post_physics(s, step, stream);

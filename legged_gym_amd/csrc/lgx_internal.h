@@ -24,8 +24,10 @@ int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int3
 int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
                          const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
                          float* extras_snapshot, hipStream_t stream);
+// wg_per_cu: persistent workgroups per CU of the weight-stationary kernel (2 when it owns the
+// chip, 1 when it shares the CUs with concurrent work on another stream)
 int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
-                            hipStream_t stream);
+                            hipStream_t stream, int wg_per_cu = 2);
 int lgx_launch_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m, const float* w,
                              hipStream_t stream);
 int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, const int32_t* dims,

@@ -28,6 +28,11 @@
 #define MLP_THREADS 256
 #define MLP_MAX_W 512
 #define MLP_MAX_LAYERS 6
+// <= 128 registers per lane: a policy-MLP workgroup fits beside a physics workgroup (376
+// registers, 85 KB LDS) on the same CU, so the rollout critic forward overlaps physics
+#ifndef LGX_MLP_MAX_VGPR
+#define LGX_MLP_MAX_VGPR 128
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -104,7 +109,7 @@ LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* 
 }
 
 template <int RS, int ACTW, int MAXT>
-__global__ void __launch_bounds__(MLP_THREADS)
+__global__ void __launch_bounds__(MLP_THREADS) __attribute__((amdgpu_num_vgpr(LGX_MLP_MAX_VGPR)))
 lgx_mlp_forward_kernel(MlpBatch batch) {
   constexpr int BM = 16 * RS;
   __shared__ float act_lds[BM * ACTW];
@@ -405,12 +410,14 @@ static int actuator_ws_enabled() {
 
 // packed actuator weights: W0t[30x128] b0 W1t[128x128] b1 W2t[128x128] b2 W3t[128x3] b3 (see lgx.h)
 int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
-                            hipStream_t stream) {
+                            hipStream_t stream, int wg_per_cu) {
   if (rows <= 0) return 0;
   if (actuator_ws_enabled()) {
     WsArgs wa{in, out, rows, w, out_scale};
     const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
-    const int grid = (int)std::min<int64_t>(tiles, 512);  // 2 persistent workgroups per CU
+    const char* e = getenv("LGX_ACT_WS_PER_CU");  // persistent workgroups per CU (A/B switch)
+    const int per_cu = e ? std::max(1, atoi(e)) : std::max(1, wg_per_cu);
+    const int grid = (int)std::min<int64_t>(tiles, 256 * per_cu);
     LGX_LAUNCH(lgx_actuator_ws_kernel, dim3(grid), dim3(256), 0, stream, wa);
     return hipGetLastError() == hipSuccess ? 0 : -2;
   }

@@ -91,7 +91,7 @@ ppo_act_kernel(lgx_ppo_act_args a) {
       logp += -(d * d) / (2.f * sd * sd) - logf(sd) - half_log_2pi;
     }
     a.st_logp[n] = logp;
-    a.st_values[n] = a.value[n];
+    if (a.value) a.st_values[n] = a.value[n];
   }
 }
 
@@ -480,8 +480,8 @@ extern "C" int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* 
 extern "C" int lgx_ppo_act(const lgx_ppo_act_args* args, void* stream) {
   if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_act: null args");
   const lgx_ppo_act_args& a = *args;
-  if (a.num_envs <= 0 || a.num_actions <= 0 || a.num_obs <= 0 || !a.mu || !a.value || !a.std || !a.noise || !a.obs ||
-      !a.actions_out || !a.st_obs || !a.st_actions || !a.st_values || !a.st_logp || !a.st_mu || !a.st_sigma ||
+  if (a.num_envs <= 0 || a.num_actions <= 0 || a.num_obs <= 0 || !a.mu || !a.std || !a.noise || !a.obs ||
+      !a.actions_out || !a.st_obs || !a.st_actions || (a.value && !a.st_values) || !a.st_logp || !a.st_mu || !a.st_sigma ||
       ((a.cobs != nullptr) != (a.st_cobs != nullptr)))
     return lgx_fail(LGX_EINVAL, "lgx_ppo_act: bad args");
   hipLaunchKernelGGL(ppo_act_kernel, dim3((unsigned)((a.num_envs + ACT_ENVS - 1) / ACT_ENVS)), dim3(TPB), 0,

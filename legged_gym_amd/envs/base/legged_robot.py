@@ -71,6 +71,9 @@ class LgxBackend:
     def rebind_obs(self, obs):
         self._check(self.lib.lgx_rebind_obs(self.handle, C.c_void_p(obs.data_ptr())), "lgx_rebind_obs")
 
+    def sync_aux(self):
+        self._check(self.lib.lgx_sync_aux(self.handle, self.stream()), "lgx_sync_aux")
+
     def rebind_extras(self, snapshot):
         self._check(self.lib.lgx_rebind_extras(self.handle, C.c_void_p(snapshot.data_ptr())), "lgx_rebind_extras")
 

@@ -48,14 +48,24 @@ class Go1(LeggedRobot):
         # history [N, 12 joints, (pos_err, vel), 5] never reset (go1.py:56-57,65-66)
         self.actuator_history = torch.zeros(N, 12 * 2 * LEN_HIST, device=dev)
         self._model_ins_all = torch.zeros(dec, N, MODEL_IN_SIZE * LEG_NUM, device=dev)
-        self.actuator_dvel = torch.zeros(dec, N, 12, device=dev)
+        self._actuator_dvel = torch.zeros(dec, N, 12, device=dev)
         self.actuator_net_weights = torch.tensor(pack_uninet_weights(net), device=dev)
         self.actuator_net_scale = torch.tensor(np.asarray(net["vel_std"], np.float32), device=dev)
         b.act_hist = _ptr(self.actuator_history)
         b.model_ins = _ptr(self._model_ins_all)
         b.act_net_w = _ptr(self.actuator_net_weights)
         b.act_net_scale = _ptr(self.actuator_net_scale)
-        b.act_dvel = _ptr(self.actuator_dvel)
+        b.act_dvel = _ptr(self._actuator_dvel)
+
+    @property
+    def actuator_dvel(self):
+        """go1.py:100-105 dVel of every substep, [decimation, N, 12].  The product path computes it
+        on lgx's auxiliary stream (nothing in the step consumes it); reading it here orders the
+        caller's current stream after that work."""
+        backend = getattr(self, "_backend", None)
+        if backend is not None and hasattr(backend, "sync_aux"):
+            backend.sync_aux()
+        return self._actuator_dvel
 
     @property
     def model_ins(self):

@@ -1,8 +1,8 @@
 """Rollout policy forward at N=4096 (actor+critic 235->512->256->128->{12,1}): the fused
-lgx_mlp_forward_kernel vs the library path (batched GEMMs + lgx_bias_act) the PPO update uses."""
+lgx_mlp_forward_kernel vs per-layer library GEMMs (+ELU) for one net and for both."""
 import torch
 
-from legged_gym_amd.rl.actor_critic import ActorCritic
+from legged_gym_amd.rl.actor_critic import ActorCritic, run_fused
 
 
 def t(fn, it=50):
@@ -23,25 +23,25 @@ N = 4096
 ac = ActorCritic(235, 235, 12, actor_hidden_dims=[512, 256, 128], critic_hidden_dims=[512, 256, 128]).to(dev)
 obs = torch.randn(N, 235, device=dev)
 with torch.inference_mode():
-    print("fused kernel us", t(lambda: ac.rollout_forward(obs, obs)))
-    W1 = torch.cat([ac.actor[0].weight, ac.critic[0].weight]).t().contiguous()      # [235, 1024]
-    W2 = torch.stack([ac.actor[2].weight.t(), ac.critic[2].weight.t()]).contiguous()  # [2,512,256]
-    W3 = torch.stack([ac.actor[4].weight.t(), ac.critic[4].weight.t()]).contiguous()
-    b1 = torch.cat([ac.actor[0].bias, ac.critic[0].bias])
-    h1 = torch.empty(N, 1024, device=dev)
-    h2 = torch.empty(2, N, 256, device=dev)
-    h3 = torch.empty(2, N, 128, device=dev)
+    print("fused kernel actor+critic us", t(lambda: ac.rollout_forward(obs, obs)))
+    print("fused kernel actor us", t(lambda: run_fused([(ac._fused_actor, obs)])))
+    lin = [m for m in ac.actor if isinstance(m, torch.nn.Linear)]
+    Wt = [l.weight.t().contiguous() for l in lin]
+    bs = [l.bias for l in lin]
+    hs = [torch.empty(N, l.out_features, device=dev) for l in lin]
 
     def lib():
-        torch.addmm(b1, obs, W1, out=h1)
-        torch.nn.functional.elu(h1, inplace=True)
-        x = h1.view(N, 2, 512).transpose(0, 1)
-        torch.bmm(x, W2, out=h2)
-        torch.nn.functional.elu(h2, inplace=True)
-        torch.bmm(h2, W3, out=h3)
-        torch.nn.functional.elu(h3, inplace=True)
-    print("library path us", t(lib))
-    print("  L1 addmm us", t(lambda: torch.addmm(b1, obs, W1, out=h1)))
-    x = h1.view(N, 2, 512).transpose(0, 1)
-    print("  L2 bmm us", t(lambda: torch.bmm(x, W2, out=h2)))
-    print("  L3 bmm us", t(lambda: torch.bmm(h2, W3, out=h3)))
+        x = obs
+        for i in range(4):
+            torch.addmm(bs[i], x, Wt[i], out=hs[i])
+            if i < 3:
+                torch.nn.functional.elu_(hs[i])
+            x = hs[i]
+    print("library actor us", t(lib))
+    for i in range(4):
+        x = obs if i == 0 else hs[i - 1]
+        print(f"  L{i} addmm us", t(lambda: torch.addmm(bs[i], x, Wt[i], out=hs[i])))
+    print("  elu 4096x512 us", t(lambda: torch.nn.functional.elu_(hs[0])))
+    ref = ac.actor(obs)
+    lib()
+    print("max |lib - torch|", (hs[3] - ref).abs().max().item())
