@@ -6,7 +6,8 @@
 //   * rsl_rl ActorCritic inference in the rollout (obs-512-256-128-{12,1}, ELU): actor and
 //     critic run in the SAME launch (blockIdx.y selects the network).
 //
-// Tiling (256-thread workgroup = 4 waves; no barrier inside a layer's K loop):
+// Tiling (NW = 8 waves per workgroup for the policy nets, 4 for narrow nets; no barrier inside
+// a layer's K loop):
 //   * a row tile of BM = 16*RS rows stays in LDS across ALL layers: layer input and output
 //     live at opposite ends of one activation region whose row strides are = 2 (mod 32), which
 //     makes the MFMA A-fragment reads (16 rows x 2 k per 32-lane half) bank-conflict free;
@@ -14,8 +15,10 @@
 //   * B fragments stream straight from the transposed weights W^T [in][out] (L2-resident,
 //     16 consecutive columns per 4 k-rows = 4 x 64 B per load) into a double-buffered ring
 //     of 8 VGPRs per lane, one group of k-steps ahead of the MFMAs consuming the other ring;
-//   * wave w owns output column tiles w, w+4, ... (16 columns each); a layer with TPW tiles
+//   * wave w owns output column tiles w, w+NW, ... (16 columns each); a layer with TPW tiles
 //     per wave processes G = 8/TPW k-steps per group, so every group is 8 B loads + 8*RS MFMAs;
+//     8 waves on a 16-row tile halve each wave's column share (more waves in flight per
+//     weight byte: 4096-row rollout 90 -> 86 us isolated, 3.85M -> 3.92M env-steps/s in situ);
 //   * LDS is only the activation tile (<= 50 KB) -> 3-4 workgroups per CU hide the latency;
 //   * grid-stride over row tiles (persistent when rows >> grid * BM).
 #include <stdlib.h>
@@ -25,11 +28,9 @@
 #include "lgx_device.h"
 #include "lgx_internal.h"
 
-#define MLP_THREADS 256
 #define MLP_MAX_W 512
 #define MLP_MAX_LAYERS 6
-// <= 128 registers per lane: a policy-MLP workgroup fits beside a physics workgroup (376
-// registers, 85 KB LDS) on the same CU, so the rollout critic forward overlaps physics
+// register budget per lane of the fused kernel (no AGPR spill copies; 4 waves per SIMD fit)
 #ifndef LGX_MLP_MAX_VGPR
 #define LGX_MLP_MAX_VGPR 128
 #endif
@@ -63,7 +64,7 @@ __host__ __device__ inline int pad16(int n) { return (n + 15) & ~15; }
 __host__ __device__ inline int act_stride(int n) { return pad32(n) + 2; }  // == 2 (mod 32)
 
 // one layer: acc = in[BM x K] @ W^T[K x N]; TPW = column tiles per wave, G = k-steps per group
-template <int RS, int TPW, int MAXT>
+template <int RS, int TPW, int MAXT, int NW>
 LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* __restrict__ W, int K, int N,
                        int wave, int ln16, int lq, f32x4 (&acc)[RS][MAXT]) {
   constexpr int G = 8 / TPW;
@@ -72,7 +73,7 @@ LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* 
   bool cv[TPW];
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
-    col[t] = (wave + 4 * t) * 16 + ln16;
+    col[t] = (wave + NW * t) * 16 + ln16;
     cv[t] = col[t] < N;
   }
   float bA[G][TPW], bB[G][TPW];
@@ -108,9 +109,10 @@ LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* 
   }
 }
 
-template <int RS, int ACTW, int MAXT>
-__global__ void __launch_bounds__(MLP_THREADS) __attribute__((amdgpu_num_vgpr(LGX_MLP_MAX_VGPR)))
+template <int RS, int ACTW, int MAXT, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_num_vgpr(LGX_MLP_MAX_VGPR)))
 lgx_mlp_forward_kernel(MlpBatch batch) {
+  constexpr int NT = 64 * NW;
   constexpr int BM = 16 * RS;
   __shared__ float act_lds[BM * ACTW];
   const MlpArgs& a = batch.m[blockIdx.y];
@@ -127,7 +129,7 @@ lgx_mlp_forward_kernel(MlpBatch batch) {
     const int K0p = pad32(K0);
     int s_in = act_stride(K0);
     int in_off = 0;
-    for (int idx = tid; idx < BM * K0p; idx += MLP_THREADS) {
+    for (int idx = tid; idx < BM * K0p; idx += NT) {
       int r = idx / K0p, k = idx - r * K0p;
       int64_t gr = r0 + r;
       act_lds[r * s_in + k] = (gr < a.rows && k < K0) ? a.x[gr * K0 + k] : 0.f;
@@ -139,7 +141,7 @@ lgx_mlp_forward_kernel(MlpBatch batch) {
       const int s_out = act_stride(N);
       const int out_off = (in_off == 0) ? ACTW * BM - BM * s_out : 0;
       const int ntile = pad16(N) >> 4;
-      const int tpw = (ntile + 3) >> 2;
+      const int tpw = (ntile + NW - 1) / NW;
       f32x4 acc[RS][MAXT];
 #pragma unroll
       for (int r = 0; r < RS; ++r)
@@ -147,19 +149,19 @@ lgx_mlp_forward_kernel(MlpBatch batch) {
         for (int t = 0; t < MAXT; ++t) acc[r][t] = f32x4{0.f, 0.f, 0.f, 0.f};
       const float* in_lds = act_lds + in_off;
       if constexpr (MAXT >= 8) {
-        if (tpw > 4) mlp_layer<RS, 8, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
-        else if (tpw > 2) mlp_layer<RS, 4, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
-        else if (tpw > 1) mlp_layer<RS, 2, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
-        else mlp_layer<RS, 1, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        if (tpw > 4) mlp_layer<RS, 8, MAXT, NW>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else if (tpw > 2) mlp_layer<RS, 4, MAXT, NW>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else if (tpw > 1) mlp_layer<RS, 2, MAXT, NW>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else mlp_layer<RS, 1, MAXT, NW>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
       } else {
-        if (tpw > 1) mlp_layer<RS, 2, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
-        else mlp_layer<RS, 1, MAXT>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        if (tpw > 1) mlp_layer<RS, 2, MAXT, NW>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
+        else mlp_layer<RS, 1, MAXT, NW>(in_lds, s_in, a.wt[l], K, N, wave, ln16, lq, acc);
       }
       // epilogue: bias + activation -> LDS output region (zero pad to pad32) or Y
       const int Np32 = pad32(N);
 #pragma unroll
       for (int t = 0; t < MAXT; ++t) {
-        const int ct = wave + 4 * t;
+        const int ct = wave + NW * t;
         if (t >= tpw) break;
         const int col = ct * 16 + ln16;
         const bool cv = col < N;
@@ -182,7 +184,7 @@ lgx_mlp_forward_kernel(MlpBatch batch) {
       if (!last) {
         // columns [pad16(N), pad32(N)) have no owning tile: zero them for the next layer's k reads
         const int p16 = pad16(N);
-        for (int idx = tid; idx < BM * (Np32 - p16); idx += MLP_THREADS) {
+        for (int idx = tid; idx < BM * (Np32 - p16); idx += NT) {
           int r = idx / (Np32 - p16), cc = p16 + idx % (Np32 - p16);
           act_lds[out_off + r * s_out + cc] = 0.f;
         }
@@ -212,6 +214,11 @@ static int needed_actw(const MlpArgs& a) {
   return w;
 }
 
+static int wide_waves() {
+  const char* e = getenv("LGX_MLP_WAVES");  // A/B switch: waves per workgroup of the wide kernel
+  return e ? atoi(e) : 8;
+}
+
 static int launch_batch(const MlpBatch& b, int count, hipStream_t stream) {
   int64_t rows = 0;
   int actw = 0;
@@ -231,16 +238,21 @@ static int launch_batch(const MlpBatch& b, int count, hipStream_t stream) {
   const bool narrow = actw <= 264 && maxw <= 128;
   if (!narrow && actw > 1032) return -1;
   // narrow nets (actuator MLP, <= 128 wide): 32-row tiles, 33 KB LDS; wide (policy): 16-row tiles
-  const int bm = narrow ? 32 : 16;
+  const int ww = wide_waves();  // 4: 16-row tiles x 4 waves; 8: 16 x 8; 16: 32-row tiles x 8 waves
+  const int bm = (narrow || (ww == 16 && actw <= 776)) ? 32 : 16;
   int64_t tiles = (rows + bm - 1) / bm;
   int64_t grid = tiles < 2048 ? tiles : 2048;
   dim3 g((unsigned)grid, (unsigned)count);
   if (narrow)
-    LGX_LAUNCH((lgx_mlp_forward_kernel<2, 264, 2>), g, dim3(MLP_THREADS), 0, stream, b);
+    LGX_LAUNCH((lgx_mlp_forward_kernel<2, 264, 2, 4>), g, dim3(256), 0, stream, b);
+  else if (actw <= 776 && ww == 16)
+    LGX_LAUNCH((lgx_mlp_forward_kernel<2, 776, 8, 8>), g, dim3(512), 0, stream, b);
+  else if (actw <= 776 && ww == 8)
+    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 776, 8, 8>), g, dim3(512), 0, stream, b);
   else if (actw <= 776)
-    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 776, 8>), g, dim3(MLP_THREADS), 0, stream, b);
+    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 776, 8, 4>), g, dim3(256), 0, stream, b);
   else
-    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 1032, 8>), g, dim3(MLP_THREADS), 0, stream, b);
+    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 1032, 8, 4>), g, dim3(256), 0, stream, b);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

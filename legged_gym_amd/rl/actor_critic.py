@@ -112,19 +112,22 @@ class _FusedMLP:
         return run_fused([(self, x)])[0]
 
 
-def run_fused(pairs):
-    """One lgx_mlp_forward_batch launch for up to two (fused_mlp, input) pairs."""
-    from legged_gym_amd.sim import abi
+def launch_forward(descs, count, stream):
+    """`count` (1 or 2) MLP descriptors in one lgx_mlp_forward_batch launch on `stream`."""
     from legged_gym_amd.sim import lib as lgxlib
-    lib = lgxlib.load()
+    lgxlib.check(lgxlib.load().lgx_mlp_forward_batch(descs, count, stream), "lgx_mlp_forward_batch")
+
+
+def run_fused(pairs):
+    """Forward of up to two (fused_mlp, input) pairs in one launch."""
+    from legged_gym_amd.sim import abi
     outs, descs = [], (abi.LgxMlpDesc * len(pairs))()
     for i, (m, x) in enumerate(pairs):
         x = x.contiguous()
         y = torch.empty(x.shape[0], m.dims[-1], device=x.device, dtype=torch.float)
         descs[i] = m.desc(x, y)
         outs.append((x, y))
-    stream = C.c_void_p(torch.cuda.current_stream(pairs[0][1].device).cuda_stream)
-    lgxlib.check(lib.lgx_mlp_forward_batch(descs, len(pairs), stream), "lgx_mlp_forward_batch")
+    launch_forward(descs, len(pairs), C.c_void_p(torch.cuda.current_stream(pairs[0][1].device).cuda_stream))
     return [y for _, y in outs]
 
 

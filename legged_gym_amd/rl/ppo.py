@@ -9,7 +9,6 @@ global mean, so every rank applies the identical Adam step and N ranks x B envs 
 1 rank x N*B envs up to reduction order.
 """
 import ctypes as C
-import os
 
 import torch
 import torch.nn as nn
@@ -17,7 +16,7 @@ import torch.optim as optim
 
 from legged_gym_amd.sim import abi
 
-from .actor_critic import ActorCritic
+from .actor_critic import ActorCritic, launch_forward
 from .fused_ppo import FusedPPOUpdate
 from .storage import RolloutStorage
 
@@ -34,9 +33,6 @@ class PPO:
                  value_loss_coef=1.0, entropy_coef=0.0, learning_rate=1e-3, max_grad_norm=1.0,
                  use_clipped_value_loss=True, schedule="fixed", desired_kl=0.01, device="cpu", use_fused_update=True):
         self.device = device
-        # critic forward of the rollout on a side stream, overlapping physics (A/B switch; off:
-        # with 4096 rows a single-net launch fills only half the chip)
-        self.overlap_critic = os.environ.get("LGX_CRITIC_OVERLAP", "0") == "1"
         self.desired_kl = desired_kl
         self.schedule = schedule
         self.learning_rate = learning_rate
@@ -85,15 +81,11 @@ class PPO:
                 and self.storage.step < self.storage.num_transitions_per_env)
 
     def _act_fused(self, obs, critic_obs):
-        """act() + add_transitions' row writes: the rollout MLP (actor and critic in one launch; the
-        critic writes its storage row directly) and lgx_ppo_act on the caller's stream.  With
-        overlap_critic the critic forward instead runs on a side stream after the actor, beside
-        this step's physics; process_env_step (time-out bootstrap) waits for it."""
+        """act() + add_transitions' row writes in two launches: the rollout MLP (actor and critic
+        in one launch; the critic writes its storage row directly) and lgx_ppo_act."""
         ac = self.actor_critic
         if not (ac._fused_ok(obs, ac._fused_actor) and ac._fused_critic.ok):
             return None
-        from legged_gym_amd.sim import lib as lgxlib
-        lib = lgxlib.load()
         st, s = self.storage, self.storage.step
         main = torch.cuda.current_stream(obs.device)
         obs = obs.contiguous()
@@ -103,23 +95,8 @@ class PPO:
             self._mean_buf = torch.empty(obs.shape[0], A, device=obs.device)
         mean = self._mean_buf
         descs = (abi.LgxMlpDesc * 2)(ac._fused_actor.desc(obs, mean),
-                                     ac._fused_critic.desc(critic_obs, st.values[s]))  # weights refreshed on main
-        if not self.overlap_critic:   # actor and critic in one launch (blockIdx.y = net)
-            lgxlib.check(lib.lgx_mlp_forward_batch(descs, 2, C.c_void_p(main.cuda_stream)), "lgx_mlp_forward_batch")
-        else:
-            lgxlib.check(lib.lgx_mlp_forward_batch(descs, 1, C.c_void_p(main.cuda_stream)), "lgx_mlp_forward_batch")
-            cdesc = (abi.LgxMlpDesc * 1)(descs[1])
-            # after the actor (not beside it: two MLPs only split the MFMA pipes), so the critic
-            # shares the CUs with the latency-bound physics kernel of this step instead
-            if getattr(self, "_side", None) is None:
-                self._side = torch.cuda.Stream(device=obs.device)
-                self._ev_in, self._ev_value = torch.cuda.Event(), torch.cuda.Event()
-            self._ev_in.record(main)
-            self._side.wait_event(self._ev_in)
-            lgxlib.check(lib.lgx_mlp_forward_batch(cdesc, 1, C.c_void_p(self._side.cuda_stream)), "lgx_mlp_forward_batch")
-            self._ev_value.record(self._side)
-            critic_obs.record_stream(self._side)
-            self._value_pending = True
+                                     ac._fused_critic.desc(critic_obs, st.values[s]))
+        launch_forward(descs, 2, C.c_void_p(main.cuda_stream))   # actor and critic in one launch
         if getattr(self, "_act_out", None) is None or self._act_out.shape != mean.shape:
             self._act_out = torch.empty_like(mean)
         noise = torch.randn_like(mean)            # Normal.sample's draws (torch generator, as upstream)
@@ -180,11 +157,8 @@ class PPO:
                 a.time_outs = to.data_ptr()
             a.st_values, a.st_rew, a.st_dones = st.values[st.step].data_ptr(), st.rewards[st.step].data_ptr(), \
                 st.dones[st.step].data_ptr()
-            main = torch.cuda.current_stream(rewards.device)
-            if getattr(self, "_value_pending", False):   # critic forward of this row (side stream)
-                main.wait_event(self._ev_value)
-                self._value_pending = False
-            self._fused.check(self._fused.lib.lgx_ppo_store(C.byref(a), C.c_void_p(main.cuda_stream)), "lgx_ppo_store")
+            self._fused.check(self._fused.lib.lgx_ppo_store(C.byref(a), C.c_void_p(
+                torch.cuda.current_stream(rewards.device).cuda_stream)), "lgx_ppo_store")
             st.step += 1
             t.clear()
             self.actor_critic.reset(dones)
