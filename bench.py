@@ -31,7 +31,41 @@ PHYS_PMC_TRAFFIC_BYTES = int((2 * 4508.4 + 11584.0) * 1024)
 ACT_PMC_TRAFFIC_BYTES = int((2 * 4521.6 + 768.0) * 1024)    # actuator MLP launch, same passes
 
 
-from legged_gym_amd.sim.flops import physics_flop_per_env_substep  # noqa: E402
+from legged_gym_amd.sim.flops import physics_flop_per_env_substep, policy_flop_per_sample  # noqa: E402
+
+# compulsory HBM bytes per env-step outside the PPO storage: physics state
+# in/out + actuator-net rows, post-physics gathers/obs/heights/state
+ENV_BYTES_PER_ENV_STEP = (3.0e6 + 11.9e6) / 4096 + 3.7e3
+
+
+def iteration_roofline(runner, env, N, it_ms):
+    """T_roof = sum over phases of max(bytes / HBM peak, FLOP / compute peak) for
+    one PPO iteration on one GPU; frac = T_roof / measured iteration time."""
+    alg, ac, st = runner.alg, runner.alg.actor_critic, runner.alg.storage
+    dims = lambda seq: [m.in_features for m in seq if hasattr(m, "in_features")][:1] + \
+        [m.out_features for m in seq if hasattr(m, "out_features")]
+    fwd, epoch = policy_flop_per_sample(dims(ac.actor), dims(ac.critic))
+    samples = runner.num_steps_per_env * N
+    row_bytes = sum(t[0].numel() * t.element_size() for t in (
+        st.observations, st.actions, st.rewards, st.dones, st.values, st.returns, st.advantages,
+        st.actions_log_prob, st.mu, st.sigma)) / st.num_envs   # storage row bytes per sample
+    decim = env.cfg.control.decimation
+    phases = {
+        "physics (fp32 VALU)": (samples * decim * physics_flop_per_env_substep(
+            env._lgx_model.num_points, 4.0, env.cfg.terrain.mesh_type in ("heightfield", "trimesh")),
+            samples * ENV_BYTES_PER_ENV_STEP),
+        "actuator net (f32 MFMA)": (samples * ACT_MLP_FLOP_PER_ENV_STEP if hasattr(env, "_actuator_dvel") else 0, 0),
+        "rollout policy forward (f32 MFMA)": (samples * fwd, 0),
+        "PPO update (f32 MFMA)": (alg.num_learning_epochs * samples * epoch,
+                                  samples * row_bytes * (1 + alg.num_learning_epochs)),
+    }
+    out, t_roof = {}, 0.0
+    for name, (flop, nbytes) in phases.items():
+        t = max(flop / (MI355X_F32_PEAK_TFLOPS * 1e12), nbytes / (MI355X_HBM_PEAK_GBS * 1e9)) * 1e3
+        out[name] = {"flop": flop, "hbm_bytes": int(nbytes), "t_roof_ms": round(t, 4)}
+        t_roof += t
+    return {"t_roof_ms": round(t_roof, 3), "t_measured_ms": round(it_ms, 3), "frac": t_roof / it_ms,
+            "peaks": {"f32_tflops": MI355X_F32_PEAK_TFLOPS, "hbm_gbs": MI355X_HBM_PEAK_GBS}, "phases": out}
 
 
 BASELINE_METRIC = "env-steps/sec (whole node), Go1 rough-terrain 4096 envs/GPU at 1/2/4/8 GPUs"
@@ -184,6 +218,7 @@ def main():
                    "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
         "roofline": roof,
         "roofline_secondary": roof2,
+        "iteration_roofline": iteration_roofline(runner, env, N, it_ms),
         "dominant_lgx_kernel": names[dom],
         "lgx_kernels": kernels,
         "last_iteration": runner.last_iteration_stats,

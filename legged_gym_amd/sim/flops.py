@@ -63,6 +63,21 @@ def actuator_mlp_flop_per_row(dims=(30, 128, 128, 128, 3)):
     return 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
 
 
+def _macs(dims):
+    return sum(a * b for a, b in zip(dims[:-1], dims[1:]))
+
+
+def policy_flop_per_sample(actor_dims, critic_dims):
+    """(rollout forward, one PPO epoch) FLOP per sample of the rsl_rl ActorCritic
+    (SURVEY.md §8 a15/a16): forward = both nets; an epoch = forward + weight gradients of every
+    layer + input gradients of every layer but the first (the observations need none)."""
+    fwd = _macs(actor_dims) + _macs(critic_dims)
+    first = actor_dims[0] * actor_dims[1] + critic_dims[0] * critic_dims[1]
+    return 2 * fwd, 2 * (fwd + fwd + (fwd - first))
+
+
 if __name__ == "__main__":
+    print("policy (235-obs) fwd / epoch FLOP per sample:",
+          policy_flop_per_sample((235, 512, 256, 128, 12), (235, 512, 256, 128, 1)))
     for name, nc, hf in (("go1 plane", 92, False), ("go1 rough", 92, True), ("anymal_c rough", 37, True)):
         print(f"{name:16s} {physics_flop_per_env_substep(nc, 4.0, hf):8.0f} FLOP/env-substep")
