@@ -9,8 +9,9 @@
 
 // ---------------------------------------------------------------- Philox4x32-10 uniforms
 // Same stream as the oracle's lgxo_uniform: counter (env, slot/4, step, tag), key = seed.
-LGX_DEV float lgx_uniform(uint64_t seed, int32_t env, int32_t slot, int64_t step, uint32_t tag) {
-  uint32_t c0 = (uint32_t)env, c1 = (uint32_t)(slot >> 2), c2 = (uint32_t)step;
+// Philox-4x32-10 block of draw slots (4q .. 4q+3): one counter per 4 consecutive slots
+LGX_DEV void lgx_uniform4(uint64_t seed, int32_t env, int32_t slot4, int64_t step, uint32_t tag, float out[4]) {
+  uint32_t c0 = (uint32_t)env, c1 = (uint32_t)slot4, c2 = (uint32_t)step;
   uint32_t c3 = tag ^ ((uint32_t)((uint64_t)step >> 32) << 8);
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
@@ -21,8 +22,15 @@ LGX_DEV float lgx_uniform(uint64_t seed, int32_t env, int32_t slot, int64_t step
     c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
     k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
   }
-  uint32_t sel = (slot & 3) == 0 ? c0 : (slot & 3) == 1 ? c1 : (slot & 3) == 2 ? c2 : c3;
-  return (float)(sel >> 8) * (1.0f / 16777216.0f);
+  const float s = 1.0f / 16777216.0f;
+  out[0] = (float)(c0 >> 8) * s; out[1] = (float)(c1 >> 8) * s;
+  out[2] = (float)(c2 >> 8) * s; out[3] = (float)(c3 >> 8) * s;
+}
+
+LGX_DEV float lgx_uniform(uint64_t seed, int32_t env, int32_t slot, int64_t step, uint32_t tag) {
+  float u[4];
+  lgx_uniform4(seed, env, slot >> 2, step, tag, u);
+  return (slot & 3) == 0 ? u[0] : (slot & 3) == 1 ? u[1] : (slot & 3) == 2 ? u[2] : u[3];
 }
 
 // ---------------------------------------------------------------- small vector math

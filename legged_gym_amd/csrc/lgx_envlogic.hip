@@ -14,6 +14,7 @@
 #include "lgx_internal.h"
 
 #define ENV_THREADS (16 * LGX_ENV_BLOCK)
+static_assert(LGX_DRAW_NOISE % 4 == 0, "observation noise slots must start a Philox block");
 
 namespace {
 
@@ -23,6 +24,15 @@ struct Draws {
   int32_t stride;
   LGX_DEV float operator()(int e, int slot, int64_t step, uint32_t tag) const {
     return inj ? inj[(int64_t)e * stride + slot] : lgx_uniform(P->seed, e, slot, step, tag);
+  }
+  // slots 4q .. 4q+3 (one Philox block); injected rows may end mid-block
+  LGX_DEV void quad(int e, int q, int64_t step, uint32_t tag, float u[4]) const {
+    if (inj) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) u[k] = 4 * q + k < stride ? inj[(int64_t)e * stride + 4 * q + k] : 0.f;
+    } else {
+      lgx_uniform4(P->seed, e, q, step, tag, u);
+    }
   }
 };
 
@@ -200,6 +210,10 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   const Draws D{P, draws, LGX_DRAW_NOISE + nobs};
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
   __shared__ float part[LGX_ENV_BLOCK][LGX_PARTIAL_STRIDE];
+  // what phase C (observations) reads, kept in LDS: heights (phase A), base-frame velocities,
+  // gravity, commands and root z (phase B, post-reset); dof state / actions are in srow below
+  __shared__ float sheight[LGX_ENV_BLOCK][LGX_MAX_HEIGHT_POINTS];
+  __shared__ float sbase[LGX_ENV_BLOCK][14];   // blv 3, bav 3, pg 3, cmd 4, root z
 
   // ---- phase A: height scan (legged_robot.py:818-854), pre-reset base pose.  The per-env yaw
   // rotation and base xy are staged in LDS; the (env, point) loop is unrolled so several
@@ -225,6 +239,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
         float* mh = B.measured_heights + (int64_t)e * np + i;
         if (P->terrain_kind == 0) {
           *mh = 0.f;
+          sheight[le][i] = 0.f;
         } else {
           const float4 b = base_xy_yaw[le];
           f3 o = quat_apply(0.f, 0.f, b.z, b.w, mk3(P->height_points[i][0], P->height_points[i][1], 0.f));
@@ -233,7 +248,9 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
           px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
           py = py < 0 ? 0 : (py > B.hf_cols - 2 ? B.hf_cols - 2 : py);
           int h1 = H[px * B.hf_cols + py], h2 = H[(px + 1) * B.hf_cols + py], h3 = H[px * B.hf_cols + py + 1];
-          *mh = (float)min(min(h1, h2), h3) * P->vertical_scale;
+          const float hv = (float)min(min(h1, h2), h3) * P->vertical_scale;
+          *mh = hv;
+          sheight[le][i] = hv;
         }
       }
     }
@@ -255,6 +272,18 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
     else if (c < 60 + LGX_MAX_BODIES * 3) v = B.last_actions[(int64_t)e * 12 + c - 48 - LGX_MAX_BODIES * 3];
     else v = B.last_dof_vel[(int64_t)e * 12 + c - 60 - LGX_MAX_BODIES * 3];
     srow[le][c] = v;
+  }
+  // episode sums [T, N] and feet_air_time [N, 4] are read-modify-written by the env lane: stage
+  // them too (coalesced over envs), so phase B has no dependent global round trips
+  __shared__ float ssum[LGX_MAX_TERMS][LGX_ENV_BLOCK];
+  __shared__ float sfat[LGX_ENV_BLOCK][4];
+  for (int idx = tid; idx < T * LGX_ENV_BLOCK; idx += ENV_THREADS) {
+    const int t = idx / LGX_ENV_BLOCK, le = idx - t * LGX_ENV_BLOCK;
+    ssum[t][le] = e0 + le < N ? B.episode_sums[(int64_t)t * N + e0 + le] : 0.f;
+  }
+  if (tid < LGX_ENV_BLOCK * 4) {
+    const int le = tid >> 2;
+    sfat[le][tid & 3] = e0 + le < N ? B.feet_air_time[(int64_t)(e0 + le) * 4 + (tid & 3)] : 0.f;
   }
   __syncthreads();
 
@@ -290,7 +319,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
       v.act = srow[tid] + 36 + LGX_MAX_BODIES * 3;
       v.la = srow[tid] + 48 + LGX_MAX_BODIES * 3;
       v.ldv = srow[tid] + 60 + LGX_MAX_BODIES * 3;
-      v.fat = B.feet_air_time + (int64_t)e * 4;
+      v.fat = sfat[tid];
       v.rootz = rs[2];
       v.mh = B.measured_heights ? B.measured_heights + (int64_t)e * P->num_height_points : nullptr;
       // check_termination :143-148
@@ -303,25 +332,34 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
       for (int t = 0; t < P->num_terms; ++t) {
         float rr = reward_term(P, v, P->term_ids[t]) * P->term_scales[t];
         rew += rr;
-        B.episode_sums[(int64_t)t * N + e] += rr;
+        ssum[t][tid] += rr;
       }
       if (P->only_positive_rewards) rew = fmaxf(rew, 0.f);
       if (P->termination_slot >= 0) {
         float rr = reward_term(P, v, LGX_R_TERMINATION) * P->termination_scale;
         rew += rr;
-        B.episode_sums[(int64_t)P->termination_slot * N + e] += rr;
+        ssum[P->termination_slot][tid] += rr;
       }
       B.rew[e] = rew;
       B.time_out[e] = v.time_out ? 1 : 0;
       B.reset[e] = v.reset ? 1 : 0;
       if (v.reset) {  // reset_idx :150-193
         for (int t = 0; t < T; ++t) {
-          part[tid][t] = B.episode_sums[(int64_t)t * N + e];
-          B.episode_sums[(int64_t)t * N + e] = 0.f;
+          part[tid][t] = ssum[t][tid];
+          ssum[t][tid] = 0.f;
         }
         part[tid][T] = 1.f;
-        reset_env(P, B, D, e, step, 0u, true, v.cmd);
+        reset_env(P, B, D, e, step, 0u, true, v.cmd);   // zeroes feet_air_time in HBM
+#pragma unroll
+        for (int f = 0; f < 4; ++f) sfat[tid][f] = 0.f;
+        for (int c = 0; c < 24; ++c) srow[tid][c] = B.dof_state[(int64_t)e * 24 + c];  // post-reset rows
       }
+      sbase[tid][0] = v.blv.x; sbase[tid][1] = v.blv.y; sbase[tid][2] = v.blv.z;
+      sbase[tid][3] = v.bav.x; sbase[tid][4] = v.bav.y; sbase[tid][5] = v.bav.z;
+      sbase[tid][6] = v.pg.x; sbase[tid][7] = v.pg.y; sbase[tid][8] = v.pg.z;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sbase[tid][9 + k] = v.cmd[k];
+      sbase[tid][13] = rs[2];
       for (int k = 0; k < 4; ++k) cmd_g[k] = v.cmd[k];
       if (P->curriculum) part[tid][T + 1] = (float)B.terrain_levels[e];
       float* o3 = B.base_lin_vel + (int64_t)e * 3;
@@ -334,33 +372,49 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   }
   block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
   __syncthreads();
+  for (int idx = tid; idx < T * LGX_ENV_BLOCK; idx += ENV_THREADS) {   // staged rows back
+    const int t = idx / LGX_ENV_BLOCK, le = idx - t * LGX_ENV_BLOCK;
+    if (e0 + le < N) B.episode_sums[(int64_t)t * N + e0 + le] = ssum[t][le];
+  }
+  if (tid < LGX_ENV_BLOCK * 4 && e0 + (tid >> 2) < N)
+    B.feet_air_time[(int64_t)(e0 + (tid >> 2)) * 4 + (tid & 3)] = sfat[tid >> 2][tid & 3];
 
-  // ---- phase C: observations (:214-231) + noise + clip (:103-104)
-  const int total = LGX_ENV_BLOCK * nobs;
-#pragma unroll 4
+  // ---- phase C: observations (:214-231) + noise + clip (:103-104); a lane owns 4 consecutive
+  // entries of a row, whose noise is one Philox block (LGX_DRAW_NOISE is a multiple of 4)
+  const int nq = (nobs + 3) >> 2;
+  const int total = LGX_ENV_BLOCK * nq;
+#pragma unroll 2
   for (int idx = tid; idx < total; idx += ENV_THREADS) {
-    int le = idx / nobs, i = idx - le * nobs;
-    int e = e0 + le;
+    const int le = idx / nq, q = idx - le * nq;
+    const int e = e0 + le;
     if (e >= N) continue;
-    float o;
-    if (i < 3) o = B.base_lin_vel[(int64_t)e * 3 + i] * P->obs_scale_lin_vel;
-    else if (i < 6) o = B.base_ang_vel[(int64_t)e * 3 + i - 3] * P->obs_scale_ang_vel;
-    else if (i < 9) o = B.projected_gravity[(int64_t)e * 3 + i - 6];
-    else if (i < 12) o = B.commands[(int64_t)e * 4 + i - 9] * (i < 11 ? P->obs_scale_lin_vel : P->obs_scale_ang_vel);
-    else if (i < 24) o = (B.dof_state[(int64_t)e * 24 + 2 * (i - 12)] - P->default_dof_pos[i - 12]) * P->obs_scale_dof_pos;
-    else if (i < 36) o = B.dof_state[(int64_t)e * 24 + 2 * (i - 24) + 1] * P->obs_scale_dof_vel;
-    else if (i < 48) o = B.actions[(int64_t)e * 12 + i - 36];
-    else o = clampf(B.root_states[(int64_t)e * 13 + 2] - 0.5f - B.measured_heights[(int64_t)e * P->num_height_points + i - 48],
-                    -1.f, 1.f) * P->obs_scale_height;
-    if (P->add_noise) o += (2.f * D(e, LGX_DRAW_NOISE + i, step, 0u) - 1.f) * P->noise_scale_vec[i];
-    B.obs[(int64_t)e * nobs + i] = clampf(o, -P->clip_obs, P->clip_obs);
+    float nz[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+    if (P->add_noise) D.quad(e, (LGX_DRAW_NOISE >> 2) + q, step, 0u, nz);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = 4 * q + u;
+      if (i >= nobs) break;
+      const float* sb = sbase[le];
+      const float* sr = srow[le];
+      float o;
+      if (i < 3) o = sb[i] * P->obs_scale_lin_vel;
+      else if (i < 6) o = sb[i] * P->obs_scale_ang_vel;
+      else if (i < 9) o = sb[i];
+      else if (i < 12) o = sb[i] * (i < 11 ? P->obs_scale_lin_vel : P->obs_scale_ang_vel);
+      else if (i < 24) o = (sr[2 * (i - 12)] - P->default_dof_pos[i - 12]) * P->obs_scale_dof_pos;
+      else if (i < 36) o = sr[2 * (i - 24) + 1] * P->obs_scale_dof_vel;
+      else if (i < 48) o = sr[36 + LGX_MAX_BODIES * 3 + i - 36];
+      else o = clampf(sb[13] - 0.5f - sheight[le][i - 48], -1.f, 1.f) * P->obs_scale_height;
+      if (P->add_noise) o += (2.f * nz[u] - 1.f) * P->noise_scale_vec[i];
+      B.obs[(int64_t)e * nobs + i] = clampf(o, -P->clip_obs, P->clip_obs);
+    }
   }
   // ---- last_* copies (:136-138), post-reset values
   for (int idx = tid; idx < LGX_ENV_BLOCK * 12; idx += ENV_THREADS) {
     int e = e0 + idx / 12, j = idx % 12;
     if (e >= N) break;
-    B.last_actions[(int64_t)e * 12 + j] = B.actions[(int64_t)e * 12 + j];
-    B.last_dof_vel[(int64_t)e * 12 + j] = B.dof_state[(int64_t)e * 24 + 2 * j + 1];
+    B.last_actions[(int64_t)e * 12 + j] = srow[idx / 12][36 + LGX_MAX_BODIES * 3 + j];
+    B.last_dof_vel[(int64_t)e * 12 + j] = srow[idx / 12][2 * j + 1];
   }
   if (tid < LGX_ENV_BLOCK && e0 + tid < N) {
     int e = e0 + tid;
