@@ -85,7 +85,7 @@ def parse():
     p.add_argument("--task", default="go1_rough")
     p.add_argument("--num_envs", type=int, default=4096)
     p.add_argument("--no_cpu_baseline", action="store_true")
-    p.add_argument("--cpu_envs", type=int, default=256)
+    p.add_argument("--cpu_envs", type=int, default=1024)
     return p.parse_args()
 
 
@@ -101,8 +101,10 @@ def cpu_baseline(task, n_envs):
     from legged_gym_amd.rl.runner import OnPolicyRunner
     from legged_gym_amd.utils.helpers import class_to_dict
     from legged_gym_amd.utils.task_registry import task_registry
+    from oracle_backend import load_oracle
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     torch.set_num_threads(threads)
+    load_oracle().lgxo_set_threads(C.c_int(threads))   # the oracle's OpenMP env loops
     env = make_env(task, num_envs=n_envs, device="cpu", backend="oracle")
     _, train_cfg = task_registry.get_cfgs(task)
     runner = OnPolicyRunner(env, class_to_dict(type(train_cfg)()), None, device="cpu")
@@ -111,9 +113,17 @@ def cpu_baseline(task, n_envs):
     runner.learn(1)
     dt = time.time() - t0
     steps = runner.num_steps_per_env * n_envs
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return dict(value=steps / dt, unit="env-steps/s", cores=threads, kind="port",
                 sample=f"1 PPO iteration ({runner.num_steps_per_env} steps x {n_envs} envs, {task}) of the C oracle "
-                       f"env (OpenMP {threads} threads) + torch-CPU ActorCritic/PPO; {dt:.1f}s")
+                       f"env (OpenMP {threads} threads over envs: physics, actuator net, rewards, observations) + "
+                       f"torch-CPU ActorCritic/PPO ({threads} threads); {dt:.1f}s",
+                cpu_model=cpu_model, nproc=os.cpu_count())
 
 
 def main():

@@ -25,6 +25,9 @@
  * throughout, like the reference (torch float32) and the kernel.
  */
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -838,7 +841,8 @@ int lgxo_post_physics(const lgx_model* m, const lgx_env_params* p, const lgx_buf
     b->time_out[e] = (float)b->episode_length[e] > p->max_episode_length;
     b->reset[e] = (uint8_t)(r | b->time_out[e]);
   }
-  /* compute_reward :195-212 */
+  /* compute_reward :195-212 (per env: its own sums, rew and feet_air_time row) */
+#pragma omp parallel for schedule(static)
   for (int e = 0; e < N; ++e) {
     float rew = 0.0f;
     for (int t = 0; t < p->num_terms; ++t) {
@@ -860,6 +864,7 @@ int lgxo_post_physics(const lgx_model* m, const lgx_env_params* p, const lgx_buf
   for (int e = 0; e < N; ++e) if (b->reset[e]) ids[n++] = e;
   reset_envs(&cx, ids, n, step, 0u, 1);
   free(ids);
+#pragma omp parallel for schedule(static)
   for (int e = 0; e < N; ++e) {
     compute_obs(&cx, e, step);
     for (int i = 0; i < p->num_obs; ++i) {
@@ -873,6 +878,15 @@ int lgxo_post_physics(const lgx_model* m, const lgx_env_params* p, const lgx_buf
     for (int i = 0; i < 6; ++i) b->last_root_vel[e * 6 + i] = b->root_states[e * 13 + 7 + i];
   }
   return 0;
+}
+
+/* OpenMP threads of the oracle's per-env loops (the CPU baseline states the count it used) */
+void lgxo_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
 }
 
 /* full LeggedRobot.step (legged_robot.py:79-107) */
@@ -894,8 +908,9 @@ int lgxo_step(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b,
 /* UniNet core MLP on rows of 30 (go1.py:22-35): 30-128-128-128-3 tanh; out *= scale */
 void lgxo_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale) {
   const int dims[5] = {30, 128, 128, 128, 3};
-  float h0[128], h1[128];
+#pragma omp parallel for schedule(static)
   for (int64_t r = 0; r < rows; ++r) {
+    float h0[128], h1[128];
     const float* x = in + r * 30;
     float* cur = h0;
     const float* src = x;
