@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
 STEP=${1:-all}
 if [[ $STEP == all || $STEP == tests ]]; then
-  timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed rc=$?"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
+  timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed rc=$?"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
   tail -3 gpurun_out/gpu_tests.log
 fi
 if [[ $STEP == all || $STEP == bench ]]; then
