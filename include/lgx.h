@@ -200,8 +200,9 @@ int lgx_version(void);
 
 /* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers), sizeof(lgx_mlp_desc),
  * sizeof(lgx_ppo_loss_args), sizeof(lgx_reduce_job), sizeof(lgx_ppo_act_args),
- * sizeof(lgx_ppo_store_args): lets bindings verify layout */
-void lgx_struct_sizes(int64_t out[8]);
+ * sizeof(lgx_ppo_store_args), sizeof(lgx_gemm_args), sizeof(lgx_copy2d_job): lets bindings
+ * verify layout */
+void lgx_struct_sizes(int64_t out[10]);
 
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
@@ -412,6 +413,49 @@ int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream);
  * one flat parameter buffer; *step is advanced on the device; lr is a device double */
 int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts, float grad_scale,
                   float max_norm, const double* lr, int64_t* step, float beta1, float beta2, float eps, void* stream);
+
+/* ---- Fused f32-MFMA GEMMs of the PPO update (lgx_gemm.hip, hand-written for gfx950).
+ * Replace the library GEMM + lgx_bias_act (forward) and GEMM + lgx_elu_bwd_colsum (backward)
+ * pairs of a minibatch step (rsl_rl PPO.update, legged_robot_config.py:226-239):
+ *   C[z][m][n] = epi( sum_k A[z*sa + m*lda + k] * B[z*sb + n*ldb + k] ),  z < batch
+ *   LGX_GEMM_PLAIN        epi(x) = x
+ *   LGX_GEMM_BIAS_ELU     epi(x) = ELU(x + bias[z*N + n])
+ *   LGX_GEMM_DELU_COLSUM  C = x * ELU'(Y) with Y (same layout as C) the ELU output, and
+ *                         partials[t][z*N + n] = sum of C over rows 128t .. 128t+127
+ * Requirements: N % 128 == 0, K % 4 == 0, A/B 16-byte aligned with lda, ldb, sa, sb % 4 == 0
+ * (pad K with zero columns).  sa may be 0 (one input shared by the batch). */
+#define LGX_GEMM_PLAIN 0
+#define LGX_GEMM_BIAS_ELU 1
+#define LGX_GEMM_DELU_COLSUM 2
+typedef struct lgx_gemm_args {
+  int64_t M;
+  int32_t N, K, batch, epi;
+  const float* A;
+  int64_t lda, sa;
+  const float* B;
+  int64_t ldb, sb;
+  float* C;
+  int64_t ldc, sc;
+  const float* bias;            /* [batch][N] (BIAS_ELU) */
+  const float* Y;               /* like C (DELU_COLSUM) */
+  float* partials;              /* [lgx_gemm_partials_floats(M, N, batch)] (DELU_COLSUM) */
+} lgx_gemm_args;
+int64_t lgx_gemm_partials_floats(int64_t M, int32_t N, int32_t batch);
+int lgx_gemm_nt(const lgx_gemm_args* args, void* stream);
+
+/* weight preparation for lgx_gemm_nt: dst[b][r][c] = src[b][r][c] (transpose 0) or
+ * dst[b][c][r] = src[b][r][c] (transpose 1), r < rows, c < cols; dst padding is untouched */
+typedef struct lgx_copy2d_job {
+  const float* src;
+  float* dst;
+  int64_t src_ld, src_bs, dst_ld, dst_bs;
+  int32_t rows, cols, batch, transpose;
+} lgx_copy2d_job;
+int lgx_copy2d(const lgx_copy2d_job* jobs, int32_t njobs, void* stream);
+
+/* lgx_ppo_gather_rows into rows of dst_ld floats, columns width .. dst_ld-1 zero-filled */
+int lgx_ppo_gather_rows_padded(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width,
+                               int32_t dst_ld, void* stream);
 
 #ifdef __cplusplus
 }

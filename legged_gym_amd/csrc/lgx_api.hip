@@ -77,7 +77,7 @@ extern "C" {
 const char* lgx_last_error(void) { return g_err.c_str(); }
 int lgx_version(void) { return 1; }
 
-void lgx_struct_sizes(int64_t out[8]) {
+void lgx_struct_sizes(int64_t out[10]) {
   out[0] = (int64_t)sizeof(lgx_model);
   out[1] = (int64_t)sizeof(lgx_env_params);
   out[2] = (int64_t)sizeof(lgx_buffers);
@@ -86,6 +86,8 @@ void lgx_struct_sizes(int64_t out[8]) {
   out[5] = (int64_t)sizeof(lgx_reduce_job);
   out[6] = (int64_t)sizeof(lgx_ppo_act_args);
   out[7] = (int64_t)sizeof(lgx_ppo_store_args);
+  out[8] = (int64_t)sizeof(lgx_gemm_args);
+  out[9] = (int64_t)sizeof(lgx_copy2d_job);
 }
 
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms) {

@@ -1,0 +1,419 @@
+// Hand-written f32 GEMMs of the PPO update with their epilogues fused (gfx950,
+// v_mfma_f32_32x32x2_f32: exact f32, one rounding per product, 64 FLOP/clk/SIMD = the f32
+// matrix peak).  They replace, per minibatch of rsl_rl PPO.update (legged_robot_config.py:
+// 226-239), the library GEMM + separate epilogue passes of
+//   forward  Y_k = ELU(Y_{k-1} W_k^T + b_k)                 (GEMM + lgx_bias_act), and
+//   backward dZ_{k-1} = (dZ_k W_k) * ELU'(Y_{k-1}),  db_{k-1} = colsum(dZ_{k-1})
+//                                                           (GEMM + lgx_elu_bwd_colsum),
+// so every activation / gradient tile is written once, straight from the accumulators.
+//
+// Both are "NT" products C[z][m][n] = sum_k A[z][m][k] B[z][n][k] with K-contiguous rows on
+// both sides (B = the nn.Linear weight for the forward, its transpose - prepared once per
+// minibatch by lgx_copy2d - for the backward):
+//   * workgroup = 4 waves, 128 x 128 output tile, wave = 64 x 64 = 2 x 2 accumulator tiles
+//     (64 floats, 4 independent MFMA chains);
+//   * K stages of 32: the A and B tiles (128 rows x 128 B each) are copied global -> LDS with
+//     coalesced 16-byte loads, double-buffered (72 KB, 2 workgroups per CU), the next stage's
+//     loads in flight during the current stage's MFMAs, one barrier per stage;
+//   * 32x32x2 fragments: lane (r = l & 31, h = l >> 5) supplies A[row r][k] and B[k][col r]
+//     for the MFMA's two k values.  One ds_read_b128 per operand gives a lane 4 consecutive k;
+//     the k order is permuted (substep s of an 8-k group pairs k = s and 4 + s) identically
+//     for A and B, so the sum is unchanged; rows padded by 16 B: conflict-free b128 reads;
+//   * XCD-aware tile order: the tile index is split so that each of the 8 XCDs (workgroups
+//     are dealt round-robin to XCDs) owns a contiguous range of tiles, n fastest, then the
+//     batch index (actor / critic), then m: the A rows of one m-block (and, for the shared
+//     layer-1 input, both networks) are reused out of one XCD's L2;
+//   * epilogue in registers: bias + ELU, or ELU' (from the forward output) with the bias
+//     gradient column sums reduced per 128-row tile in a fixed order (bitwise reproducible).
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "lgx_internal.h"
+
+#define LGX_STREAM(s) reinterpret_cast<hipStream_t>(s)
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int GT = 256;     // threads per workgroup (4 waves)
+constexpr int BM = 128;     // rows per workgroup tile
+constexpr int BN = 128;     // columns per workgroup tile
+
+struct GemmArgs {
+  int64_t M;
+  int32_t N, K, batch, epi;
+  const float* A;
+  int64_t lda, sa;
+  const float* B;
+  int64_t ldb, sb;
+  float* C;
+  int64_t ldc, sc;
+  const float* bias;
+  const float* Y;
+  float* partials;
+};
+
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : __expf(x) - 1.f; }  // v_exp_f32
+__device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+constexpr int BK = 32;              // K per LDS stage
+constexpr int LDS_LD = BK + 4;      // row stride (floats): 16-B shift per row, conflict-free b128 reads
+constexpr int TILE_FLOATS = BM * LDS_LD;
+
+__device__ __forceinline__ float comp(const float4& q, int s) {
+  return s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
+}
+
+// One K stage of the global -> LDS copy: 128 rows x 32 k of A and of B, 4 float4 per thread
+// each (8 threads per 128-byte row segment: coalesced).  k >= K is zero-filled.
+struct Stage {
+  float4 a[4], b[4];
+};
+
+__device__ __forceinline__ void stage_load(Stage& st, const float* __restrict__ A, int64_t lda, int64_t m_base,
+                                           int64_t M, const float* __restrict__ B, int64_t ldb, int n_base, int K,
+                                           int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + GT * i, row = q >> 3, c = (q & 7) * 4;
+    int64_t m = m_base + row;
+    m = m < M ? m : M - 1;  // rows past M load row M-1 (results discarded)
+    // branch-free tail: past K, load the last valid float4 (zeroed in stage_store)
+    const int kc = min(k0 + c, K - 4);
+    st.a[i] = ld4(A + m * lda + kc);
+    st.b[i] = ld4(B + (int64_t)(n_base + row) * ldb + kc);
+  }
+}
+
+__device__ __forceinline__ void stage_store(const Stage& st, float* __restrict__ la, float* __restrict__ lb, int K,
+                                            int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + GT * i, row = q >> 3, c = (q & 7) * 4;
+    const bool in = k0 + c < K;
+    float4 va = st.a[i], vb = st.b[i];
+    va.x = in ? va.x : 0.f; va.y = in ? va.y : 0.f; va.z = in ? va.z : 0.f; va.w = in ? va.w : 0.f;
+    vb.x = in ? vb.x : 0.f; vb.y = in ? vb.y : 0.f; vb.z = in ? vb.z : 0.f; vb.w = in ? vb.w : 0.f;
+    *reinterpret_cast<float4*>(la + row * LDS_LD + c) = va;
+    *reinterpret_cast<float4*>(lb + row * LDS_LD + c) = vb;
+  }
+}
+
+// MFMAs of one LDS stage.  Lane (r, h) reads 4 consecutive k of its row per ds_read_b128:
+// k group g covers k = 8g .. 8g+7, lane half h holds 8g + 4h .. 8g + 4h + 3, and substep s of
+// the group pairs (8g + s, 8g + 4 + s) - the same permutation for A and B.  The fragments of
+// group g+1 are read while group g's 16 MFMAs run (register double buffer).
+struct LdsFrag {
+  float4 a[2], b[2];
+};
+
+__device__ __forceinline__ void frag_read(LdsFrag& f, const float* __restrict__ la, const float* __restrict__ lb,
+                                          int wm, int wn, int r, int h, int g) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    f.a[i] = *reinterpret_cast<const float4*>(la + (wm * 64 + 32 * i + r) * LDS_LD + 8 * g + 4 * h);
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+    f.b[j] = *reinterpret_cast<const float4*>(lb + (wn * 64 + 32 * j + r) * LDS_LD + 8 * g + 4 * h);
+}
+
+__device__ __forceinline__ void frag_mma(const LdsFrag& f, f32x16 (&acc)[2][2]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(f.a[i], s), comp(f.b[j], s), acc[i][j], 0, 0, 0);
+}
+
+__device__ __forceinline__ void stage_mma(const float* __restrict__ la, const float* __restrict__ lb, int wm, int wn,
+                                          int r, int h, f32x16 (&acc)[2][2]) {
+  LdsFrag f0, f1;
+  frag_read(f0, la, lb, wm, wn, r, h, 0);
+#pragma unroll
+  for (int g = 0; g < BK / 8; g += 2) {
+    frag_read(f1, la, lb, wm, wn, r, h, g + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    frag_mma(f0, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (g + 2 < BK / 8) frag_read(f0, la, lb, wm, wn, r, h, g + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    frag_mma(f1, acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+struct TileId {
+  int64_t mt;
+  int nt, z;
+};
+
+__device__ __forceinline__ TileId decode_tile(int64_t tile, int ntn, int batch) {
+  TileId t;
+  t.nt = (int)(tile % ntn);
+  const int64_t rest = tile / ntn;
+  t.z = (int)(rest % batch);
+  t.mt = rest / batch;
+  return t;
+}
+
+// ---- epilogue: acc[i][j][e] is C[m0 + 32i + (e & 3) + 8(e >> 2) + 4h][n0 + 32j + r].
+// 32-bit offsets from the wave's tile corner; whole tiles (every tile when M % 128 == 0) store
+// without row guards.
+__device__ __forceinline__ int acc_row(int i, int e, int h) { return 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h; }
+
+template <int EPI, bool FULL>
+__device__ __forceinline__ void epilogue_rows(const GemmArgs& g, const f32x16 (&acc)[2][2], int64_t m0, int n0, int z,
+                                              int r, int h, float (&cs)[2]) {
+  float* C = g.C + z * g.sc + m0 * g.ldc + n0;
+  const int ldc = (int)g.ldc;
+  const int rows = (int)min<int64_t>(64, g.M - m0);
+  if (EPI == LGX_GEMM_DELU_COLSUM) {
+    const float* Y = g.Y + z * g.sc + m0 * g.ldc + n0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e0 = 0; e0 < 16; e0 += 4) {   // 8 loads of Y in flight, then 8 stores
+        float y[4][2];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int rr = acc_row(i, e0 + e, h);
+            y[e][j] = (FULL || rr < rows) ? Y[rr * ldc + 32 * j + r] : 0.f;
+          }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int rr = acc_row(i, e0 + e, h);
+            const float d = acc[i][j][e0 + e] * elu_grad_from_out(y[e][j]);
+            if (FULL || rr < rows) {
+              C[rr * ldc + 32 * j + r] = d;
+              cs[j] += d;
+            }
+          }
+      }
+  } else {
+    float bj[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bj[j] = EPI == LGX_GEMM_BIAS_ELU ? g.bias[(int64_t)z * g.N + n0 + 32 * j + r] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int rr = acc_row(i, e, h);
+          float v = acc[i][j][e];
+          if (EPI == LGX_GEMM_BIAS_ELU) v = elu_f(v + bj[j]);
+          if (FULL || rr < rows) C[rr * ldc + 32 * j + r] = v;
+        }
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x16 (&acc)[2][2], const TileId& T, int wave, int r,
+                                         int h) {
+  const int64_t m0 = T.mt * BM + (wave >> 1) * 64;
+  const int n0 = T.nt * BN + (wave & 1) * 64;
+  float cs[2] = {0.f, 0.f};
+  if (T.mt * BM + BM <= g.M) epilogue_rows<EPI, true>(g, acc, m0, n0, T.z, r, h, cs);
+  else if (m0 < g.M) epilogue_rows<EPI, false>(g, acc, m0, n0, T.z, r, h, cs);
+  if (EPI == LGX_GEMM_DELU_COLSUM) {
+    // column sums: lane halves hold different rows of the same column, then the two wave rows
+    __shared__ float red[2][2][64];  // [wave row][wave column][column within the wave's 64]
+#pragma unroll
+    for (int j = 0; j < 2; ++j) cs[j] += __shfl_xor(cs[j], 32);
+    if (h == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) red[wave >> 1][wave & 1][32 * j + r] = cs[j];
+    }
+    __syncthreads();
+    if ((wave >> 1) == 0 && h == 0) {
+      float* P = g.partials + T.mt * ((int64_t)g.batch * g.N) + (int64_t)T.z * g.N;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) P[n0 + 32 * j + r] = red[0][wave & 1][32 * j + r] + red[1][wave & 1][32 * j + r];
+    }
+  }
+}
+
+// Persistent workgroups: the tiles of XCD x (workgroups are dealt round-robin to the 8 XCDs)
+// are the contiguous range [x T / 8, (x + 1) T / 8), n fastest, then the network, then m;
+// workgroup w of the XCD takes its tiles w, w + W, ...  The first K stage of the next tile is
+// loaded while the current tile's epilogue runs.
+template <int EPI>
+__global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float lds[4 * TILE_FLOATS];  // 2 stages x (A tile, B tile): 72 KB
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = g.N / BN;
+  const int64_t total = ((g.M + BM - 1) / BM) * ntn * g.batch;
+  const int xcd = blockIdx.x & 7;
+  const int64_t wg_per_xcd = gridDim.x >> 3;     // grid is a multiple of 8
+  const int64_t lo = xcd * total / 8, hi = (xcd + 1) * total / 8;
+  int64_t tile = lo + (blockIdx.x >> 3);
+  if (tile >= hi) return;
+  const int K = g.K;
+  const int nst = (K + BK - 1) / BK;
+
+  TileId T = decode_tile(tile, ntn, g.batch);
+  Stage st;
+  stage_load(st, g.A + T.z * g.sa, g.lda, T.mt * BM, g.M, g.B + T.z * g.sb, g.ldb, T.nt * BN, K, 0, tid);
+  for (;;) {
+    const int64_t next = tile + wg_per_xcd;
+    const bool has_next = next < hi;
+    const TileId Tn = decode_tile(has_next ? next : tile, ntn, g.batch);
+    const float* A = g.A + T.z * g.sa;
+    const float* B = g.B + T.z * g.sb;
+    stage_store(st, lds, lds + TILE_FLOATS, K, 0, tid);
+    __syncthreads();
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    // double-buffered LDS stages: the global loads of stage t+1 (after the last stage: stage 0
+    // of the next tile) are in flight while stage t's MFMAs run; one barrier per stage
+    for (int t = 0; t < nst; ++t) {
+      float* cur = lds + (t & 1) * 2 * TILE_FLOATS;
+      float* nxt = lds + ((t + 1) & 1) * 2 * TILE_FLOATS;
+      const bool more = t + 1 < nst;
+      if (more) stage_load(st, A, g.lda, T.mt * BM, g.M, B, g.ldb, T.nt * BN, K, (t + 1) * BK, tid);
+      else stage_load(st, g.A + Tn.z * g.sa, g.lda, Tn.mt * BM, g.M, g.B + Tn.z * g.sb, g.ldb, Tn.nt * BN, K, 0, tid);
+      __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs they overlap
+      stage_mma(cur, cur + TILE_FLOATS, wm, wn, r, h, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) stage_store(st, nxt, nxt + TILE_FLOATS, K, (t + 1) * BK, tid);
+      __syncthreads();
+    }
+    epilogue<EPI>(g, acc, T, wave, r, h);
+    if (!has_next) break;
+    tile = next;
+    T = Tn;
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- copy2d
+// dst[b][r][c] = src[b][r][c] (transpose = 0) or dst[b][c][r] = src[b][r][c] (transpose = 1),
+// 32 x 32 tiles through LDS (odd row stride: conflict-free transposed reads).  Several jobs in
+// one launch (the per-minibatch weight preparation of the fused GEMMs).
+namespace {
+struct Copy2dJobs {
+  lgx_copy2d_job job[LGX_MAX_REDUCE_JOBS];
+  int32_t tile_start[LGX_MAX_REDUCE_JOBS + 1];
+  int32_t njobs;
+};
+
+__global__ void __launch_bounds__(256) copy2d_kernel(Copy2dJobs J) {
+  __shared__ float t[32][33];
+  int b = blockIdx.x, ji = 0;
+  while (ji + 1 < J.njobs && b >= J.tile_start[ji + 1]) ++ji;
+  const lgx_copy2d_job& jb = J.job[ji];
+  const int local = b - J.tile_start[ji];
+  const int tr = (jb.rows + 31) / 32, tc = (jb.cols + 31) / 32;
+  const int bb = local / (tr * tc), rem = local % (tr * tc);
+  const int r0 = (rem / tc) * 32, c0 = (rem % tc) * 32;
+  const float* src = jb.src + (int64_t)bb * jb.src_bs;
+  float* dst = jb.dst + (int64_t)bb * jb.dst_bs;
+  const int x = threadIdx.x & 31, y = threadIdx.x >> 5;  // 8 rows of 32 per pass
+  for (int yy = y; yy < 32; yy += 8) {
+    const int rr = r0 + yy, cc = c0 + x;
+    if (rr < jb.rows && cc < jb.cols) t[yy][x] = src[(int64_t)rr * jb.src_ld + cc];
+  }
+  __syncthreads();
+  for (int yy = y; yy < 32; yy += 8) {
+    if (jb.transpose) {
+      const int cc = c0 + yy, rr = r0 + x;  // dst row = source column
+      if (rr < jb.rows && cc < jb.cols) dst[(int64_t)cc * jb.dst_ld + rr] = t[x][yy];
+    } else {
+      const int rr = r0 + yy, cc = c0 + x;
+      if (rr < jb.rows && cc < jb.cols) dst[(int64_t)rr * jb.dst_ld + cc] = t[yy][x];
+    }
+  }
+}
+
+// dst[r][0:width] = src[idx[r]][0:width], dst[r][width:dst_ld] = 0: one row per wave
+__global__ void __launch_bounds__(256) gather_rows_padded_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                                 const int64_t* __restrict__ idx, int64_t rows,
+                                                                 int32_t width, int32_t dst_ld) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  const float* s = src + idx[r] * width;
+  float* d = dst + r * dst_ld;
+  for (int c = lane; c < dst_ld; c += 64) d[c] = c < width ? s[c] : 0.f;
+}
+}  // namespace
+
+extern "C" int64_t lgx_gemm_partials_floats(int64_t M, int32_t N, int32_t batch) {
+  return ((M + BM - 1) / BM) * (int64_t)N * batch;
+}
+
+extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
+  if (!args) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: null args");
+  const lgx_gemm_args& a = *args;
+  const bool aligned = ((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0 && a.lda % 4 == 0 &&
+                       a.ldb % 4 == 0 && a.sa % 4 == 0 && a.sb % 4 == 0;
+  if (!a.A || !a.B || !a.C || a.M <= 0 || a.N <= 0 || a.N % BN || a.K <= 0 || a.K % 4 || a.batch <= 0 ||
+      a.batch > 65535 || !aligned || a.lda < a.K || a.ldb < a.K || a.ldc < a.N || a.ldc > (1 << 22) || a.epi < 0 || a.epi > 2 ||
+      (a.epi == LGX_GEMM_BIAS_ELU && !a.bias) || (a.epi == LGX_GEMM_DELU_COLSUM && (!a.Y || !a.partials)))
+    return lgx_fail(LGX_EINVAL,
+                    "lgx_gemm_nt: bad args (N % 128, K % 4, 16-byte aligned A/B rows, epilogue operands)");
+  const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
+  if (tiles > (1ll << 31) - 1) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too large");
+  GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
+             a.partials};
+  // persistent: 2 workgroups per CU (LDS-bound), a multiple of 8 (XCD tile ranges)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t per_xcd = (tiles + 7) / 8;
+  const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, 2 * cus / 8));
+  const dim3 grid((unsigned)wgs), block(GT);
+  if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH(gemm_nt_kernel<LGX_GEMM_BIAS_ELU>, grid, block, 0, LGX_STREAM(stream), g);
+  else if (a.epi == LGX_GEMM_DELU_COLSUM)
+    LGX_LAUNCH(gemm_nt_kernel<LGX_GEMM_DELU_COLSUM>, grid, block, 0, LGX_STREAM(stream), g);
+  else LGX_LAUNCH(gemm_nt_kernel<LGX_GEMM_PLAIN>, grid, block, 0, LGX_STREAM(stream), g);
+  return lgx_hip_status("lgx_gemm_nt");
+}
+
+extern "C" int lgx_copy2d(const lgx_copy2d_job* jobs, int32_t njobs, void* stream) {
+  if (!jobs || njobs <= 0 || njobs > LGX_MAX_REDUCE_JOBS) return lgx_fail(LGX_EINVAL, "lgx_copy2d: bad job count");
+  Copy2dJobs J;
+  int64_t tiles = 0;
+  J.njobs = njobs;
+  for (int i = 0; i < njobs; ++i) {
+    const lgx_copy2d_job& j = jobs[i];
+    if (!j.src || !j.dst || j.rows <= 0 || j.cols <= 0 || j.batch <= 0 ||
+        j.src_ld < j.cols || j.dst_ld < (j.transpose ? j.rows : j.cols))
+      return lgx_fail(LGX_EINVAL, "lgx_copy2d: bad job");
+    J.job[i] = j;
+    J.tile_start[i] = (int32_t)tiles;
+    tiles += (int64_t)j.batch * ((j.rows + 31) / 32) * ((j.cols + 31) / 32);
+    if (tiles > (1 << 30)) return lgx_fail(LGX_EINVAL, "lgx_copy2d: too large");
+  }
+  J.tile_start[njobs] = (int32_t)tiles;
+  hipLaunchKernelGGL(copy2d_kernel, dim3((unsigned)tiles), dim3(256), 0, LGX_STREAM(stream), J);
+  return lgx_hip_status("lgx_copy2d");
+}
+
+extern "C" int lgx_ppo_gather_rows_padded(const float* src, float* dst, const int64_t* idx, int64_t rows,
+                                          int32_t width, int32_t dst_ld, void* stream) {
+  if (!src || !dst || !idx || rows <= 0 || width <= 0 || dst_ld < width)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_gather_rows_padded: bad args");
+  hipLaunchKernelGGL(gather_rows_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, LGX_STREAM(stream),
+                     src, dst, idx, rows, width, dst_ld);
+  return lgx_hip_status("lgx_ppo_gather_rows_padded");
+}

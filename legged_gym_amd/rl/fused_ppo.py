@@ -2,12 +2,16 @@
 forward/backward over flat parameter/gradient buffers — no autograd graph, no per-op launches.
 
 Per minibatch (M rows), on one stream, no host synchronisation:
-  gather obs rows (lgx_ppo_gather_rows)
-  hidden layers: library GEMM (mm for layer 1, bmm over {actor, critic} after) + lgx_bias_act
+  weight preparation (lgx_copy2d: zero-padded layer-1 weights, transposed hidden weights)
+  gather obs rows (lgx_ppo_gather_rows_padded, K padded to a multiple of 16)
+  hidden layers: lgx_gemm_nt with the bias + ELU epilogue, {actor, critic} batched in one launch
   heads: mm; lgx_ppo_loss = log-prob / ratio / clipped surrogate / clipped value loss / entropy
          / KL and the analytic gradient w.r.t. mu, value, std, head biases
   lgx_ppo_adapt_lr (device-side adaptive schedule; data-parallel: KL rides in the gradient all-reduce)
-  backward: lgx_head_bwd, then per layer split-K bmm for dW, bmm for dA, lgx_elu_bwd_colsum
+  backward: lgx_head_bwd, then per layer split-K bmm for dW, lgx_gemm_nt for dA with the ELU'
+            + bias-gradient column-sum epilogue
+  (hidden widths that are not multiples of 128, or LGX_PPO_GEMM=lib: library GEMMs through torch
+   + lgx_bias_act / lgx_elu_bwd_colsum instead of lgx_gemm_nt)
   lgx_reduce_slices: all split-K and bias partials -> flat gradient (one launch)
   [ONE all-reduce over RCCL when data-parallel: flat gradient + the minibatch KL]
   lgx_adam_clip: clip_grad_norm_(max_grad_norm) + Adam on the flat buffers
@@ -176,6 +180,13 @@ class FusedPPOUpdate:
         self.std_off = self.off[id(ac.std)]
         params = list(ac.parameters())
         self.optimizer = FlatAdam(params, self.flat_p, self.flat_g, ppo.learning_rate)
+        import os
+        # LGX_PPO_GEMM: "auto" (default) = lgx_gemm_nt where it measured faster than library GEMM +
+        # epilogue pass on MI355X (layer-1 forward, every backward dA); "lgx" = every hidden-layer
+        # GEMM; "lib" = none
+        mode = os.environ.get("LGX_PPO_GEMM", "auto")
+        self.lgx_gemm = all(hk % abi.GEMM_TILE_N == 0 for hk in self.hidden) and mode != "lib"
+        self.lgx_fwd_layers = set(range(self.L)) if mode == "lgx" else {0}
         self.norm_parts = torch.zeros(256, device=self.dev)
         self.stats = torch.zeros(3, device=self.dev)
         self.M = None
@@ -187,8 +198,17 @@ class FusedPPOUpdate:
         dev, h, A = self.dev, self.hidden, self.A
         self.M = M
         self.S = self.SPLITS if M % self.SPLITS == 0 else 1
-        self.X = torch.empty(M, self.num_obs, device=dev)
-        self.Xc = torch.empty(M, self.num_cobs, device=dev) if self._separate_critic_obs() else None
+        sep = self._separate_critic_obs()
+        if self.lgx_gemm:   # K of layer 1 padded to the GEMM's K step with zero columns
+            ks = abi.GEMM_K_STEP
+            self.Kp, self.Kcp = -(-self.num_obs // ks) * ks, -(-self.num_cobs // ks) * ks
+            self.Xp = torch.zeros(M, self.Kp, device=dev)
+            self.X = self.Xp[:, :self.num_obs]
+            self.Xcp = torch.zeros(M, self.Kcp, device=dev) if sep else None
+            self.Xc = self.Xcp[:, :self.num_cobs] if sep else None
+        else:
+            self.X = torch.empty(M, self.num_obs, device=dev)
+            self.Xc = torch.empty(M, self.num_cobs, device=dev) if sep else None
         self.Y = [torch.empty(2, M, hk, device=dev) for hk in h]
         self.D = [torch.empty(2, M, hk, device=dev) for hk in h[:-1]]
         self.MU = torch.empty(M, A, device=dev)
@@ -200,8 +220,81 @@ class FusedPPOUpdate:
                  [torch.empty(2 * S, h[k], h[k - 1], device=dev) for k in range(1, self.L)]
         self.loss_parts = torch.empty(int(self.lib.lgx_ppo_loss_partials_floats(M, A)), device=dev)
         self.head_parts = torch.empty(int(self.lib.lgx_head_bwd_partials_floats(M, A, h[-1])), device=dev)
-        self.col_parts = [torch.empty(int(self.lib.lgx_colsum_partials_floats(M, hk, 2)), device=dev) for hk in h[:-1]]
+        if self.lgx_gemm:
+            self.col_parts = [torch.empty(int(self.lib.lgx_gemm_partials_floats(M, hk, 2)), device=dev)
+                              for hk in h[:-1]]
+            self._build_gemm_plan()
+        else:
+            self.col_parts = [torch.empty(int(self.lib.lgx_colsum_partials_floats(M, hk, 2)), device=dev)
+                              for hk in h[:-1]]
         self._build_reduce_jobs()
+
+    def _build_gemm_plan(self):
+        """Fixed argument blocks of every lgx_gemm_nt / lgx_copy2d launch of a minibatch (the
+        buffers do not move, so a minibatch issues the prepared structs)."""
+        M, h, L, dev = self.M, self.hidden, self.L, self.dev
+        fp = self.flat_p
+        f4 = 4
+        shared = self.Xcp is None and self.num_obs == self.num_cobs
+        copies = []
+
+        def copy(src_ptr, dst, rows, cols, batch, transpose, src_ld, dst_ld):
+            j = abi.LgxCopy2dJob()
+            j.src, j.dst = src_ptr, dst.data_ptr()
+            j.src_ld, j.src_bs = src_ld, rows * cols
+            j.dst_ld, j.dst_bs = dst_ld, (cols if transpose else rows) * dst_ld
+            j.rows, j.cols, j.batch, j.transpose = rows, cols, batch, int(transpose)
+            copies.append(j)
+        w1 = fp.data_ptr() + f4 * self.Wg[0]
+        if shared:
+            self.W1p = torch.zeros(2, h[0], self.Kp, device=dev)
+            copy(w1, self.W1p, h[0], self.num_obs, 2, False, self.num_obs, self.Kp)
+        else:
+            self.W1p = torch.zeros(h[0], self.Kp, device=dev)
+            self.W1pc = torch.zeros(h[0], self.Kcp, device=dev)
+            copy(w1, self.W1p, h[0], self.num_obs, 1, False, self.num_obs, self.Kp)
+            copy(w1 + f4 * h[0] * self.num_obs, self.W1pc, h[0], self.num_cobs, 1, False, self.num_cobs, self.Kcp)
+        self.WT = [None]
+        for k in range(1, L):   # W_k [2, h_k, h_{k-1}] -> W_k^T [2, h_{k-1}, h_k]
+            wt = torch.empty(2, h[k - 1], h[k], device=dev)
+            copy(fp.data_ptr() + f4 * self.Wg[k], wt, h[k], h[k - 1], 2, True, h[k - 1], h[k])
+            self.WT.append(wt)
+        if len(copies) > abi.MAX_REDUCE_JOBS:
+            raise RuntimeError("too many weight-preparation jobs for one launch")
+        self.copy_jobs = (abi.LgxCopy2dJob * len(copies))(*copies)
+
+        def gemm(A, lda, sa, B, ldb, sb, C, N, K, batch, epi, bias=None, Y=None, parts=None):
+            g = abi.LgxGemmArgs()
+            g.M, g.N, g.K, g.batch, g.epi = M, N, K, batch, epi
+            g.A, g.lda, g.sa = A, lda, sa
+            g.B, g.ldb, g.sb = B, ldb, sb
+            g.C, g.ldc, g.sc = C.data_ptr(), N, M * N
+            g.bias = bias
+            g.Y = Y.data_ptr() if Y is not None else None
+            g.partials = parts.data_ptr() if parts is not None else None
+            return g
+        fwd = [[]]
+        b0 = fp.data_ptr() + f4 * self.bo[0]
+        if shared:   # one input for both networks: batch stride 0
+            fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, self.W1p.data_ptr(), self.Kp, h[0] * self.Kp, self.Y[0],
+                            h[0], self.Kp, 2, abi.GEMM_BIAS_ELU, bias=b0))
+        else:
+            fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, self.W1p.data_ptr(), self.Kp, 0, self.Y[0][0], h[0],
+                               self.Kp, 1, abi.GEMM_BIAS_ELU, bias=b0))
+            xc = self.Xcp if self.Xcp is not None else self.Xp
+            fwd[0].append(gemm(xc.data_ptr(), self.Kcp, 0, self.W1pc.data_ptr(), self.Kcp, 0, self.Y[0][1], h[0],
+                            self.Kcp, 1, abi.GEMM_BIAS_ELU, bias=b0 + f4 * h[0]))
+        for k in range(1, L):
+            fwd.append(gemm(self.Y[k - 1].data_ptr(), h[k - 1], M * h[k - 1], fp.data_ptr() + f4 * self.Wg[k], h[k - 1],
+                            h[k] * h[k - 1], self.Y[k], h[k], h[k - 1], 2, abi.GEMM_BIAS_ELU,
+                            bias=fp.data_ptr() + f4 * self.bo[k]))
+        self.gemm_fwd = fwd
+        bwd = {}
+        for k in range(L - 1, 0, -1):   # dZ_{k-1} = (dZ_k W_k) * elu'(Y_{k-1}); dZ_{L-1} lives in Y[L-1]
+            dz = self.Y[L - 1] if k == L - 1 else self.D[k]
+            bwd[k] = gemm(dz.data_ptr(), h[k], M * h[k], self.WT[k].data_ptr(), h[k], h[k - 1] * h[k], self.D[k - 1],
+                          h[k - 1], h[k], 2, abi.GEMM_DELU_COLSUM, Y=self.Y[k - 1], parts=self.col_parts[k - 1])
+        self.gemm_bwd = bwd
 
     def _separate_critic_obs(self):
         st = self.ppo.storage
@@ -307,24 +400,46 @@ class FusedPPOUpdate:
         lib, chk = self.lib, self.check
         ppo = self.ppo
         M, S, h, L, A = self.M, self.S, self.hidden, self.L, self.A
-        chk(lib.lgx_ppo_gather_rows(_vp(obs), _vp(self.X), _vp(idx), M, obs.shape[1], stream), "gather")
+        fused = self.lgx_gemm
         Xc = self.X
-        if cobs is not None:
-            chk(lib.lgx_ppo_gather_rows(_vp(cobs), _vp(self.Xc), _vp(idx), M, cobs.shape[1], stream), "gather")
-            Xc = self.Xc
+        if fused:
+            chk(lib.lgx_copy2d(self.copy_jobs, len(self.copy_jobs), stream), "copy2d")
+            chk(lib.lgx_ppo_gather_rows_padded(_vp(obs), _vp(self.Xp), _vp(idx), M, obs.shape[1], self.Kp, stream),
+                "gather")
+            if cobs is not None:
+                chk(lib.lgx_ppo_gather_rows_padded(_vp(cobs), _vp(self.Xcp), _vp(idx), M, cobs.shape[1], self.Kcp,
+                                                   stream), "gather")
+                Xc = self.Xc
+        else:
+            chk(lib.lgx_ppo_gather_rows(_vp(obs), _vp(self.X), _vp(idx), M, obs.shape[1], stream), "gather")
+            if cobs is not None:
+                chk(lib.lgx_ppo_gather_rows(_vp(cobs), _vp(self.Xc), _vp(idx), M, cobs.shape[1], stream), "gather")
+                Xc = self.Xc
         # ---- forward
         wa, wc = self.W[0]
-        if cobs is None:   # shared input: one batched GEMM over {actor, critic} with a stride-0 input
-            torch.bmm(self.X.unsqueeze(0).expand(2, M, self.num_obs), self.W1s.transpose(1, 2), out=self.Y[0])
-        else:
-            torch.mm(self.X, wa.t(), out=self.Y[0][0])
-            torch.mm(Xc, wc.t(), out=self.Y[0][1])
         fp = self.flat_p
-        chk(lib.lgx_bias_act(_vp(self.Y[0]), C.c_void_p(fp.data_ptr() + 4 * self.bo[0]), M, h[0], 2, 1, stream), "bias")
-        for k in range(1, L):
-            torch.bmm(self.Y[k - 1], self.W[k].transpose(1, 2), out=self.Y[k])
-            chk(lib.lgx_bias_act(_vp(self.Y[k]), C.c_void_p(fp.data_ptr() + 4 * self.bo[k]), M, h[k], 2, 1, stream),
+        if fused:
+            for g in self.gemm_fwd[0]:
+                chk(lib.lgx_gemm_nt(C.byref(g), stream), "gemm_nt")
+            for k in range(1, L):
+                if k in self.lgx_fwd_layers:
+                    chk(lib.lgx_gemm_nt(C.byref(self.gemm_fwd[k]), stream), "gemm_nt")
+                else:
+                    torch.bmm(self.Y[k - 1], self.W[k].transpose(1, 2), out=self.Y[k])
+                    chk(lib.lgx_bias_act(_vp(self.Y[k]), C.c_void_p(fp.data_ptr() + 4 * self.bo[k]), M, h[k], 2, 1,
+                                         stream), "bias")
+        else:
+            if cobs is None:   # shared input: one batched GEMM over {actor, critic} with a stride-0 input
+                torch.bmm(self.X.unsqueeze(0).expand(2, M, self.num_obs), self.W1s.transpose(1, 2), out=self.Y[0])
+            else:
+                torch.mm(self.X, wa.t(), out=self.Y[0][0])
+                torch.mm(Xc, wc.t(), out=self.Y[0][1])
+            chk(lib.lgx_bias_act(_vp(self.Y[0]), C.c_void_p(fp.data_ptr() + 4 * self.bo[0]), M, h[0], 2, 1, stream),
                 "bias")
+            for k in range(1, L):
+                torch.bmm(self.Y[k - 1], self.W[k].transpose(1, 2), out=self.Y[k])
+                chk(lib.lgx_bias_act(_vp(self.Y[k]), C.c_void_p(fp.data_ptr() + 4 * self.bo[k]), M, h[k], 2, 1,
+                                     stream), "bias")
         wha, whc = self.W[L]
         torch.mm(self.Y[L - 1][0], wha.t(), out=self.MU)
         torch.mm(self.Y[L - 1][1], whc.t(), out=self.V)
@@ -343,12 +458,15 @@ class FusedPPOUpdate:
             # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
             torch.bmm(dZ.view(2 * S, M // S, h[k]).transpose(1, 2), self.Y[k - 1].view(2 * S, M // S, h[k - 1]),
                       out=self.P[k])
-            torch.bmm(dZ, self.W[k], out=self.D[k - 1])
-            chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
-                                       _vp(self.col_parts[k - 1]), stream), "elu_bwd")
+            if fused:
+                chk(lib.lgx_gemm_nt(C.byref(self.gemm_bwd[k]), stream), "gemm_nt")
+            else:
+                torch.bmm(dZ, self.W[k], out=self.D[k - 1])
+                chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
+                                           _vp(self.col_parts[k - 1]), stream), "elu_bwd")
             dZ = self.D[k - 1]
-        torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), self.X.view(S, M // S, -1), out=self.P[0][0])
-        torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.view(S, M // S, -1), out=self.P[0][1])
+        torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), self.X.unflatten(0, (S, M // S)), out=self.P[0][0])
+        torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
         chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
         if not apply:
             return

@@ -124,8 +124,22 @@ class LgxPpoStoreArgs(C.Structure):
         (n, C.c_void_p) for n in ("rew", "reset", "time_outs", "st_values", "st_rew", "st_dones")]
 
 
+class LgxGemmArgs(C.Structure):
+    _fields_ = [("M", i64), ("N", i32), ("K", i32), ("batch", i32), ("epi", i32),
+                ("A", C.c_void_p), ("lda", i64), ("sa", i64), ("B", C.c_void_p), ("ldb", i64), ("sb", i64),
+                ("C", C.c_void_p), ("ldc", i64), ("sc", i64), ("bias", C.c_void_p), ("Y", C.c_void_p),
+                ("partials", C.c_void_p)]
+
+
+class LgxCopy2dJob(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("src_ld", i64), ("src_bs", i64), ("dst_ld", i64),
+                ("dst_bs", i64), ("rows", i32), ("cols", i32), ("batch", i32), ("transpose", i32)]
+
+
 PPO_MAX_ACTIONS = 16
 MAX_REDUCE_JOBS = 8
+GEMM_PLAIN, GEMM_BIAS_ELU, GEMM_DELU_COLSUM = 0, 1, 2
+GEMM_TILE_M, GEMM_TILE_N, GEMM_K_STEP = 128, 128, 16
 
 
 def declare(lib, prefix="lgx"):
@@ -170,6 +184,10 @@ def declare(lib, prefix="lgx"):
             "colsum_partials_floats": (i64, [i64, i32, i32]),
             "elu_bwd_colsum": (C.c_int, [vp, vp, i64, i32, i32, vp, vp]),
             "reduce_slices": (C.c_int, [C.POINTER(LgxReduceJob), i32, vp]),
+            "gemm_partials_floats": (i64, [i64, i32, i32]),
+            "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
+            "copy2d": (C.c_int, [C.POINTER(LgxCopy2dJob), i32, vp]),
+            "ppo_gather_rows_padded": (C.c_int, [vp, vp, vp, i64, i32, i32, vp]),
             "adam_clip": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
                                     C.c_float, C.c_float, vp]),
         })
@@ -186,16 +204,17 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
-            "lgx_reduce_slices", "lgx_adam_clip", "lgx_ppo_act", "lgx_ppo_store"]
+            "lgx_reduce_slices", "lgx_adam_clip", "lgx_ppo_act", "lgx_ppo_store",
+            "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded"]
 
 
-def check_layout(sizes_fn, n=8):
+def check_layout(sizes_fn, n=10):
     """Compare the library's sizeof() of every ABI struct with these mirrors (the oracle
     reports the first 3)."""
-    out = (C.c_int64 * 8)()
+    out = (C.c_int64 * 16)()
     sizes_fn(out)
     mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers), C.sizeof(LgxMlpDesc),
             C.sizeof(LgxPpoLossArgs), C.sizeof(LgxReduceJob), C.sizeof(LgxPpoActArgs),
-            C.sizeof(LgxPpoStoreArgs))[:n]
+            C.sizeof(LgxPpoStoreArgs), C.sizeof(LgxGemmArgs), C.sizeof(LgxCopy2dJob))[:n]
     if tuple(out)[:n] != mine:
         raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)[:n]} vs bindings {mine}")

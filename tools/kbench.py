@@ -97,6 +97,69 @@ def mlp_ab():
     os.environ.pop("LGX_MLP_WIDE_RS")
 
 
+def ppo_ab(T=24, N=4096, OBS=235, ACT=12, modes=("lib", "auto", "lgx", "lib", "auto", "lgx"), gemms=True):
+    """A/B the PPO update: hand-written fused GEMMs (lgx_gemm_nt) vs library GEMMs + epilogue
+    passes, one full update (5 epochs x 4 minibatches) at the bench shape; plus per-GEMM timings."""
+    import ctypes as C
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    from legged_gym_amd.rl.ppo import PPO
+    from legged_gym_amd.sim import abi
+    dev = "cuda:0"
+    res = {}
+    for mode in modes:
+        os.environ["LGX_PPO_GEMM"] = mode
+        torch.manual_seed(0)
+        ac = ActorCritic(OBS, OBS, ACT, [512, 256, 128], [512, 256, 128]).to(dev)
+        ppo = PPO(ac, num_learning_epochs=5, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95,
+                  value_loss_coef=1.0, entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0,
+                  schedule="adaptive", desired_kl=0.01, device=dev, use_fused_update=True)
+        ppo.init_storage(N, T, [OBS], [None], [ACT])
+        st = ppo.storage
+        g = torch.Generator(device=dev).manual_seed(3)
+        st.observations.copy_(torch.randn(T, N, OBS, device=dev, generator=g))
+        st.actions.copy_(torch.randn(T, N, ACT, device=dev, generator=g))
+        st.rewards.copy_(torch.randn(T, N, 1, device=dev, generator=g))
+        st.values.copy_(torch.randn(T, N, 1, device=dev, generator=g))
+        st.actions_log_prob.copy_(torch.randn(T, N, 1, device=dev, generator=g) * 0.3 - 17)
+        st.mu.copy_(torch.randn(T, N, ACT, device=dev, generator=g) * 0.1)
+        st.sigma.copy_(torch.rand(T, N, ACT, device=dev, generator=g) * 0.5 + 0.75)
+        st.step = T
+        st.compute_returns(torch.randn(N, 1, device=dev, generator=g), 0.99, 0.95)
+        assert ppo._fused.lgx_gemm == (mode != "lib")
+        ms = timeit(lambda: ppo.update(), iters=5, warm=2)
+        res.setdefault(mode, []).append(ms)
+        print(f"PPO update ({mode} GEMMs): {ms:.2f} ms", flush=True)
+    os.environ.pop("LGX_PPO_GEMM")
+    if gemms:
+        gemm_bench(T * N // 4, torch_too=True)
+
+
+def gemm_bench(M=24576, torch_too=False, iters=20):
+    """lgx_gemm_nt at the PPO-update shapes (and torch bmm without epilogue for reference)."""
+    import ctypes as C
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim import lib as lgxlib
+    dev = "cuda:0"
+    lib = lgxlib.load()
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for (n_, k_, epi) in ((512, 240, 1), (256, 512, 1), (128, 256, 1), (256, 128, 2), (512, 256, 2)):
+        A = torch.randn(2, M, k_, device=dev)
+        B = torch.randn(2, n_, k_, device=dev)
+        Cc = torch.empty(2, M, n_, device=dev)
+        Y = torch.randn(2, M, n_, device=dev)
+        bias = torch.randn(2, n_, device=dev)
+        parts = torch.empty(lib.lgx_gemm_partials_floats(M, n_, 2), device=dev)
+        a = abi.LgxGemmArgs()
+        a.M, a.N, a.K, a.batch, a.epi = M, n_, k_, 2, epi
+        a.A, a.lda, a.sa, a.B, a.ldb, a.sb = A.data_ptr(), k_, M * k_, B.data_ptr(), k_, n_ * k_
+        a.C, a.ldc, a.sc, a.bias, a.Y, a.partials = Cc.data_ptr(), n_, M * n_, bias.data_ptr(), Y.data_ptr(), parts.data_ptr()
+        t1 = timeit(lambda: lib.lgx_gemm_nt(C.byref(a), stream), iters=iters)
+        t2 = timeit(lambda: torch.bmm(A, B.transpose(1, 2), out=Cc), iters=iters) if torch_too else float("nan")
+        f = 2.0 * 2 * M * n_ * k_
+        print(f"gemm M={M} N={n_} K={k_} epi={epi}: lgx {t1*1e3:.1f} us {f/t1/1e9:.1f} TF/s | torch bmm (no epilogue) "
+              f"{t2*1e3:.1f} us {f/t2/1e9:.1f} TF/s", flush=True)
+
+
 def phys_run(task="go1_rough", n=4096, steps=10):
     """Short env-step loop for PMC collection (rocprofv3 --pmc): 10 env steps after reset."""
     from oracle_backend import make_env
@@ -120,5 +183,12 @@ if __name__ == "__main__":
         mlp_ab()
     if "physrun" in what:
         phys_run()
+    if "ppo" in what:
+        ppo_ab()
+    for m in ("lib", "auto", "lgx"):
+        if f"ppo_{m}" in what:
+            ppo_ab(modes=(m,), gemms=False)
+    if "gemm" in what:
+        gemm_bench()
 
 
