@@ -7,6 +7,24 @@
 
 #define LGX_DEV __device__ __forceinline__
 
+// Phase timing of one wave (block 0, thread 0) for kernel tuning: build with
+// EXTRA=-DLGX_PHASE_CLOCK (tools/phase_clock.sh); compiled out of the product library.
+#ifdef LGX_PHASE_CLOCK
+#include <stdio.h>
+#define LGX_CLK_DECL(n) uint64_t lgx_clk_acc[n] = {}; uint64_t lgx_clk_t = clock64();
+#define LGX_CLK(i) do { const uint64_t _t = clock64(); lgx_clk_acc[i] += _t - lgx_clk_t; lgx_clk_t = _t; } while (0)
+#define LGX_CLK_PRINT(name, n)                                                                        \
+  if (blockIdx.x == 0 && threadIdx.x == 0) {                                                          \
+    printf("%s cycles:", name);                                                                       \
+    for (int _i = 0; _i < n; ++_i) printf(" %d=%llu", _i, (unsigned long long)lgx_clk_acc[_i]);        \
+    printf("\n");                                                                                     \
+  }
+#else
+#define LGX_CLK_DECL(n)
+#define LGX_CLK(i) do { } while (0)
+#define LGX_CLK_PRINT(name, n)
+#endif
+
 // ---------------------------------------------------------------- Philox4x32-10 uniforms
 // Same stream as the oracle's lgxo_uniform: counter (env, slot/4, step, tag), key = seed.
 // Philox-4x32-10 block of draw slots (4q .. 4q+3): one counter per 4 consecutive slots

@@ -209,11 +209,34 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   const int tid = threadIdx.x;
   const Draws D{P, draws, LGX_DRAW_NOISE + nobs};
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
+  LGX_CLK_DECL(6)
   __shared__ float part[LGX_ENV_BLOCK][LGX_PARTIAL_STRIDE];
   // what phase C (observations) reads, kept in LDS: heights (phase A), base-frame velocities,
   // gravity, commands and root z (phase B, post-reset); dof state / actions are in srow below
   __shared__ float sheight[LGX_ENV_BLOCK][LGX_MAX_HEIGHT_POINTS];
   __shared__ float sbase[LGX_ENV_BLOCK][14];   // blv 3, bav 3, pg 3, cmd 4, root z
+  // per-observation-index constants (scale, offset, noise scale) and the scan pattern, staged once
+  // per workgroup: phases A and C index them per lane, which from global memory is a dependent
+  // vector load per entry
+  __shared__ float obs_mul[LGX_MAX_OBS], obs_sub[LGX_MAX_OBS], obs_nsc[LGX_MAX_OBS];
+  __shared__ float2 scan_pt[LGX_MAX_HEIGHT_POINTS];
+  for (int i = tid; i < nobs; i += ENV_THREADS) {
+    float mul, sub = 0.f;
+    if (i < 3) mul = P->obs_scale_lin_vel;
+    else if (i < 6) mul = P->obs_scale_ang_vel;
+    else if (i < 9) mul = 1.f;
+    else if (i < 12) mul = i < 11 ? P->obs_scale_lin_vel : P->obs_scale_ang_vel;
+    else if (i < 24) { mul = P->obs_scale_dof_pos; sub = P->default_dof_pos[i - 12]; }
+    else if (i < 36) mul = P->obs_scale_dof_vel;
+    else if (i < 48) mul = 1.f;
+    else mul = P->obs_scale_height;
+    obs_mul[i] = mul;
+    obs_sub[i] = sub;
+    obs_nsc[i] = P->add_noise ? P->noise_scale_vec[i] : 0.f;
+  }
+  if (P->measure_heights)
+    for (int i = tid; i < P->num_height_points; i += ENV_THREADS)
+      scan_pt[i] = make_float2(P->height_points[i][0], P->height_points[i][1]);
 
   // ---- phase A: height scan (legged_robot.py:818-854), pre-reset base pose.  The per-env yaw
   // rotation and base xy are staged in LDS; the (env, point) loop is unrolled so several
@@ -242,7 +265,8 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
           sheight[le][i] = 0.f;
         } else {
           const float4 b = base_xy_yaw[le];
-          f3 o = quat_apply(0.f, 0.f, b.z, b.w, mk3(P->height_points[i][0], P->height_points[i][1], 0.f));
+          const float2 hp = scan_pt[i];
+          f3 o = quat_apply(0.f, 0.f, b.z, b.w, mk3(hp.x, hp.y, 0.f));
           float x = o.x + b.x + P->border_size, y = o.y + b.y + P->border_size;  // (p + root) + border, as :833-834
           int64_t px = (int64_t)(x / P->horizontal_scale), py = (int64_t)(y / P->horizontal_scale);
           px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
@@ -257,6 +281,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
     __syncthreads();
   }
 
+  LGX_CLK(0);
   // ---- stage the per-env rows the reward terms read (coalesced, all lanes) into LDS: the
   // term loop below re-reads them many times from a single lane per env
   constexpr int SROW = 24 + 12 + LGX_MAX_BODIES * 3 + 12 + 12 + 12;  // ds tq cf act la ldv
@@ -287,6 +312,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   }
   __syncthreads();
 
+  LGX_CLK(1);
   // ---- phase B: one env per lane
   if (tid < LGX_ENV_BLOCK) {
     const int e = e0 + tid;
@@ -370,6 +396,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
       o3[0] = v.pg.x; o3[1] = v.pg.y; o3[2] = v.pg.z;
     }
   }
+  LGX_CLK(2);
   block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
   __syncthreads();
   for (int idx = tid; idx < T * LGX_ENV_BLOCK; idx += ENV_THREADS) {   // staged rows back
@@ -379,6 +406,7 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   if (tid < LGX_ENV_BLOCK * 4 && e0 + (tid >> 2) < N)
     B.feet_air_time[(int64_t)(e0 + (tid >> 2)) * 4 + (tid & 3)] = sfat[tid >> 2][tid & 3];
 
+  LGX_CLK(3);
   // ---- phase C: observations (:214-231) + noise + clip (:103-104); a lane owns 4 consecutive
   // entries of a row, whose noise is one Philox block (LGX_DRAW_NOISE is a multiple of 4)
   const int nq = (nobs + 3) >> 2;
@@ -396,19 +424,18 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
       if (i >= nobs) break;
       const float* sb = sbase[le];
       const float* sr = srow[le];
-      float o;
-      if (i < 3) o = sb[i] * P->obs_scale_lin_vel;
-      else if (i < 6) o = sb[i] * P->obs_scale_ang_vel;
-      else if (i < 9) o = sb[i];
-      else if (i < 12) o = sb[i] * (i < 11 ? P->obs_scale_lin_vel : P->obs_scale_ang_vel);
-      else if (i < 24) o = (sr[2 * (i - 12)] - P->default_dof_pos[i - 12]) * P->obs_scale_dof_pos;
-      else if (i < 36) o = sr[2 * (i - 24) + 1] * P->obs_scale_dof_vel;
-      else if (i < 48) o = sr[36 + LGX_MAX_BODIES * 3 + i - 36];
-      else o = clampf(sb[13] - 0.5f - sheight[le][i - 48], -1.f, 1.f) * P->obs_scale_height;
-      if (P->add_noise) o += (2.f * nz[u] - 1.f) * P->noise_scale_vec[i];
+      float v;   // source value (reference order, legged_robot.py:216-226)
+      if (i < 12) v = sb[i];
+      else if (i < 24) v = sr[2 * (i - 12)];
+      else if (i < 36) v = sr[2 * (i - 24) + 1];
+      else if (i < 48) v = sr[36 + LGX_MAX_BODIES * 3 + i - 36];
+      else v = clampf(sb[13] - 0.5f - sheight[le][i - 48], -1.f, 1.f);
+      float o = (v - obs_sub[i]) * obs_mul[i];
+      if (P->add_noise) o += (2.f * nz[u] - 1.f) * obs_nsc[i];
       B.obs[(int64_t)e * nobs + i] = clampf(o, -P->clip_obs, P->clip_obs);
     }
   }
+  LGX_CLK(4);
   // ---- last_* copies (:136-138), post-reset values
   for (int idx = tid; idx < LGX_ENV_BLOCK * 12; idx += ENV_THREADS) {
     int e = e0 + idx / 12, j = idx % 12;
@@ -420,6 +447,8 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
     int e = e0 + tid;
     for (int i = 0; i < 6; ++i) B.last_root_vel[(int64_t)e * 6 + i] = B.root_states[(int64_t)e * 13 + 7 + i];
   }
+  LGX_CLK(5);
+  LGX_CLK_PRINT("post_physics", 6)
 }
 
 // reset_idx on an explicit env list (BaseTask.reset, base_task.py:111-115)

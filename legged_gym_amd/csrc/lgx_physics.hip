@@ -255,6 +255,11 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   constexpr int ENVS = 16;                          // envs per workgroup
   __shared__ lgx_dev_model smodel;                  // model tables staged once per workgroup
   __shared__ float4 slot_state[SLOTS][PHYS_BLOCK];  // per own candidate: status, fslide.xyz (lane-minor: no bank conflicts)
+  // contact geometry of the candidates penetrating in pass 0 (positions do not change within a
+  // substep): pass 0's classification, pass 1 and the force report read it instead of redoing
+  // the frame transform and the terrain query
+  __shared__ float4 geo_p[SLOTS][PHYS_BLOCK];      // contact point Pc (base-origin frame), depth
+  __shared__ float4 geo_n[SLOTS][PHYS_BLOCK];      // terrain normal, candidate index
   __shared__ float hist_lds[ENVS * 4 * HIST_STRIDE];  // Go1 actuator history per (env, leg)
   // Per-leg / per-env quantities that every lane of the leg / env holds identically are kept
   // in LDS instead of VGPRs (all those lanes store the same values, so no cross-lane ordering
@@ -285,6 +290,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   const bool valid = e < N;
   const int ec = valid ? e : N - 1;  // inactive lanes compute on a clamped env, never store
 
+  LGX_CLK_DECL(8)
   const float dt = M->sim_dt;
   // ---- load state
   const float* rs = B.root_states + (int64_t)ec * 13;
@@ -354,6 +360,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   f3 cf_base = mk3(0, 0, 0);
   float tq[3] = {0.f, 0.f, 0.f};
 
+  LGX_CLK(6);
   for (int s = 0; s < nsub; ++s) {
     // ---- Go1 actuator-net history (go1.py:79-98), model_ins per substep
     if (use_hist) {
@@ -391,6 +398,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         tex[k] = clampf(t, -P->torque_limits[j], P->torque_limits[j]);
       }
     }
+    LGX_CLK(0);
     // ---- kinematics
     m33 R0 = quat_to_mat(qx, qy, qz, qw);
     m33 Rb[3];
@@ -492,6 +500,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         rl0[k] = s2 + dqv[k] - dt * Cl[k];
       }
     }
+    LGX_CLK(1);
     // ---- drives and limits
     float Dimp[3] = {0.f, 0.f, 0.f};
     bool impl[3] = {false, false, false};
@@ -527,6 +536,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       lsys[24 + i] = rb0[i];
     }
     lsys[30] = rl0[0]; lsys[31] = rl0[1]; lsys[32] = rl0[2];
+    LGX_CLK(2);
     // ---- contacts: two passes (pass 0 implicit stick, pass 1 with slide / drop decisions)
     const float kn = M->contact_k, cn = M->contact_c, ct = M->friction_c;
     const float wn = dt * (cn + dt * kn);
@@ -544,23 +554,38 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
         if (c >= npts) break;
         float4 st = slot_state[sl][tid];
-        if (pass == 1 && st.x == 0.f) continue;  // separated in pass 0: same geometry, no contact
-        int pi = DM->lane_pts[leg][c];
-        int db = M->point_dyn[pi];
-        int k = db == 0 ? -1 : (db - 1) % 3;
-        const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;   // body rotation (+ origin) in LDS
-        m33 R;
+        f3 Pc, n;
+        float depth;
+        int k;
+        if (pass == 0) {
+          const int pi = DM->lane_pts[leg][c];
+          const int db = M->point_dyn[pi];
+          k = db == 0 ? -1 : (db - 1) % 3;
+          const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;   // body rotation (+ origin) in LDS
+          m33 R;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
-        f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
-        f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
-        f3 n;
-        float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n, patch, pi0, pj0);
-        float rad = M->point_radius[pi];
-        float depth = (h - (Pp.z + pos.z)) * n.z + rad;
-        if (pass == 0) { st.x = depth > 0.f ? 1.f : 0.f; slot_state[sl][tid] = st; }
-        if (depth <= 0.f || st.x == 0.f) continue;
-        f3 Pc = Pp - rad * n;
+          for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
+          f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
+          f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
+          float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n, patch,
+                                  pi0, pj0);
+          float rad = M->point_radius[pi];
+          depth = (h - (Pp.z + pos.z)) * n.z + rad;
+          st.x = depth > 0.f ? 1.f : 0.f;
+          slot_state[sl][tid] = st;
+          if (depth <= 0.f) continue;
+          Pc = Pp - rad * n;
+          geo_p[sl][tid] = make_float4(Pc.x, Pc.y, Pc.z, depth);
+          geo_n[sl][tid] = make_float4(n.x, n.y, n.z, (float)pi);
+        } else {
+          if (st.x == 0.f) continue;  // separated in pass 0: same geometry, no contact
+          const float4 gp = geo_p[sl][tid], gn = geo_n[sl][tid];
+          Pc = mk3(gp.x, gp.y, gp.z);
+          depth = gp.w;
+          n = mk3(gn.x, gn.y, gn.z);
+          const int db = M->point_dyn[(int)gn.w];
+          k = db == 0 ? -1 : (db - 1) % 3;
+        }
         float wt = (pass == 0 || st.x == 1.f) ? dt * ct : 0.f;
         f3 f = (dt * kn * depth) * n;
         if (pass == 1 && st.x == 2.f) f = f + dt * mk3(st.y, st.z, st.w);
@@ -578,7 +603,9 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       }
 #pragma unroll
       for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + lsys[30 + k];
+      LGX_CLK(3);
       arrow_solve(L, ecom, ecom + 21, lane0, xb, xl);
+      LGX_CLK(4);
       // contact status (after pass 0) / reported forces (after pass 1, last substep)
       const bool report = pass == 1 && s == nsub - 1;
       if (pass == 0 || report) {
@@ -591,20 +618,12 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
           if (c >= npts) break;
           float4 st = slot_state[sl][tid];
           if (st.x == 0.f) continue;
-          int pi = DM->lane_pts[leg][c];
-          int db = M->point_dyn[pi];
-          int k = db == 0 ? -1 : (db - 1) % 3;
-          const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;
-          m33 R;
-#pragma unroll
-          for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
-          f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
-          f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
-          f3 n;
-          float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n, patch, pi0, pj0);
-          float rad = M->point_radius[pi];
-          float depth = (h - (Pp.z + pos.z)) * n.z + rad;
-          f3 Pc = Pp - rad * n;
+          const float4 gp = geo_p[sl][tid], gn = geo_n[sl][tid];
+          const f3 Pc = mk3(gp.x, gp.y, gp.z), n = mk3(gn.x, gn.y, gn.z);
+          const float depth = gp.w;
+          const int pi = (int)gn.w;
+          const int db = M->point_dyn[pi];
+          const int k = db == 0 ? -1 : (db - 1) % 3;
           sv V = db == 0 ? Vb : sel3(k, Vl[0], Vl[1], Vl[2]);
           f3 vp = V.l + cross(V.a, Pc);
           float vn = dot(vp, n);
@@ -634,6 +653,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
           }
         }
       }
+      LGX_CLK(5);  // classification / reporting
     }
     // ---- joint outputs and integration
     float qdn[3] = {xl.x, xl.y, xl.z};
@@ -705,6 +725,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     ro[7] = vlin.x; ro[8] = vlin.y; ro[9] = vlin.z;
     ro[10] = wang.x; ro[11] = wang.y; ro[12] = wang.z;
   }
+  LGX_CLK(7);
+  LGX_CLK_PRINT("physics", 8)
 }
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,

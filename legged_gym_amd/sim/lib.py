@@ -10,6 +10,8 @@ from . import abi
 
 _LIB = None
 LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "liblgx.so")
+# an instrumented build of the same sources (tools/phase_clock.sh) may be selected for tuning runs
+LIB_PATH = os.environ.get("LGX_LIB_PATH", LIB_PATH)
 
 
 class LgxError(RuntimeError):
