@@ -190,7 +190,7 @@ typedef struct lgx_buffers {
   float* act_dvel;           /* [decimation,N,12] actuator-net outputs (dVel, go1.py:100-105) */
   float* extras;             /* [T + 2]: episode means per term, terrain_level, reset count */
   uint8_t* extras_time_outs; /* [N] time_outs as last published (stale semantics) */
-  float* scratch;            /* [lgx_scratch_floats(N)] reduction partials */
+  float* scratch;            /* [lgx_scratch_floats(N)] reduction partials + completion ticket */
 } lgx_buffers;
 
 typedef struct lgx_sim lgx_sim;

@@ -170,6 +170,11 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   }
   rc = hip_check(hipMemcpy(s->d_model, &dm, sizeof dm, hipMemcpyHostToDevice), "hipMemcpy(model)");
   if (!rc) rc = hip_check(hipMemcpy(s->d_params, params, sizeof *params, hipMemcpyHostToDevice), "hipMemcpy(params)");
+  // the post-physics completion ticket (after the block partials in scratch) starts at zero
+  if (!rc) {
+    const int64_t blocks = (params->num_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
+    rc = hip_check(hipMemset(bufs->scratch + blocks * LGX_PARTIAL_STRIDE, 0, sizeof(unsigned int)), "hipMemset(ticket)");
+  }
   if (rc) { (void)hipFree(s->d_model); (void)hipFree(s->d_params); delete s; return rc; }
   *out = s;
   return 0;
@@ -215,9 +220,12 @@ static int join_aux(lgx_sim* s, hipStream_t st) {
   return hip_check(hipStreamWaitEvent(st, s->aux_done, 0), "hipStreamWaitEvent(aux)");
 }
 
-static int aux_enabled() {
-  const char* e = getenv("LGX_ACT_OVERLAP");  // A/B switch: 0 = actuator net on the caller's stream
-  return e ? atoi(e) : 1;
+// Where the Go1 actuator net runs (A/B switch LGX_ACT_OVERLAP): 2 (default) = on workgroups of
+// its own inside the post-physics launch, 1 = its own launch on an auxiliary stream, 0 = its own
+// launch on the caller's stream.
+static int act_mode() {
+  const char* e = getenv("LGX_ACT_OVERLAP");
+  return e ? atoi(e) : 2;
 }
 
 int lgx_sync_aux(lgx_sim* s, void* stream) {
@@ -257,10 +265,24 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
   rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, actions, st),
                     "lgx_step: physics launch");
   if (rc) return rc;
-  if (p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel) {
+  const bool act_net = p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel;
+  const int mode = act_mode();
+  if (act_net && mode == 2) {
+    // UniNet on every (substep, env, leg) row of this step's model_ins, inside the post-physics
+    // launch (the next physics launch, stream-ordered after it, rewrites model_ins)
+    arm(s, 2, sample);
+    rc = launch_check(lgx_launch_post_physics_act(s->d_params, s->bufs, p.num_envs, step, s->draws, s->extras_snapshot,
+                                                  s->bufs.model_ins, s->bufs.act_dvel,
+                                                  (int64_t)p.decimation * p.num_envs * 4, s->bufs.act_net_w,
+                                                  s->bufs.act_net_scale, st),
+                      "lgx_step: post-physics + actuator launch");
+    lgx_timing = lgx_timing_slot{};
+    return rc;
+  }
+  if (act_net) {
     // UniNet on every (substep, env, leg) row of this step's model_ins; result = dVel
     hipStream_t ast = st;
-    if (aux_enabled()) {
+    if (mode == 1) {
       if (!s->aux) {
         rc = hip_check(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking), "hipStreamCreate(aux)");
         if (!rc) rc = hip_check(hipEventCreateWithFlags(&s->aux_in, hipEventDisableTiming), "hipEventCreate(aux)");

@@ -8,10 +8,13 @@
 //   A  (all lanes) height scan: (env, point) pairs, coalesced int16 gathers
 //   B  (one lane per env) scalar env logic: scalar logic, rewards, reset
 //   C  (all lanes) observation rows: (env, obs index) pairs, coalesced stores
-// Extras (episode means over reset envs) are reduced per block in LDS, then by a one-block
-// finalize kernel in fixed order (bitwise reproducible).
+// Extras (episode means over reset envs) are reduced per block in LDS, then by the workgroup
+// that finishes last, in fixed order (bitwise reproducible).
+#include <algorithm>
+
 #include "lgx_device.h"
 #include "lgx_internal.h"
+#include "lgx_actuator_ws.h"
 
 #define ENV_THREADS (16 * LGX_ENV_BLOCK)
 static_assert(LGX_DRAW_NOISE % 4 == 0, "observation noise slots must start a Philox block");
@@ -199,13 +202,74 @@ LGX_DEV void block_partials(float (*lds)[LGX_PARTIAL_STRIDE], int nrows, float* 
   }
 }
 
-}  // namespace
+// extras finalize: deterministic sum of the block partials; publish only if >= 1 env reset.
+// level_scan: sum terrain levels over all envs here (reset_idx path) instead of partials.
+// Runs on one workgroup of nt threads (a multiple of 64).
+LGX_DEV void extras_finalize_body(const lgx_env_params* __restrict__ P, const lgx_buffers& B, int32_t nblocks,
+                                  int32_t level_scan, float* __restrict__ snapshot, int nt) {
+  const int N = P->num_envs;
+  const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
+  __shared__ float sums[LGX_PARTIAL_STRIDE];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = nt >> 6;
+  // wave w reduces rows w, w+nw, ...: lanes take blocks lane, lane+64, ... then a fixed-order
+  // butterfly (deterministic, no atomics)
+  const int rows = T + 2;
+  for (int r = wave; r < rows; r += nw) {
+    float s = 0.f;
+    if (r == T + 1 && level_scan) {
+      if (P->curriculum)
+        for (int e = lane; e < N; e += 64) s += (float)B.terrain_levels[e];
+    } else {
+      for (int b = lane; b < nblocks; b += 64) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + r];
+    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
+    if (lane == 0) sums[r] = s;
+  }
+  __syncthreads();
+  const float count = sums[T];
+  const bool update = count > 0.f;  // else the reference keeps stale extras (legged_robot.py:160-161)
+  if (t < rows) {
+    float v = B.extras[t];
+    if (update) {
+      if (t < T) v = (sums[t] / count) / P->max_episode_length_s;
+      else if (t == T + 1) v = count;
+      else if (P->curriculum) v = sums[T + 1] / (float)N;
+      B.extras[t] = v;
+    }
+    if (snapshot) snapshot[t] = v;  // this step's published copy (lgx_rebind_extras)
+  }
+  if (!update) return;
+  if (P->send_timeouts)
+    for (int e = t; e < N; e += nt) B.extras_time_outs[e] = B.time_out[e];
+}
 
-__global__ void __launch_bounds__(ENV_THREADS)
-lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int64_t step, const float* draws) {
+// Completion ticket of the post-physics workgroups (a counter after the block partials in
+// scratch, zero between launches): the workgroup that takes the last ticket runs the extras
+// finalize, so the reduction needs no second launch.  Release: every thread's partial /
+// time_out / level writes are fenced at device scope before the ticket; acquire: the last
+// workgroup fences again before reading them (the L2s of the 8 XCDs are not coherent).
+LGX_DEV bool take_last_ticket(const lgx_buffers& B, int nblocks) {
+  __shared__ int last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned int* ctr = reinterpret_cast<unsigned int*>(B.scratch + (int64_t)nblocks * LGX_PARTIAL_STRIDE);
+    const unsigned int ticket = atomicAdd(ctr, 1u);
+    last = ticket == (unsigned int)nblocks - 1u;
+    if (last) atomicExch(ctr, 0u);  // ready for the next launch (stream-ordered after this one)
+  }
+  __syncthreads();
+  if (last) __threadfence();
+  return last;
+}
+
+// one post-physics workgroup: envs [blk * LGX_ENV_BLOCK, +LGX_ENV_BLOCK) of nblocks
+LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_buffers& B, int64_t step,
+                               const float* draws, int blk, int nblocks, float* snapshot) {
   const int N = P->num_envs;
   const int nobs = P->num_obs;
-  const int e0 = blockIdx.x * LGX_ENV_BLOCK;
+  const int e0 = blk * LGX_ENV_BLOCK;
   const int tid = threadIdx.x;
   const Draws D{P, draws, LGX_DRAW_NOISE + nobs};
   const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
@@ -397,8 +461,8 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
     }
   }
   LGX_CLK(2);
-  block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
-  __syncthreads();
+  block_partials(part, T, B.scratch + (int64_t)blk * LGX_PARTIAL_STRIDE);
+  const bool finalize = take_last_ticket(B, nblocks);
   for (int idx = tid; idx < T * LGX_ENV_BLOCK; idx += ENV_THREADS) {   // staged rows back
     const int t = idx / LGX_ENV_BLOCK, le = idx - t * LGX_ENV_BLOCK;
     if (e0 + le < N) B.episode_sums[(int64_t)t * N + e0 + le] = ssum[t][le];
@@ -449,6 +513,30 @@ lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int
   }
   LGX_CLK(5);
   LGX_CLK_PRINT("post_physics", 6)
+  if (finalize) {
+    __syncthreads();
+    extras_finalize_body(P, B, nblocks, 0, snapshot, ENV_THREADS);
+  }
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(ENV_THREADS)
+lgx_post_physics_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int64_t step, const float* draws,
+                        float* snapshot) {
+  post_physics_body(P, B, step, draws, blockIdx.x, gridDim.x, snapshot);
+}
+
+// post-physics and the Go1 actuator network in ONE launch: workgroups [0, nblocks) are the
+// post-physics workgroups, the rest persistent actuator-net workgroups.  The actuator output is
+// not read by the env step (go1.py:71-73), so the two are independent; sharing a launch lets the
+// latency-bound env logic and the MFMA-bound network fill the CUs together without a second
+// stream's event record / wait per step.
+__global__ void __launch_bounds__(ENV_THREADS, 2)
+lgx_post_physics_act_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int64_t step, const float* draws,
+                            float* snapshot, WsArgs wa, int32_t nblocks) {
+  if ((int)blockIdx.x < nblocks) post_physics_body(P, B, step, draws, blockIdx.x, nblocks, snapshot);
+  else actuator_ws_body(wa, blockIdx.x - nblocks, gridDim.x - nblocks);
 }
 
 // reset_idx on an explicit env list (BaseTask.reset, base_task.py:111-115)
@@ -477,46 +565,10 @@ lgx_reset_idx_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, const 
   block_partials(part, T, B.scratch + (int64_t)blockIdx.x * LGX_PARTIAL_STRIDE);
 }
 
-// extras finalize: deterministic sum of block partials; publish only if >= 1 env reset.
-// level_scan: sum terrain levels over all envs here (reset_idx path) instead of partials.
 __global__ void __launch_bounds__(256)
 lgx_extras_finalize_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int32_t nblocks, int32_t level_scan,
                            float* __restrict__ snapshot) {
-  const int N = P->num_envs;
-  const int T = P->num_terms + (P->termination_slot >= 0 ? 1 : 0);
-  __shared__ float sums[LGX_PARTIAL_STRIDE];
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  // wave w reduces rows w, w+4, ...: lanes take blocks lane, lane+64, ... then a fixed-order
-  // butterfly (deterministic, no atomics)
-  const int rows = T + 2;
-  for (int r = wave; r < rows; r += 4) {
-    float s = 0.f;
-    if (r == T + 1 && level_scan) {
-      if (P->curriculum)
-        for (int e = lane; e < N; e += 64) s += (float)B.terrain_levels[e];
-    } else {
-      for (int b = lane; b < nblocks; b += 64) s += B.scratch[(int64_t)b * LGX_PARTIAL_STRIDE + r];
-    }
-#pragma unroll
-    for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m);
-    if (lane == 0) sums[r] = s;
-  }
-  __syncthreads();
-  const float count = sums[T];
-  const bool update = count > 0.f;  // else the reference keeps stale extras (legged_robot.py:160-161)
-  if (t < rows) {
-    float v = B.extras[t];
-    if (update) {
-      if (t < T) v = (sums[t] / count) / P->max_episode_length_s;
-      else if (t == T + 1) v = count;
-      else if (P->curriculum) v = sums[T + 1] / (float)N;
-      B.extras[t] = v;
-    }
-    if (snapshot) snapshot[t] = v;  // this step's published copy (lgx_rebind_extras)
-  }
-  if (!update) return;
-  if (P->send_timeouts)
-    for (int e = t; e < N; e += 256) B.extras_time_outs[e] = B.time_out[e];
+  extras_finalize_body(P, B, nblocks, level_scan, snapshot, 256);
 }
 
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
@@ -524,8 +576,24 @@ int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int3
                             float* extras_snapshot, hipStream_t stream) {
   (void)num_obs; (void)n_term_rows; (void)measure_heights;
   int blocks = (n_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
-  LGX_LAUNCH(lgx_post_physics_kernel, dim3(blocks), dim3(ENV_THREADS), 0, stream, dp, b, step, draws);
-  hipLaunchKernelGGL(lgx_extras_finalize_kernel, dim3(1), dim3(256), 0, stream, dp, b, blocks, 0, extras_snapshot);
+  LGX_LAUNCH(lgx_post_physics_kernel, dim3(blocks), dim3(ENV_THREADS), 0, stream, dp, b, step, draws,
+             extras_snapshot);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int lgx_launch_post_physics_act(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int64_t step,
+                                const float* draws, float* extras_snapshot, const float* act_in, float* act_out,
+                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream) {
+  static_assert(ENV_THREADS == 256, "the actuator-net workgroups are 256 threads");
+  const int blocks = (n_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
+  const int64_t tiles = (act_rows + WS_BM - 1) / WS_BM;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  // one persistent actuator workgroup per CU next to the post-physics workgroups
+  const int act_wgs = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cus));
+  WsArgs wa{act_in, act_out, act_rows, act_w, act_scale};
+  LGX_LAUNCH(lgx_post_physics_act_kernel, dim3(blocks + act_wgs), dim3(ENV_THREADS), 0, stream, dp, b, step, draws,
+             extras_snapshot, wa, blocks);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -236,7 +236,11 @@ def test_lstm_matches_oracle(gpu):
         assert ok, f"lstm {name} max err {e}"
 
 
-def test_rough_terrain_step_matches_oracle(gpu):
+@pytest.mark.parametrize("act_mode", ["2", "1", "0"])
+def test_rough_terrain_step_matches_oracle(gpu, monkeypatch, act_mode):
+    """act_mode (LGX_ACT_OVERLAP): the actuator net inside the post-physics launch (2, default),
+    on an auxiliary stream (1) or serially on the step's stream (0)."""
+    monkeypatch.setenv("LGX_ACT_OVERLAP", act_mode)
     ora = make_env("go1_rough", num_envs=64, device="cpu", backend="oracle")
     dev = make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
     assert torch.equal(ora.height_samples, dev.height_samples.cpu()), "same seed -> same heightfield"
@@ -256,6 +260,10 @@ def test_rough_terrain_step_matches_oracle(gpu):
     assert ok, f"obs max err {e}"
     ok, e = close(dev.actuator_dvel, ora.actuator_dvel, 1e-3, 1e-3)
     assert ok, f"dVel max err {e}"
+    for name in ["rew_buf", "_episode_sums_buf", "_extras_buf"]:
+        ok, e = close(getattr(dev, name), getattr(ora, name), 1e-4, 1e-3)
+        assert ok, f"{name} max err {e}"
+    assert torch.equal(dev._extras_time_outs.cpu(), ora._extras_time_outs)
 
 
 def test_mlp_forward_batch_actor_critic(gpu):
