@@ -29,7 +29,10 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
+#include <type_traits>
 
 #include "lgx_internal.h"
 
@@ -39,7 +42,6 @@ namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int GT = 256;     // threads per workgroup (4 waves)
 constexpr int BM = 128;     // rows per workgroup tile
 constexpr int BN = 128;     // columns per workgroup tile
 
@@ -70,82 +72,136 @@ __device__ __forceinline__ float comp(const float4& q, int s) {
   return s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
 }
 
-// One K stage of the global -> LDS copy: 128 rows x 32 k of A and of B, 4 float4 per thread
-// each (8 threads per 128-byte row segment: coalesced).  k >= K is zero-filled.
-struct Stage {
-  float4 a[4], b[4];
+// Wave layouts of the 128 x 128 workgroup tile (template NW = waves per workgroup):
+//   NW = 4: 2 x 2 waves of 64 x 64 (2 x 2 accumulator tiles of 32 x 32, 64 floats per lane);
+//   NW = 8: 2 x 4 waves of 64 x 32 (2 x 1 tiles): half the accumulators per wave, 4 waves per
+//           SIMD at 2 workgroups per CU, so one workgroup's epilogue and barriers are covered by
+//           the other's MFMAs.
+template <int NW>
+struct Cfg {
+  static constexpr int GT = 64 * NW;            // threads per workgroup
+  static constexpr int WI = 2;                  // 32-row accumulator tiles per wave
+  static constexpr int WJ = NW == 4 ? 2 : 1;    // 32-column accumulator tiles per wave
+  static constexpr int WGN = BN / (32 * WJ);    // waves along N
+  static constexpr int WGM = NW / WGN;          // waves along M
+  static constexpr int NL = 1024 / GT;          // float4 per thread per operand per K stage
+  static constexpr int RSTEP = GT / 8;          // row step between a thread's float4s
+  static_assert(WGM * 32 * WI == BM, "wave grid covers the tile rows");
 };
 
-__device__ __forceinline__ void stage_load(Stage& st, const float* __restrict__ A, int64_t lda, int64_t m_base,
-                                           int64_t M, const float* __restrict__ B, int64_t ldb, int n_base, int K,
-                                           int k0, int tid) {
+// One K stage of the global -> LDS copy: 128 rows x 32 k of A and of B (8 threads per 128-byte
+// row segment: coalesced).  Thread t copies rows (t >> 3) + RSTEP i at columns c = (t & 7) * 4;
+// its row offsets are 32-bit (the caller checks that every operand has < 2^30 floats: 32-bit
+// byte offsets), so the loads address from the uniform base pointer (SGPRs) plus one VGPR
+// offset instead of a 64-bit VGPR address per load.  k >= K is zero-filled.
+template <int NW>
+struct Stage {
+  float4 a[Cfg<NW>::NL], b[Cfg<NW>::NL];
+};
+template <int NW>
+struct RowOffs {
+  uint32_t a[Cfg<NW>::NL], b[Cfg<NW>::NL];
+};
+
+template <int NW>
+__device__ __forceinline__ void row_offs(RowOffs<NW>& o, int64_t lda, int64_t m_base, int64_t M, int64_t ldb,
+                                         int n_base, int tid) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = tid + GT * i, row = q >> 3, c = (q & 7) * 4;
-    int64_t m = m_base + row;
-    m = m < M ? m : M - 1;  // rows past M load row M-1 (results discarded)
-    // branch-free tail: past K, load the last valid float4 (zeroed in stage_store)
-    const int kc = min(k0 + c, K - 4);
-    st.a[i] = ld4(A + m * lda + kc);
-    st.b[i] = ld4(B + (int64_t)(n_base + row) * ldb + kc);
+  for (int i = 0; i < Cfg<NW>::NL; ++i) {
+    const int row = (tid >> 3) + Cfg<NW>::RSTEP * i;
+    const int64_t m = min(m_base + row, M - 1);  // rows past M load row M-1 (results discarded)
+    o.a[i] = (uint32_t)(m * lda);
+    o.b[i] = (uint32_t)((int64_t)(n_base + row) * ldb);
   }
 }
 
-__device__ __forceinline__ void stage_store(const Stage& st, float* __restrict__ la, float* __restrict__ lb, int K,
-                                            int k0, int tid) {
+template <int NW>
+__device__ __forceinline__ void stage_load(Stage<NW>& st, const float* __restrict__ A, const float* __restrict__ B,
+                                           const RowOffs<NW>& o, int K, int k0, int c) {
+  // branch-free tail: past K, load the last valid float4 (zeroed in stage_store)
+  const uint32_t kc = (uint32_t)min(k0 + c, K - 4);
+  const char* Ab = reinterpret_cast<const char*>(A);
+  const char* Bb = reinterpret_cast<const char*>(B);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = tid + GT * i, row = q >> 3, c = (q & 7) * 4;
-    const bool in = k0 + c < K;
+  for (int i = 0; i < Cfg<NW>::NL; ++i) {  // 32-bit byte offsets: base (SGPR) + offset (VGPR)
+    st.a[i] = *reinterpret_cast<const float4*>(Ab + (uint32_t)((o.a[i] + kc) * 4u));
+    st.b[i] = *reinterpret_cast<const float4*>(Bb + (uint32_t)((o.b[i] + kc) * 4u));
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void stage_store(const Stage<NW>& st, float* __restrict__ la, float* __restrict__ lb, int K,
+                                            int k0, int tid) {
+  const int c = (tid & 7) * 4, r0 = tid >> 3;
+  constexpr int RS = Cfg<NW>::RSTEP;
+  if (k0 + BK <= K) {  // whole stage inside K (uniform)
+#pragma unroll
+    for (int i = 0; i < Cfg<NW>::NL; ++i) {
+      *reinterpret_cast<float4*>(la + (r0 + RS * i) * LDS_LD + c) = st.a[i];
+      *reinterpret_cast<float4*>(lb + (r0 + RS * i) * LDS_LD + c) = st.b[i];
+    }
+    return;
+  }
+  const bool in = k0 + c < K;
+#pragma unroll
+  for (int i = 0; i < Cfg<NW>::NL; ++i) {
     float4 va = st.a[i], vb = st.b[i];
     va.x = in ? va.x : 0.f; va.y = in ? va.y : 0.f; va.z = in ? va.z : 0.f; va.w = in ? va.w : 0.f;
     vb.x = in ? vb.x : 0.f; vb.y = in ? vb.y : 0.f; vb.z = in ? vb.z : 0.f; vb.w = in ? vb.w : 0.f;
-    *reinterpret_cast<float4*>(la + row * LDS_LD + c) = va;
-    *reinterpret_cast<float4*>(lb + row * LDS_LD + c) = vb;
+    *reinterpret_cast<float4*>(la + (r0 + RS * i) * LDS_LD + c) = va;
+    *reinterpret_cast<float4*>(lb + (r0 + RS * i) * LDS_LD + c) = vb;
   }
 }
 
 // MFMAs of one LDS stage.  Lane (r, h) reads 4 consecutive k of its row per ds_read_b128:
 // k group g covers k = 8g .. 8g+7, lane half h holds 8g + 4h .. 8g + 4h + 3, and substep s of
 // the group pairs (8g + s, 8g + 4 + s) - the same permutation for A and B.  The fragments of
-// group g+1 are read while group g's 16 MFMAs run (register double buffer).
+// group g+1 are read while group g's MFMAs run (register double buffer).
+template <int NW>
 struct LdsFrag {
-  float4 a[2], b[2];
+  float4 a[Cfg<NW>::WI], b[Cfg<NW>::WJ];
 };
 
-__device__ __forceinline__ void frag_read(LdsFrag& f, const float* __restrict__ la, const float* __restrict__ lb,
+template <int NW>
+using Acc = f32x16[Cfg<NW>::WI][Cfg<NW>::WJ];
+
+template <int NW>
+__device__ __forceinline__ void frag_read(LdsFrag<NW>& f, const float* __restrict__ la, const float* __restrict__ lb,
                                           int wm, int wn, int r, int h, int g) {
+  constexpr int WI = Cfg<NW>::WI, WJ = Cfg<NW>::WJ;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    f.a[i] = *reinterpret_cast<const float4*>(la + (wm * 64 + 32 * i + r) * LDS_LD + 8 * g + 4 * h);
+  for (int i = 0; i < WI; ++i)
+    f.a[i] = *reinterpret_cast<const float4*>(la + (wm * 32 * WI + 32 * i + r) * LDS_LD + 8 * g + 4 * h);
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
-    f.b[j] = *reinterpret_cast<const float4*>(lb + (wn * 64 + 32 * j + r) * LDS_LD + 8 * g + 4 * h);
+  for (int j = 0; j < WJ; ++j)
+    f.b[j] = *reinterpret_cast<const float4*>(lb + (wn * 32 * WJ + 32 * j + r) * LDS_LD + 8 * g + 4 * h);
 }
 
-__device__ __forceinline__ void frag_mma(const LdsFrag& f, f32x16 (&acc)[2][2]) {
+template <int NW>
+__device__ __forceinline__ void frag_mma(const LdsFrag<NW>& f, Acc<NW>& acc) {
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < Cfg<NW>::WI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < Cfg<NW>::WJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(f.a[i], s), comp(f.b[j], s), acc[i][j], 0, 0, 0);
 }
 
+template <int NW>
 __device__ __forceinline__ void stage_mma(const float* __restrict__ la, const float* __restrict__ lb, int wm, int wn,
-                                          int r, int h, f32x16 (&acc)[2][2]) {
-  LdsFrag f0, f1;
-  frag_read(f0, la, lb, wm, wn, r, h, 0);
+                                          int r, int h, Acc<NW>& acc) {
+  LdsFrag<NW> f0, f1;
+  frag_read<NW>(f0, la, lb, wm, wn, r, h, 0);
 #pragma unroll
   for (int g = 0; g < BK / 8; g += 2) {
-    frag_read(f1, la, lb, wm, wn, r, h, g + 1);
+    frag_read<NW>(f1, la, lb, wm, wn, r, h, g + 1);
     __builtin_amdgcn_sched_barrier(0);
-    frag_mma(f0, acc);
+    frag_mma<NW>(f0, acc);
     __builtin_amdgcn_sched_barrier(0);
-    if (g + 2 < BK / 8) frag_read(f0, la, lb, wm, wn, r, h, g + 2);
+    if (g + 2 < BK / 8) frag_read<NW>(f0, la, lb, wm, wn, r, h, g + 2);
     __builtin_amdgcn_sched_barrier(0);
-    frag_mma(f1, acc);
+    frag_mma<NW>(f1, acc);
     __builtin_amdgcn_sched_barrier(0);
   }
 }
@@ -165,82 +221,99 @@ __device__ __forceinline__ TileId decode_tile(int64_t tile, int ntn, int batch) 
 }
 
 // ---- epilogue: acc[i][j][e] is C[m0 + 32i + (e & 3) + 8(e >> 2) + 4h][n0 + 32j + r].
-// 32-bit offsets from the wave's tile corner; whole tiles (every tile when M % 128 == 0) store
-// without row guards.
-__device__ __forceinline__ int acc_row(int i, int e, int h) { return 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h; }
+// Every store / load addresses a wave-uniform row pointer (SGPRs) plus ONE per-lane 32-bit
+// byte offset (4h rows + r columns), so no per-row 64-bit addresses live in VGPRs; whole tiles
+// (every tile when M % 128 == 0) store without row guards.
+__device__ __forceinline__ int acc_row(int i, int e) { return 32 * i + (e & 3) + 8 * (e >> 2); }
 
-template <int EPI, bool FULL>
-__device__ __forceinline__ void epilogue_rows(const GemmArgs& g, const f32x16 (&acc)[2][2], int64_t m0, int n0, int z,
-                                              int r, int h, float (&cs)[2]) {
+template <typename T>
+__device__ __forceinline__ T* at_bytes(T* p, uint32_t off) {
+  return reinterpret_cast<T*>(reinterpret_cast<typename std::conditional<std::is_const<T>::value, const char, char>::type*>(p) + off);
+}
+
+template <int NW, int EPI, bool FULL>
+__device__ __forceinline__ void epilogue_rows(const GemmArgs& g, const Acc<NW>& acc, int64_t m0, int n0, int z, int r,
+                                              int h, float (&cs)[Cfg<NW>::WJ]) {
+  constexpr int WI = Cfg<NW>::WI, WJ = Cfg<NW>::WJ;
   float* C = g.C + z * g.sc + m0 * g.ldc + n0;
-  const int ldc = (int)g.ldc;
-  const int rows = (int)min<int64_t>(64, g.M - m0);
+  const int64_t ldc = g.ldc;
+  const int rows = (int)min<int64_t>(32 * WI, g.M - m0);
+  const uint32_t lo = (uint32_t)((4 * h * ldc + r) * 4);  // this lane's byte offset from a row pointer
   if (EPI == LGX_GEMM_DELU_COLSUM) {
     const float* Y = g.Y + z * g.sc + m0 * g.ldc + n0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
-      for (int e0 = 0; e0 < 16; e0 += 4) {   // 8 loads of Y in flight, then 8 stores
-        float y[4][2];
+      for (int e0 = 0; e0 < 16; e0 += 4) {   // 4 * WJ loads of Y in flight, then the stores
+        float y[4][WJ];
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int rr = acc_row(i, e0 + e, h);
-            y[e][j] = (FULL || rr < rows) ? Y[rr * ldc + 32 * j + r] : 0.f;
+          for (int j = 0; j < WJ; ++j) {
+            const int rr = acc_row(i, e0 + e);
+            y[e][j] = (FULL || rr + 4 * h < rows) ? *at_bytes(Y + rr * ldc + 32 * j, lo) : 0.f;
           }
 #pragma unroll
         for (int e = 0; e < 4; ++e)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int rr = acc_row(i, e0 + e, h);
+          for (int j = 0; j < WJ; ++j) {
+            const int rr = acc_row(i, e0 + e);
             const float d = acc[i][j][e0 + e] * elu_grad_from_out(y[e][j]);
-            if (FULL || rr < rows) {
-              C[rr * ldc + 32 * j + r] = d;
+            if (FULL || rr + 4 * h < rows) {
+              *at_bytes(C + rr * ldc + 32 * j, lo) = d;
               cs[j] += d;
             }
           }
       }
   } else {
-    float bj[2];
+    float bj[WJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bj[j] = EPI == LGX_GEMM_BIAS_ELU ? g.bias[(int64_t)z * g.N + n0 + 32 * j + r] : 0.f;
+    for (int j = 0; j < WJ; ++j) bj[j] = EPI == LGX_GEMM_BIAS_ELU ? g.bias[(int64_t)z * g.N + n0 + 32 * j + r] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int rr = acc_row(i, e, h);
+        for (int j = 0; j < WJ; ++j) {
+          const int rr = acc_row(i, e);
           float v = acc[i][j][e];
           if (EPI == LGX_GEMM_BIAS_ELU) v = elu_f(v + bj[j]);
-          if (FULL || rr < rows) C[rr * ldc + 32 * j + r] = v;
+          if (FULL || rr + 4 * h < rows) *at_bytes(C + rr * ldc + 32 * j, lo) = v;
         }
   }
 }
 
-template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x16 (&acc)[2][2], const TileId& T, int wave, int r,
+template <int NW, int EPI>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, const Acc<NW>& acc, const TileId& T, int wm, int wn, int r,
                                          int h) {
-  const int64_t m0 = T.mt * BM + (wave >> 1) * 64;
-  const int n0 = T.nt * BN + (wave & 1) * 64;
-  float cs[2] = {0.f, 0.f};
-  if (T.mt * BM + BM <= g.M) epilogue_rows<EPI, true>(g, acc, m0, n0, T.z, r, h, cs);
-  else if (m0 < g.M) epilogue_rows<EPI, false>(g, acc, m0, n0, T.z, r, h, cs);
-  if (EPI == LGX_GEMM_DELU_COLSUM) {
-    // column sums: lane halves hold different rows of the same column, then the two wave rows
-    __shared__ float red[2][2][64];  // [wave row][wave column][column within the wave's 64]
+  constexpr int WI = Cfg<NW>::WI, WJ = Cfg<NW>::WJ, WGM = Cfg<NW>::WGM;
+  const int64_t m0 = T.mt * BM + wm * 32 * WI;
+  const int n0 = T.nt * BN + wn * 32 * WJ;
+  float cs[WJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) cs[j] += __shfl_xor(cs[j], 32);
+  for (int j = 0; j < WJ; ++j) cs[j] = 0.f;
+  if (T.mt * BM + BM <= g.M) epilogue_rows<NW, EPI, true>(g, acc, m0, n0, T.z, r, h, cs);
+  else if (m0 < g.M) epilogue_rows<NW, EPI, false>(g, acc, m0, n0, T.z, r, h, cs);
+  if (EPI == LGX_GEMM_DELU_COLSUM) {
+    // column sums: lane halves hold different rows of the same column, then the wave rows
+    __shared__ float red[WGM][BN];  // [wave row][column within the tile]
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) cs[j] += __shfl_xor(cs[j], 32);
+    const int cl = wn * 32 * WJ;  // the wave's first column within the tile
     if (h == 0) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) red[wave >> 1][wave & 1][32 * j + r] = cs[j];
+      for (int j = 0; j < WJ; ++j) red[wm][cl + 32 * j + r] = cs[j];
     }
     __syncthreads();
-    if ((wave >> 1) == 0 && h == 0) {
+    if (wm == 0 && h == 0) {
       float* P = g.partials + T.mt * ((int64_t)g.batch * g.N) + (int64_t)T.z * g.N;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) P[n0 + 32 * j + r] = red[0][wave & 1][32 * j + r] + red[1][wave & 1][32 * j + r];
+      for (int j = 0; j < WJ; ++j) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) v += red[w][cl + 32 * j + r];   // fixed order
+        P[n0 + 32 * j + r] = v;
+      }
     }
   }
 }
@@ -248,13 +321,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs& g, const f32x16 (&acc)[
 // Persistent workgroups: the tiles of XCD x (workgroups are dealt round-robin to the 8 XCDs)
 // are the contiguous range [x T / 8, (x + 1) T / 8), n fastest, then the network, then m;
 // workgroup w of the XCD takes its tiles w, w + W, ...  The first K stage of the next tile is
-// loaded while the current tile's epilogue runs.
-template <int EPI>
-__global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs g) {
+// loaded while the current tile's last stage and epilogue run.
+template <int NW, int EPI>
+__global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) gemm_nt_kernel(GemmArgs g) {  // 2 workgroups per CU
   __shared__ __attribute__((aligned(16))) float lds[4 * TILE_FLOATS];  // 2 stages x (A tile, B tile): 72 KB
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / Cfg<NW>::WGN, wn = wave % Cfg<NW>::WGN;
   const int ntn = g.N / BN;
   const int64_t total = ((g.M + BM - 1) / BM) * ntn * g.batch;
   const int xcd = blockIdx.x & 7;
@@ -266,38 +339,48 @@ __global__ void __launch_bounds__(GT, 2) gemm_nt_kernel(GemmArgs g) {
   const int nst = (K + BK - 1) / BK;
 
   TileId T = decode_tile(tile, ntn, g.batch);
-  Stage st;
-  stage_load(st, g.A + T.z * g.sa, g.lda, T.mt * BM, g.M, g.B + T.z * g.sb, g.ldb, T.nt * BN, K, 0, tid);
+  const int c = (tid & 7) * 4;
+  RowOffs<NW> o;
+  row_offs<NW>(o, g.lda, T.mt * BM, g.M, g.ldb, T.nt * BN, tid);
+  Stage<NW> st;
+  stage_load<NW>(st, g.A + T.z * g.sa, g.B + T.z * g.sb, o, K, 0, c);
   for (;;) {
     const int64_t next = tile + wg_per_xcd;
     const bool has_next = next < hi;
     const TileId Tn = decode_tile(has_next ? next : tile, ntn, g.batch);
     const float* A = g.A + T.z * g.sa;
     const float* B = g.B + T.z * g.sb;
-    stage_store(st, lds, lds + TILE_FLOATS, K, 0, tid);
+    stage_store<NW>(st, lds, lds + TILE_FLOATS, K, 0, tid);
     __syncthreads();
-    f32x16 acc[2][2];
+    Acc<NW> acc;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < Cfg<NW>::WI; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < Cfg<NW>::WJ; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    // double-buffered LDS stages: the global loads of stage t+1 (after the last stage: stage 0
-    // of the next tile) are in flight while stage t's MFMAs run; one barrier per stage
-    for (int t = 0; t < nst; ++t) {
+    // double-buffered LDS stages: the global loads of stage t+1 are in flight while stage t's
+    // MFMAs run; one barrier per stage
+    for (int t = 0; t + 1 < nst; ++t) {
       float* cur = lds + (t & 1) * 2 * TILE_FLOATS;
       float* nxt = lds + ((t + 1) & 1) * 2 * TILE_FLOATS;
-      const bool more = t + 1 < nst;
-      if (more) stage_load(st, A, g.lda, T.mt * BM, g.M, B, g.ldb, T.nt * BN, K, (t + 1) * BK, tid);
-      else stage_load(st, g.A + Tn.z * g.sa, g.lda, Tn.mt * BM, g.M, g.B + Tn.z * g.sb, g.ldb, Tn.nt * BN, K, 0, tid);
+      stage_load<NW>(st, A, B, o, K, (t + 1) * BK, c);
       __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs they overlap
-      stage_mma(cur, cur + TILE_FLOATS, wm, wn, r, h, acc);
+      stage_mma<NW>(cur, cur + TILE_FLOATS, wm, wn, r, h, acc);
       __builtin_amdgcn_sched_barrier(0);
-      if (more) stage_store(st, nxt, nxt + TILE_FLOATS, K, (t + 1) * BK, tid);
+      stage_store<NW>(st, nxt, nxt + TILE_FLOATS, K, (t + 1) * BK, tid);
       __syncthreads();
     }
-    epilogue<EPI>(g, acc, T, wave, r, h);
+    {  // last stage: the next tile's stage 0 is in flight during its MFMAs and the epilogue
+      float* cur = lds + ((nst - 1) & 1) * 2 * TILE_FLOATS;
+      row_offs<NW>(o, g.lda, Tn.mt * BM, g.M, g.ldb, Tn.nt * BN, tid);
+      stage_load<NW>(st, g.A + Tn.z * g.sa, g.B + Tn.z * g.sb, o, K, 0, c);
+      __builtin_amdgcn_sched_barrier(0);
+      stage_mma<NW>(cur, cur + TILE_FLOATS, wm, wn, r, h, acc);
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+    }
+    epilogue<NW, EPI>(g, acc, T, wm, wn, r, h);
     if (!has_next) break;
     tile = next;
     T = Tn;
@@ -372,6 +455,8 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
       (a.epi == LGX_GEMM_BIAS_ELU && !a.bias) || (a.epi == LGX_GEMM_DELU_COLSUM && (!a.Y || !a.partials)))
     return lgx_fail(LGX_EINVAL,
                     "lgx_gemm_nt: bad args (N % 128, K % 4, 16-byte aligned A/B rows, epilogue operands)");
+  if (a.M * a.lda >= (1ll << 30) || (int64_t)a.N * a.ldb >= (1ll << 30))
+    return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: operand too large for 32-bit row offsets");
   const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
   if (tiles > (1ll << 31) - 1) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too large");
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
@@ -381,11 +466,22 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, 2 * cus / 8));
-  const dim3 grid((unsigned)wgs), block(GT);
-  if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH(gemm_nt_kernel<LGX_GEMM_BIAS_ELU>, grid, block, 0, LGX_STREAM(stream), g);
-  else if (a.epi == LGX_GEMM_DELU_COLSUM)
-    LGX_LAUNCH(gemm_nt_kernel<LGX_GEMM_DELU_COLSUM>, grid, block, 0, LGX_STREAM(stream), g);
-  else LGX_LAUNCH(gemm_nt_kernel<LGX_GEMM_PLAIN>, grid, block, 0, LGX_STREAM(stream), g);
+  const dim3 grid((unsigned)wgs);
+  const char* ew = getenv("LGX_GEMM_WAVES");  // A/B switch: 4 or 8 waves per 128 x 128 tile
+  const int nw = ew && atoi(ew) == 4 ? 4 : 8;
+  if (nw == 8) {
+    const dim3 block(512);
+    if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_BIAS_ELU>), grid, block, 0, LGX_STREAM(stream), g);
+    else if (a.epi == LGX_GEMM_DELU_COLSUM)
+      LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_DELU_COLSUM>), grid, block, 0, LGX_STREAM(stream), g);
+    else LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_PLAIN>), grid, block, 0, LGX_STREAM(stream), g);
+  } else {
+    const dim3 block(256);
+    if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH((gemm_nt_kernel<4, LGX_GEMM_BIAS_ELU>), grid, block, 0, LGX_STREAM(stream), g);
+    else if (a.epi == LGX_GEMM_DELU_COLSUM)
+      LGX_LAUNCH((gemm_nt_kernel<4, LGX_GEMM_DELU_COLSUM>), grid, block, 0, LGX_STREAM(stream), g);
+    else LGX_LAUNCH((gemm_nt_kernel<4, LGX_GEMM_PLAIN>), grid, block, 0, LGX_STREAM(stream), g);
+  }
   return lgx_hip_status("lgx_gemm_nt");
 }
 

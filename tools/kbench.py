@@ -153,11 +153,15 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
         a.M, a.N, a.K, a.batch, a.epi = M, n_, k_, 2, epi
         a.A, a.lda, a.sa, a.B, a.ldb, a.sb = A.data_ptr(), k_, M * k_, B.data_ptr(), k_, n_ * k_
         a.C, a.ldc, a.sc, a.bias, a.Y, a.partials = Cc.data_ptr(), n_, M * n_, bias.data_ptr(), Y.data_ptr(), parts.data_ptr()
-        t1 = timeit(lambda: lib.lgx_gemm_nt(C.byref(a), stream), iters=iters)
-        t2 = timeit(lambda: torch.bmm(A, B.transpose(1, 2), out=Cc), iters=iters) if torch_too else float("nan")
         f = 2.0 * 2 * M * n_ * k_
-        print(f"gemm M={M} N={n_} K={k_} epi={epi}: lgx {t1*1e3:.1f} us {f/t1/1e9:.1f} TF/s | torch bmm (no epilogue) "
-              f"{t2*1e3:.1f} us {f/t2/1e9:.1f} TF/s", flush=True)
+        for waves in ("4", "8"):
+            os.environ["LGX_GEMM_WAVES"] = waves
+            t1 = timeit(lambda: lib.lgx_gemm_nt(C.byref(a), stream), iters=iters)
+            print(f"gemm M={M} N={n_} K={k_} epi={epi} waves={waves}: lgx {t1*1e3:.1f} us {f/t1/1e9:.1f} TF/s", flush=True)
+        os.environ.pop("LGX_GEMM_WAVES")
+        if torch_too:
+            t2 = timeit(lambda: torch.bmm(A, B.transpose(1, 2), out=Cc), iters=iters)
+            print(f"  torch bmm (no epilogue) {t2*1e3:.1f} us {f/t2/1e9:.1f} TF/s", flush=True)
 
 
 def phys_run(task="go1_rough", n=4096, steps=10):
@@ -189,6 +193,6 @@ if __name__ == "__main__":
         if f"ppo_{m}" in what:
             ppo_ab(modes=(m,), gemms=False)
     if "gemm" in what:
-        gemm_bench()
+        gemm_bench(torch_too="torch" in what)
 
 
