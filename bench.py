@@ -3,7 +3,7 @@ node) for Go1 on rough trimesh terrain with the 187-point height scan, 4096 envs
 (BASELINE.json metric; workload = configs[2] "C3", which fits one GPU; N>1 = configs[3]).
 
 One "step" = one PPO iteration: 24 x (policy act on the fused MFMA MLP + lgx_step) + GAE +
-5 epochs x 4 minibatches of PPO (autograd, RCCL gradient all-reduce when N>1).
+5 epochs x 4 minibatches of PPO (fused f32-MFMA update, RCCL gradient all-reduce when N>1).
 value = 24 * envs_per_gpu * world * K / max-over-ranks wall time of K iterations.
 
 Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N>1 the driver uses
@@ -25,10 +25,22 @@ sys.path.insert(0, ROOT)
 ACT_MLP_FLOP_PER_ENV_STEP = 4 * 4 * 2 * (30 * 128 + 128 * 128 * 2 + 128 * 3)
 MI355X_F32_PEAK_TFLOPS = 157.3      # vector FP32 == f32 MFMA peak (MI355X_MICROARCH.md)
 MI355X_HBM_PEAK_GBS = 8000.0
-# HBM bytes per physics launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE
-# counts half of wide reads), rocprofv3 --pmc passes in profiles/r01_pmc_env_kernels.json
-PHYS_PMC_TRAFFIC_BYTES = int((2 * 4508.4 + 11584.0) * 1024)
-ACT_PMC_TRAFFIC_BYTES = int((2 * 4521.6 + 768.0) * 1024)    # actuator MLP launch, same passes
+# HBM bytes per launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts
+# half of wide reads), from the rocprofv3 --pmc passes of the same build (tools/pmc_round.sh ->
+# profiles/r01_pmc_env_kernels.json); the actuator net from the passes that launch it on its own
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_env_kernels.json")
+
+
+def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
+    try:
+        p = json.load(open(PMC_FILE))["passes"]
+        return int((2 * p[fetch_pass][kernel]["FETCH_SIZE"] + p[write_pass][kernel]["WRITE_SIZE"]) * 1024)
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
+ACT_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_actuator_ws_kernel", "fetch_sep", "write_sep")
 
 
 from legged_gym_amd.sim.flops import physics_flop_per_env_substep, policy_flop_per_sample  # noqa: E402
@@ -235,7 +247,7 @@ def main():
             "algorithmic_per_launch": phys_flop,
             "note": ("compute roof = FP32 peak (vector FP32 = f32 MFMA = 157.3 TF on gfx950); algorithmic FLOP "
                      "from legged_gym_amd/sim/flops.py x envs x substeps; traffic = FETCH_SIZE*2 + WRITE_SIZE "
-                     "per launch from profiles/r01_pmc_env_kernels.json; latency-bound, see DESIGN.md 4.1")}
+                     "per launch from profiles/r01_pmc_env_kernels.json (tools/pmc_round.sh); latency-bound, see DESIGN.md 4.1")}
     act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
     roof2 = {"kernel": "lgx_actuator_ws_kernel", "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
              "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None,
