@@ -70,19 +70,27 @@ LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* 
   constexpr int G = 8 / TPW;
   const int Kp = pad32(K);
   int col[TPW];
-  bool cv[TPW];
+  float cm[TPW];  // 1 for a real column, 0 for a padding lane
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
     col[t] = (wave + NW * t) * 16 + ln16;
-    cv[t] = col[t] < N;
+    cm[t] = col[t] < N ? 1.f : 0.f;
+    col[t] = min(col[t], N - 1);
   }
   float bA[G][TPW], bB[G][TPW];
+  // every lane loads (row and column clamped into W; padding lanes multiply by 0 - the weights
+  // are finite): a conditional load or select here becomes an exec-masked branch with a
+  // vmcnt(0) per load, serialising the whole B stream.  32-bit byte offsets from the SGPR base.
+  const char* Wb = reinterpret_cast<const char*>(W);
   auto load = [&](float (&b)[G][TPW], int k0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const int k = k0 + 4 * g + lq;
+      const uint32_t row = (uint32_t)(min(k, K - 1) * N);
+      const float km = k < K ? 1.f : 0.f;
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) b[g][t] = (cv[t] && k < K) ? W[(int64_t)k * N + col[t]] : 0.f;
+      for (int t = 0; t < TPW; ++t)
+        b[g][t] = *reinterpret_cast<const float*>(Wb + (row + (uint32_t)col[t]) * 4u) * (km * cm[t]);
     }
   };
   auto compute = [&](const float (&b)[G][TPW], int k0) {
