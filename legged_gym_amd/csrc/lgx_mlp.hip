@@ -70,27 +70,21 @@ LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* 
   constexpr int G = 8 / TPW;
   const int Kp = pad32(K);
   int col[TPW];
-  float cm[TPW];  // 1 for a real column, 0 for a padding lane
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    col[t] = (wave + NW * t) * 16 + ln16;
-    cm[t] = col[t] < N ? 1.f : 0.f;
-    col[t] = min(col[t], N - 1);
-  }
+  for (int t = 0; t < TPW; ++t) col[t] = min((wave + NW * t) * 16 + ln16, N - 1);
   float bA[G][TPW], bB[G][TPW];
-  // every lane loads (row and column clamped into W; padding lanes multiply by 0 - the weights
-  // are finite): a conditional load or select here becomes an exec-masked branch with a
-  // vmcnt(0) per load, serialising the whole B stream.  32-bit byte offsets from the SGPR base.
+  // Every lane loads, from a clamped row / column of W, with no select: padding columns
+  // (col >= N) only feed accumulator columns the epilogue discards, and rows k >= K meet the
+  // zero-padded activation columns (finite weights x 0 = 0).  A conditional load or select here
+  // compiles to an exec-masked branch or an early vmcnt wait per load, serialising the B stream.
+  // 32-bit byte offsets from the SGPR base.
   const char* Wb = reinterpret_cast<const char*>(W);
   auto load = [&](float (&b)[G][TPW], int k0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int k = k0 + 4 * g + lq;
-      const uint32_t row = (uint32_t)(min(k, K - 1) * N);
-      const float km = k < K ? 1.f : 0.f;
+      const uint32_t row = (uint32_t)(min(k0 + 4 * g + lq, K - 1) * N);
 #pragma unroll
-      for (int t = 0; t < TPW; ++t)
-        b[g][t] = *reinterpret_cast<const float*>(Wb + (row + (uint32_t)col[t]) * 4u) * (km * cm[t]);
+      for (int t = 0; t < TPW; ++t) b[g][t] = *reinterpret_cast<const float*>(Wb + (row + (uint32_t)col[t]) * 4u);
     }
   };
   auto compute = [&](const float (&b)[G][TPW], int k0) {
