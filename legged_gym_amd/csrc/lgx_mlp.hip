@@ -87,27 +87,33 @@ LGX_DEV void mlp_layer(const float* __restrict__ in_lds, int s_in, const float* 
       for (int t = 0; t < TPW; ++t) b[g][t] = *reinterpret_cast<const float*>(Wb + (row + (uint32_t)col[t]) * 4u);
     }
   };
-  auto compute = [&](const float (&b)[G][TPW], int k0) {
+  // A fragments (activations in LDS) are read one group ahead as well, so the MFMAs of a group
+  // never wait on their own LDS read
+  float aA[G][RS], aB[G][RS];
+  auto loadA = [&](float (&av)[G][RS], int k0) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      const int k = k0 + 4 * g + lq;
-      float av[RS];
+    for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int r = 0; r < RS; ++r) av[r] = in_lds[(r * 16 + ln16) * s_in + k];
+      for (int r = 0; r < RS; ++r) av[g][r] = in_lds[(r * 16 + ln16) * s_in + k0 + 4 * g + lq];
+  };
+  auto compute = [&](const float (&b)[G][TPW], const float (&av)[G][RS]) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
 #pragma unroll
       for (int t = 0; t < TPW; ++t)
 #pragma unroll
-        for (int r = 0; r < RS; ++r) acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], b[g][t], acc[r][t], 0, 0, 0);
-    }
+        for (int r = 0; r < RS; ++r)
+          acc[r][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[g][r], b[g][t], acc[r][t], 0, 0, 0);
   };
   constexpr int KG = 4 * G;  // k per group
   load(bA, 0);
+  loadA(aA, 0);
   for (int k0 = 0; k0 < Kp; k0 += 2 * KG) {
-    if (k0 + KG < Kp) load(bB, k0 + KG);
-    compute(bA, k0);
+    if (k0 + KG < Kp) { load(bB, k0 + KG); loadA(aB, k0 + KG); }
+    compute(bA, aA);
     if (k0 + KG >= Kp) break;
-    if (k0 + 2 * KG < Kp) load(bA, k0 + 2 * KG);
-    compute(bB, k0 + KG);
+    if (k0 + 2 * KG < Kp) { load(bA, k0 + 2 * KG); loadA(aA, k0 + 2 * KG); }
+    compute(bB, aB);
   }
 }
 
