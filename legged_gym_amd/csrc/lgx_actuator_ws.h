@@ -28,10 +28,8 @@ struct WsArgs {
 // tanh(x) = 1 - 2 / (exp(2x) + 1): |error| <= ~1.5e-7 absolute (fast exp), exact +-1 saturation
 LGX_DEV float fast_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
 
-LGX_DEV void ws_layer_epilogue(const lgx_f32x16& acc, const float* __restrict__ bias, float* __restrict__ out, int wave,
-                               int lane) {
+LGX_DEV void ws_layer_epilogue(const lgx_f32x16& acc, float bb, float* __restrict__ out, int wave, int lane) {
   const int col = wave * 32 + (lane & 31);
-  const float bb = bias[col];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int row = 8 * (i >> 2) + 4 * (lane >> 5) + (i & 3);
@@ -67,6 +65,11 @@ LGX_DEV void actuator_ws_body(const WsArgs& a, int wg, int nwg) {
     wr2[ks] = W2[(2 * ks + kh) * WS_H + col];
   }
   for (int i = tid; i < WS_H * 3 + 3; i += 256) w3[i] = i < WS_H * 3 ? W3[i] : b3[i - WS_H * 3];
+  // this lane's bias of each hidden layer and the output scale, in registers for the whole launch:
+  // a global load inside the tile loop would make its wait (vmcnt 0) also drain the next tile's
+  // prefetch
+  const float bb0 = b0[col], bb1 = b1[col], bb2 = b2[col];
+  const float osc = a.out_scale ? a.out_scale[min(tid & 7, 2)] : 1.f;
   const int64_t ntiles = (a.rows + WS_BM - 1) / WS_BM;
   // next tile's input rows are prefetched into registers while the current tile computes
   float pre[4];
@@ -96,7 +99,7 @@ LGX_DEV void actuator_ws_body(const WsArgs& a, int wg, int nwg) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(act0[(lane & 31) * WS_S0 + 2 * ks + kh], wr0[ks], acc, 0, 0, 0);
-    ws_layer_epilogue(acc, b0, act1, wave, lane);
+    ws_layer_epilogue(acc, bb0, act1, wave, lane);
     __syncthreads();
     // layer 1: 128 -> 128
 #pragma unroll
@@ -104,7 +107,7 @@ LGX_DEV void actuator_ws_body(const WsArgs& a, int wg, int nwg) {
 #pragma unroll
     for (int ks = 0; ks < 64; ++ks)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(act1[(lane & 31) * WS_S1 + 2 * ks + kh], wr1[ks], acc, 0, 0, 0);
-    ws_layer_epilogue(acc, b1, act0, wave, lane);  // act0 (layer-0 input) is no longer read
+    ws_layer_epilogue(acc, bb1, act0, wave, lane);  // act0 (layer-0 input) is no longer read
     __syncthreads();
     // layer 2: 128 -> 128
 #pragma unroll
@@ -112,7 +115,7 @@ LGX_DEV void actuator_ws_body(const WsArgs& a, int wg, int nwg) {
 #pragma unroll
     for (int ks = 0; ks < 64; ++ks)
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(act0[(lane & 31) * WS_S1 + 2 * ks + kh], wr2[ks], acc, 0, 0, 0);
-    ws_layer_epilogue(acc, b2, act1, wave, lane);
+    ws_layer_epilogue(acc, bb2, act1, wave, lane);
     __syncthreads();
     // layer 3: 128 -> 3 on the VALU; thread = (row, 16-wide k slice), 8-lane shuffle reduction
     {
@@ -132,7 +135,7 @@ LGX_DEV void actuator_ws_body(const WsArgs& a, int wg, int nwg) {
       const int64_t gr = r0 + r;
       if (part < 3 && gr < a.rows) {
         const float sv = part == 0 ? s0 : (part == 1 ? s1 : s2);
-        a.y[gr * 3 + part] = (sv + w3[WS_H * 3 + part]) * (a.out_scale ? a.out_scale[part] : 1.f);
+        a.y[gr * 3 + part] = (sv + w3[WS_H * 3 + part]) * osc;
       }
     }
   }
