@@ -317,27 +317,43 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
     __syncthreads();
     const int np = P->num_height_points;
     const int total = LGX_ENV_BLOCK * np;
-    const int16_t* H = B.height_samples;
-#pragma unroll 4
-    for (int idx = tid; idx < total; idx += ENV_THREADS) {
-      const int le = idx / np, i = idx - le * np;
-      const int e = e0 + le;
-      if (e < N) {
-        float* mh = B.measured_heights + (int64_t)e * np + i;
-        if (P->terrain_kind == 0) {
-          *mh = 0.f;
-          sheight[le][i] = 0.f;
-        } else {
+    if (P->terrain_kind == 0) {  // plane: zeros (:831-832)
+      for (int idx = tid; idx < total; idx += ENV_THREADS) {
+        const int le = idx / np, i = idx - le * np;
+        if (e0 + le < N) B.measured_heights[(int64_t)(e0 + le) * np + i] = 0.f;
+        sheight[le][i] = 0.f;
+      }
+    } else {
+      // every lane gathers (rows past N use the clamped env staged above; only the stores are
+      // predicated): a gather inside a branch compiles to one exposed round trip per iteration,
+      // unconditional ones let the unrolled iterations' gathers overlap
+      const int16_t* H = B.height_samples;
+      const int cols = B.hf_cols;
+      const float rmax = (float)(B.hf_rows - 2), cmax = (float)(B.hf_cols - 2);
+      constexpr int U = 4;  // (env, point) pairs per lane in flight: all gathers issued before any store
+      for (int base = tid; base < total; base += U * ENV_THREADS) {
+        int hq[U][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int idx = min(base + u * ENV_THREADS, total - 1);
+          const int le = idx / np, i = idx - le * np;
           const float4 b = base_xy_yaw[le];
           const float2 hp = scan_pt[i];
           f3 o = quat_apply(0.f, 0.f, b.z, b.w, mk3(hp.x, hp.y, 0.f));
           float x = o.x + b.x + P->border_size, y = o.y + b.y + P->border_size;  // (p + root) + border, as :833-834
-          int64_t px = (int64_t)(x / P->horizontal_scale), py = (int64_t)(y / P->horizontal_scale);
-          px = px < 0 ? 0 : (px > B.hf_rows - 2 ? B.hf_rows - 2 : px);
-          py = py < 0 ? 0 : (py > B.hf_cols - 2 ? B.hf_cols - 2 : py);
-          int h1 = H[px * B.hf_cols + py], h2 = H[(px + 1) * B.hf_cols + py], h3 = H[px * B.hf_cols + py + 1];
-          const float hv = (float)min(min(h1, h2), h3) * P->vertical_scale;
-          *mh = hv;
+          // .long() truncation then clip to [0, rows - 2] (:835-838) == clamp then truncate
+          const int px = (int)fminf(fmaxf(x / P->horizontal_scale, 0.f), rmax);
+          const int py = (int)fminf(fmaxf(y / P->horizontal_scale, 0.f), cmax);
+          const int16_t* q = H + px * cols + py;
+          hq[u][0] = q[0]; hq[u][1] = q[cols]; hq[u][2] = q[1];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int idx = base + u * ENV_THREADS;
+          if (idx >= total) break;
+          const int le = idx / np, i = idx - le * np;
+          const float hv = (float)min(min(hq[u][0], hq[u][1]), hq[u][2]) * P->vertical_scale;
+          if (e0 + le < N) B.measured_heights[(int64_t)(e0 + le) * np + i] = hv;
           sheight[le][i] = hv;
         }
       }
