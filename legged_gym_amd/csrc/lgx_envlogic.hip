@@ -366,17 +366,32 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
   // term loop below re-reads them many times from a single lane per env
   constexpr int SROW = 24 + 12 + LGX_MAX_BODIES * 3 + 12 + 12 + 12;  // ds tq cf act la ldv
   __shared__ float srow[LGX_ENV_BLOCK][SROW + 1];
-  for (int idx = tid; idx < LGX_ENV_BLOCK * SROW; idx += ENV_THREADS) {
-    const int le = idx / SROW, c = idx - le * SROW;
-    const int e = min(e0 + le, N - 1);
-    float v;
-    if (c < 24) v = B.dof_state[(int64_t)e * 24 + c];
-    else if (c < 36) v = B.torques[(int64_t)e * 12 + c - 24];
-    else if (c < 36 + LGX_MAX_BODIES * 3) v = B.contact_forces[(int64_t)e * LGX_MAX_BODIES * 3 + c - 36];
-    else if (c < 48 + LGX_MAX_BODIES * 3) v = B.actions[(int64_t)e * 12 + c - 36 - LGX_MAX_BODIES * 3];
-    else if (c < 60 + LGX_MAX_BODIES * 3) v = B.last_actions[(int64_t)e * 12 + c - 48 - LGX_MAX_BODIES * 3];
-    else v = B.last_dof_vel[(int64_t)e * 12 + c - 60 - LGX_MAX_BODIES * 3];
-    srow[le][c] = v;
+  {
+    // the source address is selected, the load itself is unconditional, and U of them are in
+    // flight per lane before the LDS stores (a load per branch arm is one round trip each)
+    constexpr int U = 4;
+    for (int base = tid; base < LGX_ENV_BLOCK * SROW; base += U * ENV_THREADS) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = min(base + u * ENV_THREADS, LGX_ENV_BLOCK * SROW - 1);
+        const int le = idx / SROW, c = idx - le * SROW;
+        const int64_t e = min(e0 + le, N - 1);
+        const float* src;
+        if (c < 24) src = B.dof_state + e * 24 + c;
+        else if (c < 36) src = B.torques + e * 12 + c - 24;
+        else if (c < 36 + LGX_MAX_BODIES * 3) src = B.contact_forces + e * LGX_MAX_BODIES * 3 + c - 36;
+        else if (c < 48 + LGX_MAX_BODIES * 3) src = B.actions + e * 12 + c - 36 - LGX_MAX_BODIES * 3;
+        else if (c < 60 + LGX_MAX_BODIES * 3) src = B.last_actions + e * 12 + c - 48 - LGX_MAX_BODIES * 3;
+        else src = B.last_dof_vel + e * 12 + c - 60 - LGX_MAX_BODIES * 3;
+        v[u] = *src;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = base + u * ENV_THREADS;
+        if (idx < LGX_ENV_BLOCK * SROW) srow[idx / SROW][idx % SROW] = v[u];
+      }
+    }
   }
   // episode sums [T, N] and feet_air_time [N, 4] are read-modify-written by the env lane: stage
   // them too (coalesced over envs), so phase B has no dependent global round trips
