@@ -40,6 +40,20 @@ def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
 
 
 PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
+PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_ppo_kernels.json")
+GEMM_KERNELS = {1: "gemm_nt_kernel<8, 1>", 2: "gemm_nt_kernel<8, 2>"}
+GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: layer-1 forward of actor and critic (K = num_obs padded to 256)",
+              2: "lgx_gemm_nt LGX_GEMM_DELU_COLSUM: backward dA of the hidden layers (512x256 and 256x128 weights)"}
+
+
+def pmc_ppo_traffic_bytes(kernel):
+    """HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KB) of a PPO-update kernel from the PMC
+    passes over one bench iteration (tools/pmc_ppo.sh)."""
+    try:
+        p = json.load(open(PPO_PMC_FILE))["passes"]
+        return int((2 * p["fetch"][kernel]["FETCH_SIZE"] + p["write"][kernel]["WRITE_SIZE"]) * 1024)
+    except (OSError, KeyError, ValueError):
+        return None
 ACT_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_actuator_ws_kernel", "fetch_sep", "write_sep")
 
 
@@ -202,6 +216,9 @@ def main():
     gc.disable()   # no collector pauses inside the timed region (host-side Python only)
     timing_period = int(os.environ.get("LGX_BENCH_KERNEL_TIMING", "1"))   # time every k-th env step (0: off)
     lib.lgx_profile_enable(handle, timing_period)
+    fused = getattr(runner.alg, "_fused", None)
+    if fused is not None:   # HIP events around the PPO-update GEMM launches of every k-th minibatch
+        fused.time_gemms(int(os.environ.get("LGX_BENCH_GEMM_TIMING", "5")))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -213,6 +230,9 @@ def main():
     elapsed = time.perf_counter() - t0
     gc.enable()
     lib.lgx_profile_enable(handle, 0)
+    gemm_t = fused.gemm_timings() if fused is not None else {}
+    if fused is not None:
+        fused.time_gemms(0)
     ms = (C.c_double * 3)()
     cnt = (C.c_int64 * 3)()
     lgxlib.check(lib.lgx_profile_collect(handle, ms, cnt), "lgx_profile_collect")
@@ -236,7 +256,6 @@ def main():
         avg[1], launches = standalone_actuator_ms(lib, env, torch)
         act_note = (f"standalone lgx_actuator_ws_kernel on this step's model_ins rows, {launches} launches after the "
                     "timed region (in the rollout it runs on workgroups of lgx_post_physics_act_kernel)")
-    dom = max(range(3), key=lambda i: ms[i])
     decim = env.cfg.control.decimation
     phys_flop = N * decim * physics_flop_per_env_substep(
         env._lgx_model.num_points, 4.0, env.cfg.terrain.mesh_type in ("heightfield", "trimesh"))
@@ -259,8 +278,30 @@ def main():
         if r["achieved"] is not None:
             r["frac"] = r["achieved"] / r["peak"]
     it_ms = 1000.0 * elapsed / args.steps
+    # the PPO-update GEMM instantiations, timed live (events on the launch stream)
+    mb_per_iter = runner.alg.num_learning_epochs * runner.alg.num_mini_batches
+    gemm_roofs = []
+    for epi, (n, t_ms, flop, mbs) in sorted(gemm_t.items()):
+        if not n or not mbs:
+            continue
+        kname = GEMM_KERNELS.get(epi, f"gemm_nt_kernel<8, {epi}>")
+        gemm_roofs.append({
+            "kernel": kname, "bound": "mfma", "compute_pipe": "f32 MFMA (v_mfma_f32_32x32x2_f32)",
+            "achieved": flop / (t_ms * 1e-3) / 1e12, "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": flop / (t_ms * 1e-3) / 1e12 / MI355X_F32_PEAK_TFLOPS,
+            "traffic": pmc_ppo_traffic_bytes(kname), "algorithmic_per_launch": flop / n, "avg_ms": t_ms / n,
+            "launches_timed": n, "share_of_iteration": (t_ms / mbs) * mb_per_iter / it_ms,
+            "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K; "
+                    "HIP events around every launch of every k-th minibatch (LGX_BENCH_GEMM_TIMING); traffic = "
+                    "2 FETCH_SIZE + WRITE_SIZE per launch from profiles/r01_pmc_ppo_kernels.json"})
     kernels = {n: {"avg_ms": round(a, 4), "launches": int(c), "share_of_iteration": round(m / args.steps / it_ms, 4)}
                for n, a, c, m in zip(names, avg, cnt, ms)}
+    # `roofline` = the lgx kernel with the largest share of the iteration (the others follow it)
+    phys_share = ms[0] / args.steps / it_ms
+    roof["share_of_iteration"] = phys_share
+    cands = [roof] + gemm_roofs
+    cands.sort(key=lambda r: -r.get("share_of_iteration", 0.0))
+    roof, others = cands[0], cands[1:]
     out = {
         "metric": (BASELINE_METRIC if (args.task == "go1_rough" and N == 4096)
                    else f"env-steps/sec (whole node), {args.task} {N} envs/GPU"),
@@ -271,9 +312,10 @@ def main():
                                f"{runner.alg.num_learning_epochs} epochs x {runner.alg.num_mini_batches} minibatches",
                    "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
         "roofline": roof,
+        "roofline_others": others,
         "roofline_secondary": roof2,
         "iteration_roofline": iteration_roofline(runner, env, N, it_ms),
-        "dominant_lgx_kernel": names[dom],
+        "dominant_lgx_kernel": roof["kernel"],
         "lgx_kernels": kernels,
         "last_iteration": runner.last_iteration_stats,
     }

@@ -359,8 +359,8 @@ typedef struct lgx_ppo_loss_args {
   int32_t use_clipped_value_loss;
   float clip_param, value_loss_coef, entropy_coef;
   const int64_t* idx;           /* storage row of minibatch row r (NULL: identity) */
-  const float* mu_raw;          /* [M,A] actor output before its bias */
-  const float* v_raw;           /* [M]   critic output before its bias */
+  const float* mu_raw;          /* [M,A] actor output before its bias (head_in == NULL) */
+  const float* v_raw;           /* [M]   critic output before its bias (head_in == NULL) */
   const float* b4a;             /* [A] */
   const float* b4c;             /* [1] */
   const float* std;             /* [A] action std parameter */
@@ -380,6 +380,19 @@ typedef struct lgx_ppo_loss_args {
   float* g_b4a;                 /* [A] */
   float* g_b4c;                 /* [1] */
   float* stats;                 /* [3]: KL mean (this minibatch), += surrogate mean, += value-loss mean */
+  /* non-NULL: rsl_rl's adaptive schedule applied on the device from this minibatch's KL in the
+   * same call (lgx_ppo_adapt_lr semantics, kl_scale 1); NULL: the caller adapts separately
+   * (data-parallel: after the all-reduce of the KL) */
+  double* lr;
+  double desired_kl;
+  /* non-NULL: the output layers are evaluated in the same call (mu_raw, v_raw unused):
+   * head_in = last hidden activations [2, M, hidden] (actor, critic), W4a [A, hidden],
+   * W4c [1, hidden]; hidden % 16 == 0, (A + 1) * hidden * 4 <= 64 KB */
+  const float* head_in;
+  const float* W4a;
+  const float* W4c;
+  int32_t hidden;
+  int32_t pad_;
 } lgx_ppo_loss_args;
 int64_t lgx_ppo_loss_partials_floats(int64_t rows, int32_t num_actions);
 /* loss = mean(max(-adv r, -adv clip(r))) + c_v mean(value loss) - c_e mean(entropy), with its

@@ -31,6 +31,15 @@ constexpr int LOSS_TPB = 64;    // rows per loss workgroup (384 workgroups per 2
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
 
+// rsl_rl adaptive schedule (PPO.update): lr /= 1.5 if KL > 2 kl*, *= 1.5 if 0 < KL < kl*/2,
+// bounded [1e-5, 1e-2]; python-float (double) arithmetic as upstream
+__device__ __forceinline__ void adapt_lr(double kl, double* lr, double desired_kl) {
+  double l = lr[0];
+  if (kl > desired_kl * 2.0) l = fmax(1e-5, l / 1.5);
+  else if (desired_kl / 2.0 > kl && kl > 0.0) l = fmin(1e-2, l * 1.5);
+  lr[0] = l;
+}
+
 // ---------------------------------------------------------------------------------------- gather
 __global__ void __launch_bounds__(TPB)
 gather_rows_kernel(const float* __restrict__ src, float* __restrict__ dst, const int64_t* __restrict__ idx,
@@ -131,12 +140,65 @@ bias_act_kernel(float* __restrict__ z, const float* __restrict__ b, int64_t rows
 //   [A, 2A)     d loss / d b4a_j          (= sum of dMU over rows)
 //   2A          d loss / d b4c            (= sum of dV)
 //   2A+1        KL sum, 2A+2 surrogate sum, 2A+3 value-loss sum
-__global__ void __launch_bounds__(LOSS_TPB)
+// HEAD: the output layers are computed here too (mu_raw = A3a W4a^T, v_raw = A3c w4c^T from the
+// last hidden activations, instead of two library GEMMs): 256 threads per 64 rows, 4 lanes per
+// row each dot a quarter of the H columns (16-byte loads, weights broadcast from LDS), combined
+// across the 4 lanes in a fixed order; then one thread per row as without HEAD.
+template <bool HEAD>
+__global__ void __launch_bounds__(HEAD ? 4 * LOSS_TPB : LOSS_TPB)
 ppo_loss_kernel(lgx_ppo_loss_args a) {
   constexpr int MAXA = LGX_PPO_MAX_ACTIONS;
   const int A = a.num_actions;
   const int NP = 2 * A + 4;
   __shared__ float red[LOSS_TPB][2 * MAXA + 4 + 1];
+  __shared__ float hout[HEAD ? LOSS_TPB : 1][MAXA + 1];
+  if constexpr (HEAD) {
+    extern __shared__ float4 wsh[];               // [A + 1][H / 4]: W4a rows, then w4c
+    const int H = a.hidden, H4 = H >> 2;
+    for (int i = threadIdx.x; i < (A + 1) * H4; i += 4 * LOSS_TPB)
+      wsh[i] = i < A * H4 ? reinterpret_cast<const float4*>(a.W4a)[i]
+                          : reinterpret_cast<const float4*>(a.W4c)[i - A * H4];
+    __syncthreads();
+    const int lr = threadIdx.x >> 2, q = threadIdx.x & 3;
+    const int64_t row = min((int64_t)blockIdx.x * LOSS_TPB + lr, a.rows - 1);   // clamped: tail rows unused
+    const int qn = H4 >> 2;                       // float4 columns per lane
+    const float4* xa = reinterpret_cast<const float4*>(a.head_in + row * H) + q * qn;
+    const float4* xc = reinterpret_cast<const float4*>(a.head_in + (a.rows + row) * H) + q * qn;
+    float acc[MAXA + 1];
+#pragma unroll
+    for (int j = 0; j <= MAXA; ++j) acc[j] = 0.f;
+    for (int c = 0; c < qn; ++c) {
+      const float4 x = xa[c], y = xc[c];
+      const int col = q * qn + c;
+#pragma unroll
+      for (int j = 0; j < MAXA; ++j) {
+        if (j < A) {
+          const float4 w = wsh[j * H4 + col];
+          acc[j] += x.x * w.x + x.y * w.y + x.z * w.z + x.w * w.w;
+        }
+      }
+      const float4 w = wsh[A * H4 + col];
+      acc[MAXA] += y.x * w.x + y.y * w.y + y.z * w.z + y.w * w.w;
+    }
+#pragma unroll
+    for (int j = 0; j <= MAXA; ++j) {             // lanes q = 0..3 of a row are adjacent
+      float v = acc[j];
+      v += __shfl_xor(v, 1);
+      v += __shfl_xor(v, 2);
+      acc[j] = v;
+    }
+    if (q == 0) {
+#pragma unroll
+      for (int j = 0; j < MAXA; ++j)
+        if (j < A) hout[lr][j] = acc[j];
+      hout[lr][MAXA] = acc[MAXA];
+    }
+    __syncthreads();
+    if (threadIdx.x >= LOSS_TPB) {                // rows are handled by the first 64 threads
+      __syncthreads();
+      return;
+    }
+  }
   const int64_t r = (int64_t)blockIdx.x * LOSS_TPB + threadIdx.x;
   float* my = red[threadIdx.x];
   for (int k = 0; k < NP; ++k) my[k] = 0.f;
@@ -147,7 +209,7 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
     float logp = 0.f, kl = 0.f;
     const float half_log_2pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
     for (int j = 0; j < A; ++j) {
-      mu[j] = a.mu_raw[r * A + j] + a.b4a[j];
+      mu[j] = (HEAD ? hout[threadIdx.x][j] : a.mu_raw[r * A + j]) + a.b4a[j];
       sd[j] = a.std[j];
       act[j] = a.actions[g * A + j];
       float var = sd[j] * sd[j];
@@ -178,7 +240,7 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
       my[j] = dlogp * (d * d / (var * sd[j]) - 1.f / sd[j]);
     }
     // value loss
-    const float v = a.v_raw[r] + a.b4c[0];
+    const float v = (HEAD ? hout[threadIdx.x][MAXA] : a.v_raw[r]) + a.b4c[0];
     const float tv = a.target_values[g], ret = a.returns[g];
     float vl, dv;
     if (a.use_clipped_value_loss) {
@@ -241,20 +303,18 @@ ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) {
   if (t < A) a.g_std[t] = s - a.entropy_coef / a.std[t];   // entropy: -c_e mean(sum_j log std_j + c)
   else if (t < 2 * A) a.g_b4a[t - A] = s;
   else if (t == 2 * A) a.g_b4c[0] = s;
-  else if (t == 2 * A + 1) a.stats[0] = s * invM;          // KL mean of this minibatch (local)
+  else if (t == 2 * A + 1) {
+    const float kl = s * invM;
+    a.stats[0] = kl;                                         // KL mean of this minibatch (local)
+    if (a.lr) adapt_lr((double)kl, a.lr, a.desired_kl);     // single process: schedule applied here
+  }
   else if (t == 2 * A + 2) a.stats[1] += s * invM;         // running surrogate-loss sum
   else a.stats[2] += s * invM;                             // running value-loss sum
 }
 
-// rsl_rl adaptive schedule (PPO.update): lr /= 1.5 if KL > 2 kl*, *= 1.5 if 0 < KL < kl*/2,
-// bounded [1e-5, 1e-2]; python-float (double) arithmetic as upstream
 __global__ void adapt_lr_kernel(const float* __restrict__ kl_sum, float kl_scale, double* __restrict__ lr,
                                 double desired_kl) {
-  double kl = (double)(kl_sum[0] * kl_scale);
-  double l = lr[0];
-  if (kl > desired_kl * 2.0) l = fmax(1e-5, l / 1.5);
-  else if (desired_kl / 2.0 > kl && kl > 0.0) l = fmin(1e-2, l * 1.5);
-  lr[0] = l;
+  adapt_lr((double)(kl_sum[0] * kl_scale), lr, desired_kl);
 }
 
 // ---------------------------------------------------------------------------------------- head bwd
@@ -517,13 +577,21 @@ extern "C" int64_t lgx_ppo_loss_partials_floats(int64_t rows, int32_t num_action
 extern "C" int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream) {
   if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: null args");
   lgx_ppo_loss_args a = *args;
-  if (a.rows <= 0 || a.num_actions <= 0 || a.num_actions > LGX_PPO_MAX_ACTIONS || !a.mu_raw || !a.v_raw || !a.b4a ||
+  if (a.rows <= 0 || a.num_actions <= 0 || a.num_actions > LGX_PPO_MAX_ACTIONS || !a.b4a ||
       !a.b4c || !a.std || !a.actions || !a.old_logp || !a.old_mu || !a.old_sigma || !a.advantages ||
       !a.target_values || !a.returns || !a.d_mu || !a.d_v || !a.partials || !a.g_std || !a.g_b4a || !a.g_b4c ||
       !a.stats)
     return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: bad args");
   int blocks = (int)((a.rows + LOSS_TPB - 1) / LOSS_TPB);
-  hipLaunchKernelGGL(ppo_loss_kernel, dim3(blocks), dim3(LOSS_TPB), 0, LGX_STREAM(stream), a);
+  if (a.head_in) {
+    const size_t lds = (size_t)(a.num_actions + 1) * a.hidden * sizeof(float);
+    if (!a.W4a || !a.W4c || a.hidden <= 0 || a.hidden % 16 || lds > 65536)
+      return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: bad output-layer args (hidden % 16, (A+1)*hidden*4 <= 64 KB)");
+    hipLaunchKernelGGL(ppo_loss_kernel<true>, dim3(blocks), dim3(4 * LOSS_TPB), lds, LGX_STREAM(stream), a);
+  } else {
+    if (!a.mu_raw || !a.v_raw) return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: mu_raw / v_raw or head_in required");
+    hipLaunchKernelGGL(ppo_loss_kernel<false>, dim3(blocks), dim3(LOSS_TPB), 0, LGX_STREAM(stream), a);
+  }
   hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
   return lgx_hip_status("lgx_ppo_loss");
 }

@@ -5,9 +5,10 @@ Per minibatch (M rows), on one stream, no host synchronisation:
   weight preparation (lgx_copy2d: zero-padded layer-1 weights, transposed hidden weights)
   gather obs rows (lgx_ppo_gather_rows_padded, K padded to a multiple of 16)
   hidden layers: lgx_gemm_nt with the bias + ELU epilogue, {actor, critic} batched in one launch
-  heads: mm; lgx_ppo_loss = log-prob / ratio / clipped surrogate / clipped value loss / entropy
-         / KL and the analytic gradient w.r.t. mu, value, std, head biases
-  lgx_ppo_adapt_lr (device-side adaptive schedule; data-parallel: KL rides in the gradient all-reduce)
+  heads + loss: lgx_ppo_loss = output layers (in-kernel dot products), log-prob / ratio / clipped surrogate / clipped value loss / entropy
+         / KL and the analytic gradient w.r.t. mu, value, std, head biases; its finalize applies the
+         device-side adaptive schedule (data-parallel: lgx_ppo_adapt_lr after the gradient
+         all-reduce the KL rides in)
   backward: lgx_head_bwd, then per layer split-K bmm for dW, lgx_gemm_nt for dA with the ELU'
             + bias-gradient column-sum epilogue
   (hidden widths that are not multiples of 128, or LGX_PPO_GEMM=lib: library GEMMs through torch
@@ -20,6 +21,7 @@ the rollout's fused inference see the updated weights; the optimizer is `FlatAda
 state_dict has torch.optim.Adam's format (checkpoints stay loadable by upstream tooling).
 """
 import ctypes as C
+import os
 
 import torch
 import torch.nn as nn
@@ -275,6 +277,7 @@ class FusedPPOUpdate:
             return g
         fwd = [[]]
         b0 = fp.data_ptr() + f4 * self.bo[0]
+        self.fwd0_src = ["x"] if shared else ["x", "xc"]
         if shared:   # one input for both networks: batch stride 0
             fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, self.W1p.data_ptr(), self.Kp, h[0] * self.Kp, self.Y[0],
                             h[0], self.Kp, 2, abi.GEMM_BIAS_ELU, bias=b0))
@@ -350,15 +353,34 @@ class FusedPPOUpdate:
                        old_mu=st.mu.view(B, -1), old_sigma=st.sigma.view(B, -1), advantages=st.advantages.view(B),
                        target_values=st.values.view(B), returns=st.returns.view(B))
         args = self._loss_args(storage)
+        xs = None
+        if self.lgx_gemm:
+            # rsl_rl draws ONE permutation per update and every epoch walks the same minibatches,
+            # so the padded layer-1 inputs are gathered once (one launch over all B rows) and a
+            # minibatch reads its contiguous slice: no per-minibatch gather
+            xs = self._gather_all(indices, obs, cobs, nmb * M, stream)
         for _ in range(ppo.num_learning_epochs):
             for i in range(nmb):
                 idx = indices[i * M:(i + 1) * M]
-                self._minibatch(idx, obs, cobs, args, stream)
+                self._minibatch(idx, obs, cobs, args, stream,
+                                xs=None if xs is None else tuple(x[i * M:(i + 1) * M] if x is not None else None
+                                                                 for x in xs))
         n = ppo.num_learning_epochs * nmb
         s = self.stats.tolist()   # the one host synchronisation of the update
         ppo.learning_rate = float(self.optimizer.lr_dev.item())
         self.optimizer.param_groups[0]["lr"] = ppo.learning_rate
         return s[2] / n, s[1] / n
+
+    def _gather_all(self, indices, obs, cobs, rows, stream):
+        if getattr(self, "Xall", None) is None or self.Xall.shape[0] != rows:
+            self.Xall = torch.zeros(rows, self.Kp, device=self.dev)     # padding columns stay zero
+            self.Xcall = torch.zeros(rows, self.Kcp, device=self.dev) if self.Xcp is not None else None
+        self.check(self.lib.lgx_ppo_gather_rows_padded(_vp(obs), _vp(self.Xall), _vp(indices), rows, obs.shape[1],
+                                                       self.Kp, stream), "gather")
+        if cobs is not None:
+            self.check(self.lib.lgx_ppo_gather_rows_padded(_vp(cobs), _vp(self.Xcall), _vp(indices), rows,
+                                                           cobs.shape[1], self.Kcp, stream), "gather")
+        return self.Xall, self.Xcall
 
     def _loss_args(self, storage):
         a = abi.LgxPpoLossArgs()
@@ -377,6 +399,21 @@ class FusedPPOUpdate:
         a.g_b4c = a.g_b4a + 4 * self.A
         a.g_std = self.flat_g.data_ptr() + 4 * self.std_off
         a.stats = self.stats.data_ptr()
+        # output layers evaluated inside the loss call (no head GEMM launches) when they fit its LDS
+        H = self.hidden[-1]
+        self.head_in_loss = (os.environ.get("LGX_PPO_HEAD_IN_LOSS", "1") != "0" and H % 16 == 0
+                             and (self.A + 1) * H * 4 <= 65536)
+        if self.head_in_loss:
+            a.head_in, a.hidden = self.Y[self.L - 1].data_ptr(), H
+            a.W4a, a.W4c = self.W[self.L][0].data_ptr(), self.W[self.L][1].data_ptr()
+        else:
+            a.head_in, a.W4a, a.W4c, a.hidden = None, None, None, 0
+        # single process with the adaptive schedule: the loss finalize adapts the learning rate
+        # (data-parallel: lgx_ppo_adapt_lr after the all-reduce the KL rides in)
+        if p.desired_kl is not None and p.schedule == "adaptive" and p.dist is None:
+            a.lr, a.desired_kl = self.optimizer.lr_dev.data_ptr(), float(p.desired_kl)
+        else:
+            a.lr, a.desired_kl = None, 0.0
         self._keep = storage
         return a
 
@@ -395,21 +432,62 @@ class FusedPPOUpdate:
         self._minibatch(idx, obs, cobs, self._loss_args(storage), stream, apply=apply)
         return self.flat_g.clone()
 
+    # ------------------------------------------------------------------ GEMM timing (bench.py)
+    def time_gemms(self, period):
+        """Bracket every lgx_gemm_nt launch of every `period`-th minibatch with HIP events on the
+        launch stream (0: off); gemm_timings() reads them back per epilogue (kernel instantiation)."""
+        self._t_period, self._t_count, self._t_events, self._t_mb = int(period), 0, [], 0
+
+    def _gemm(self, g, stream):
+        rec = getattr(self, "_t_period", 0) and self._t_count % self._t_period == 0
+        if rec:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self.check(self.lib.lgx_gemm_nt(C.byref(g), stream), "gemm_nt")
+        if rec:
+            e1.record()
+            # algorithmic FLOP: the unpadded K of layer 1 (num_obs), not the zero-padded columns
+            k = self.num_obs if g.K == self.Kp else (self.num_cobs if g.K == getattr(self, "Kcp", -1) else g.K)
+            self._t_events.append((g.epi, 2.0 * g.M * g.N * k * g.batch, e0, e1))
+
+    def gemm_timings(self):
+        """{epilogue: (launches, total ms, total algorithmic FLOP, timed minibatches)} of the timed
+        launches."""
+        torch.cuda.synchronize()
+        out = {}
+        for epi, flop, e0, e1 in getattr(self, "_t_events", []):
+            n, ms, f, _ = out.get(epi, (0, 0.0, 0.0, 0))
+            out[epi] = (n + 1, ms + e0.elapsed_time(e1), f + flop, self._t_mb)
+        return out
+
     @torch.no_grad()
-    def _minibatch(self, idx, obs, cobs, args, stream, apply=True):
+    def _minibatch(self, idx, obs, cobs, args, stream, apply=True, xs=None):
+        """One minibatch: rows `idx` of the storage; `xs` = their padded layer-1 inputs already
+        gathered (slices of _gather_all's buffers), None = gather here."""
         lib, chk = self.lib, self.check
         ppo = self.ppo
         M, S, h, L, A = self.M, self.S, self.hidden, self.L, self.A
+        if getattr(self, "_t_period", 0):
+            self._t_mb += self._t_count % self._t_period == 0
+            self._t_count += 1
         fused = self.lgx_gemm
-        Xc = self.X
+        X = Xc = self.X
         if fused:
             chk(lib.lgx_copy2d(self.copy_jobs, len(self.copy_jobs), stream), "copy2d")
-            chk(lib.lgx_ppo_gather_rows_padded(_vp(obs), _vp(self.Xp), _vp(idx), M, obs.shape[1], self.Kp, stream),
-                "gather")
-            if cobs is not None:
-                chk(lib.lgx_ppo_gather_rows_padded(_vp(cobs), _vp(self.Xcp), _vp(idx), M, cobs.shape[1], self.Kcp,
+            if xs is None:
+                chk(lib.lgx_ppo_gather_rows_padded(_vp(obs), _vp(self.Xp), _vp(idx), M, obs.shape[1], self.Kp,
                                                    stream), "gather")
-                Xc = self.Xc
+                if cobs is not None:
+                    chk(lib.lgx_ppo_gather_rows_padded(_vp(cobs), _vp(self.Xcp), _vp(idx), M, cobs.shape[1],
+                                                       self.Kcp, stream), "gather")
+                xp, xcp = self.Xp, self.Xcp
+            else:
+                xp, xcp = xs
+            X = Xc = xp[:, :self.num_obs]
+            if cobs is not None:
+                Xc = xcp[:, :self.num_cobs]
+            for g, src in zip(self.gemm_fwd[0], self.fwd0_src):
+                g.A = (xp if src == "x" or xcp is None else xcp).data_ptr()
         else:
             chk(lib.lgx_ppo_gather_rows(_vp(obs), _vp(self.X), _vp(idx), M, obs.shape[1], stream), "gather")
             if cobs is not None:
@@ -420,19 +498,19 @@ class FusedPPOUpdate:
         fp = self.flat_p
         if fused:
             for g in self.gemm_fwd[0]:
-                chk(lib.lgx_gemm_nt(C.byref(g), stream), "gemm_nt")
+                self._gemm(g, stream)
             for k in range(1, L):
                 if k in self.lgx_fwd_layers:
-                    chk(lib.lgx_gemm_nt(C.byref(self.gemm_fwd[k]), stream), "gemm_nt")
+                    self._gemm(self.gemm_fwd[k], stream)
                 else:
                     torch.bmm(self.Y[k - 1], self.W[k].transpose(1, 2), out=self.Y[k])
                     chk(lib.lgx_bias_act(_vp(self.Y[k]), C.c_void_p(fp.data_ptr() + 4 * self.bo[k]), M, h[k], 2, 1,
                                          stream), "bias")
         else:
             if cobs is None:   # shared input: one batched GEMM over {actor, critic} with a stride-0 input
-                torch.bmm(self.X.unsqueeze(0).expand(2, M, self.num_obs), self.W1s.transpose(1, 2), out=self.Y[0])
+                torch.bmm(X.unsqueeze(0).expand(2, M, self.num_obs), self.W1s.transpose(1, 2), out=self.Y[0])
             else:
-                torch.mm(self.X, wa.t(), out=self.Y[0][0])
+                torch.mm(X, wa.t(), out=self.Y[0][0])
                 torch.mm(Xc, wc.t(), out=self.Y[0][1])
             chk(lib.lgx_bias_act(_vp(self.Y[0]), C.c_void_p(fp.data_ptr() + 4 * self.bo[0]), M, h[0], 2, 1, stream),
                 "bias")
@@ -441,15 +519,13 @@ class FusedPPOUpdate:
                 chk(lib.lgx_bias_act(_vp(self.Y[k]), C.c_void_p(fp.data_ptr() + 4 * self.bo[k]), M, h[k], 2, 1,
                                      stream), "bias")
         wha, whc = self.W[L]
-        torch.mm(self.Y[L - 1][0], wha.t(), out=self.MU)
-        torch.mm(self.Y[L - 1][1], whc.t(), out=self.V)
+        if not self.head_in_loss:
+            torch.mm(self.Y[L - 1][0], wha.t(), out=self.MU)
+            torch.mm(self.Y[L - 1][1], whc.t(), out=self.V)
         # ---- loss, gradient at the heads, KL -> adaptive learning rate
         args.idx = idx.data_ptr()
         chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
-        adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"
-        if adaptive and ppo.dist is None:   # (data-parallel: after the joint all-reduce below)
-            chk(lib.lgx_ppo_adapt_lr(_vp(self.stats), 1.0, _vp(self.optimizer.lr_dev), ppo.desired_kl, stream),
-                "adapt_lr")
+        adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"   # (single process: in the loss call)
         # ---- backward
         chk(lib.lgx_head_bwd(_vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc), _vp(self.Y[L - 1]), M, A, h[-1],
                              _vp(self.head_parts), stream), "head_bwd")
@@ -459,13 +535,13 @@ class FusedPPOUpdate:
             torch.bmm(dZ.view(2 * S, M // S, h[k]).transpose(1, 2), self.Y[k - 1].view(2 * S, M // S, h[k - 1]),
                       out=self.P[k])
             if fused:
-                chk(lib.lgx_gemm_nt(C.byref(self.gemm_bwd[k]), stream), "gemm_nt")
+                self._gemm(self.gemm_bwd[k], stream)
             else:
                 torch.bmm(dZ, self.W[k], out=self.D[k - 1])
                 chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
                                            _vp(self.col_parts[k - 1]), stream), "elu_bwd")
             dZ = self.D[k - 1]
-        torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), self.X.unflatten(0, (S, M // S)), out=self.P[0][0])
+        torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
         torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
         chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
         if not apply:

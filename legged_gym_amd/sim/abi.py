@@ -105,7 +105,8 @@ class LgxPpoLossArgs(C.Structure):
                 ("value_loss_coef", C.c_float), ("entropy_coef", C.c_float)] + [
         (n, C.c_void_p) for n in ("idx", "mu_raw", "v_raw", "b4a", "b4c", "std", "actions", "old_logp", "old_mu",
                                   "old_sigma", "advantages", "target_values", "returns", "d_mu", "d_v", "partials",
-                                  "g_std", "g_b4a", "g_b4c", "stats")]
+                                  "g_std", "g_b4a", "g_b4c", "stats", "lr")] + [("desired_kl", C.c_double)] + [
+        (n, C.c_void_p) for n in ("head_in", "W4a", "W4c")] + [("hidden", i32), ("pad_", i32)]
 
 
 class LgxReduceJob(C.Structure):

@@ -85,6 +85,19 @@ def test_fused_minibatch_gradient_matches_autograd(gpu):
         assert ((a - b).abs() <= tol).all(), (n, (a - b).abs().max().item(), b.abs().max().item())
 
 
+def test_fused_minibatch_gradient_library_heads(gpu, monkeypatch):
+    """The output layers on library GEMMs (LGX_PPO_HEAD_IN_LOSS=0) instead of inside lgx_ppo_loss."""
+    monkeypatch.setenv("LGX_PPO_HEAD_IN_LOSS", "0")
+    ref, fus = make_pair()
+    idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
+    gref = autograd_grads(ref, idx)
+    fus._fused.gradients(idx)
+    assert not fus._fused.head_in_loss
+    for n, p in fus.actor_critic.named_parameters():
+        a, b = p.grad, gref[n]
+        assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), n
+
+
 @pytest.mark.parametrize("schedule", ["adaptive", "fixed"])
 def test_fused_update_matches_autograd_update(gpu, schedule):
     ref, fus = make_pair(schedule)

@@ -10,7 +10,8 @@ from collections import defaultdict
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_pmc_env_kernels.json"
-out = {"what": "rocprofv3 --kernel-trace --pmc, per-dispatch means over tools/kbench.py physrun (go1_rough, "
+what = sys.argv[3] if len(sys.argv) > 3 else None
+out = {"what": what or "rocprofv3 --kernel-trace --pmc, per-dispatch means over tools/kbench.py physrun (go1_rough, "
                "4096 envs, 10 env steps); FETCH_SIZE/WRITE_SIZE in KB (gfx950: FETCH_SIZE reads half of wide "
                "coalesced bytes); SQ_* = wave-instruction totals per dispatch; passes *_sep ran with "
                "LGX_ACT_OVERLAP=0 (actuator net as its own launch)",
@@ -19,8 +20,10 @@ for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv")))
     name = os.path.basename(os.path.dirname(f))
     acc = defaultdict(lambda: defaultdict(list))
     for r in csv.DictReader(open(f)):
-        k = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
-        if not k.startswith("lgx_"):
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+        k = re.sub(r"\(.*", "", k)
+        if k.startswith(("at::", "rocprim", "Cijk", "__amd")) or not ("lgx_" in k or k.endswith("_kernel>") or
+                                                                    "_kernel" in k):
             continue
         acc[k][r["Counter_Name"]].append((int(r.get("Dispatch_Id", 0)), float(r["Counter_Value"])))
     res = {}
