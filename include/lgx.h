@@ -392,7 +392,9 @@ typedef struct lgx_ppo_loss_args {
   const float* W4a;
   const float* W4c;
   int32_t hidden;
-  int32_t pad_;
+  /* nonzero: lgx_ppo_loss leaves the partial reduction (gradient slots, stats, adaptive LR) to
+   * the following lgx_head_bwd_finalize call, which runs it on one extra workgroup */
+  int32_t defer_finalize;
 } lgx_ppo_loss_args;
 int64_t lgx_ppo_loss_partials_floats(int64_t rows, int32_t num_actions);
 /* loss = mean(max(-adv r, -adv clip(r))) + c_v mean(value loss) - c_e mean(entropy), with its
@@ -407,6 +409,11 @@ int lgx_ppo_adapt_lr(const float* kl_sum, float kl_scale, double* lr, double des
 int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_actions, int32_t hidden);
 int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3, int64_t rows,
                  int32_t num_actions, int32_t hidden, float* partials, void* stream);
+/* lgx_head_bwd plus the finalize of a deferred lgx_ppo_loss call (loss->defer_finalize != 0,
+ * same rows / actions) on one extra workgroup of the same launch */
+int lgx_head_bwd_finalize(const lgx_ppo_loss_args* loss, const float* d_mu, const float* d_v, const float* W4a,
+                          const float* W4c, float* A3, int64_t rows, int32_t num_actions, int32_t hidden,
+                          float* partials, void* stream);
 
 /* dA [nets,M,H] -> dA * elu'(Y) in place (Y = ELU output) + per-chunk column sums */
 int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int32_t nets);
@@ -465,6 +472,13 @@ typedef struct lgx_copy2d_job {
   int32_t rows, cols, batch, transpose;
 } lgx_copy2d_job;
 int lgx_copy2d(const lgx_copy2d_job* jobs, int32_t njobs, void* stream);
+
+/* lgx_adam_clip that also writes every updated parameter of the `mirrors` blocks (lgx_copy2d
+ * job layout; src = a contiguous block of p) into its derived copy (zero-padded / transposed
+ * GEMM operands), replacing the lgx_copy2d pass before the next minibatch; <= 8 mirrors */
+int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
+                         float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1, float beta2,
+                         float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors, void* stream);
 
 /* lgx_ppo_gather_rows into rows of dst_ld floats, columns width .. dst_ld-1 zero-filled */
 int lgx_ppo_gather_rows_padded(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width,

@@ -273,8 +273,7 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
 // one workgroup: reduce the loss partials, write d std / d b4a / d b4c into the flat gradient,
 // the KL mean and the running loss sums.  Thread (g, k): value k over partial blocks g, g+8, ...
 // then a fixed-order combine of the 8 groups.
-__global__ void __launch_bounds__(TPB)
-ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) {
+__device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks) {   // TPB threads
   const int A = a.num_actions;
   const int NP = 2 * A + 4;               // <= 36
   __shared__ float red[8][2 * LGX_PPO_MAX_ACTIONS + 4];
@@ -312,6 +311,9 @@ ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) {
   else a.stats[2] += s * invM;                             // running value-loss sum
 }
 
+__global__ void __launch_bounds__(TPB)
+ppo_loss_finalize_kernel(lgx_ppo_loss_args a, int32_t nblocks) { loss_finalize(a, nblocks); }
+
 __global__ void adapt_lr_kernel(const float* __restrict__ kl_sum, float kl_scale, double* __restrict__ lr,
                                 double desired_kl) {
   adapt_lr((double)(kl_sum[0] * kl_scale), lr, desired_kl);
@@ -326,7 +328,13 @@ template <int MAXA>
 __global__ void __launch_bounds__(TPB)
 head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, const float* __restrict__ W4a,
                 const float* __restrict__ W4c, float* __restrict__ A3, int64_t rows, int32_t A, int32_t H,
-                float* __restrict__ partials) {
+                float* __restrict__ partials, lgx_ppo_loss_args fin, int32_t fin_blocks) {
+  // fin_blocks > 0: one extra (last) workgroup runs the loss finalize (it reads only the loss
+  // partials, complete at launch), so the finalize costs no launch of its own
+  if (fin_blocks > 0 && blockIdx.x == gridDim.x - 1) {
+    loss_finalize(fin, fin_blocks);
+    return;
+  }
   constexpr int DS = ((MAXA + 1 + 3) / 4) * 4;  // dMU row (+ dV) padded for 16-byte LDS reads
   __shared__ __align__(16) float dmu[HEAD_CHUNK][DS];
   const int64_t r0 = (int64_t)blockIdx.x * HEAD_CHUNK;
@@ -485,10 +493,25 @@ sumsq_kernel(const float* __restrict__ g, int64_t n, float scale, float* __restr
 // stage 2: every block re-reduces the (few) partials -> global norm -> clip coefficient
 // (torch clip_grad_norm_: coef = min(max_norm / (norm + 1e-6), 1)), then torch Adam
 // (fused form: step_size = lr / bc1; denom = sqrt(v) / sqrt(bc2) + eps)
+// Mirrors: derived copies of parameter blocks that the next minibatch's GEMMs read (zero-padded
+// layer-1 weights, transposed hidden weights; lgx_copy2d job layout with src inside p) written
+// with the updated value, so no weight-preparation pass runs between minibatches.
+struct Mirror {
+  int64_t off, dst_ld, dst_bs;  // off: first flat index of the block in p
+  float* dst;
+  int32_t count, rows, cols, transpose;   // count = batch * rows * cols
+};
+constexpr int MAX_MIRRORS = 8;
+struct Mirrors {
+  Mirror mj[MAX_MIRRORS];
+  int32_t n;
+};
+
 __global__ void __launch_bounds__(TPB)
 adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v, int64_t n,
                  const float* __restrict__ partials, int32_t nparts, float grad_scale, float max_norm,
-                 const double* __restrict__ lr, const int64_t* __restrict__ step, float beta1, float beta2, float eps) {
+                 const double* __restrict__ lr, const int64_t* __restrict__ step, float beta1, float beta2, float eps,
+                 Mirrors mir) {
   __shared__ float red[TPB];
   __shared__ float coef_s;
   float s = 0.f;
@@ -519,7 +542,17 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
     m[i] = mi;
     v[i] = vi;
     float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] -= step_size * mi / denom;
+    const float pi = p[i] - step_size * mi / denom;
+    p[i] = pi;
+    for (int q = 0; q < mir.n; ++q) {
+      const Mirror& J = mir.mj[q];
+      const uint64_t li = (uint64_t)(i - J.off);
+      if (li < (uint64_t)J.count) {
+        const int32_t l = (int32_t)li, rc = J.rows * J.cols;
+        const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
+        J.dst[b * J.dst_bs + (J.transpose ? (int64_t)cc * J.dst_ld + rr : (int64_t)rr * J.dst_ld + cc)] = pi;
+      }
+    }
   }
 }
 
@@ -592,7 +625,8 @@ extern "C" int lgx_ppo_loss(const lgx_ppo_loss_args* args, void* stream) {
     if (!a.mu_raw || !a.v_raw) return lgx_fail(LGX_EINVAL, "lgx_ppo_loss: mu_raw / v_raw or head_in required");
     hipLaunchKernelGGL(ppo_loss_kernel<false>, dim3(blocks), dim3(LOSS_TPB), 0, LGX_STREAM(stream), a);
   }
-  hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
+  if (!a.defer_finalize)
+    hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
   return lgx_hip_status("lgx_ppo_loss");
 }
 
@@ -606,19 +640,40 @@ extern "C" int64_t lgx_head_bwd_partials_floats(int64_t rows, int32_t num_action
   return ((rows + HEAD_CHUNK - 1) / HEAD_CHUNK) * ((int64_t)(num_actions + 1) * hidden + 2 * (int64_t)hidden);
 }
 
-extern "C" int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3,
-                            int64_t rows, int32_t num_actions, int32_t hidden, float* partials, void* stream) {
+static int head_bwd_launch(const lgx_ppo_loss_args* fin, const float* d_mu, const float* d_v, const float* W4a,
+                           const float* W4c, float* A3, int64_t rows, int32_t num_actions, int32_t hidden,
+                           float* partials, void* stream) {
   if (!d_mu || !d_v || !W4a || !W4c || !A3 || !partials || rows <= 0 || num_actions <= 0 ||
       num_actions > LGX_PPO_MAX_ACTIONS || hidden <= 0 || hidden > 1024)
     return lgx_fail(LGX_EINVAL, "lgx_head_bwd: bad args");
   int blocks = (int)((rows + HEAD_CHUNK - 1) / HEAD_CHUNK);
+  lgx_ppo_loss_args f{};
+  int32_t fin_blocks = 0;
+  if (fin) {
+    f = *fin;
+    fin_blocks = (int32_t)((f.rows + LOSS_TPB - 1) / LOSS_TPB);
+    blocks += 1;
+  }
   if (num_actions <= 12)
     hipLaunchKernelGGL(head_bwd_kernel<12>, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), d_mu, d_v, W4a, W4c, A3,
-                       rows, num_actions, hidden, partials);
+                       rows, num_actions, hidden, partials, f, fin_blocks);
   else
     hipLaunchKernelGGL(head_bwd_kernel<LGX_PPO_MAX_ACTIONS>, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), d_mu, d_v,
-                       W4a, W4c, A3, rows, num_actions, hidden, partials);
+                       W4a, W4c, A3, rows, num_actions, hidden, partials, f, fin_blocks);
   return lgx_hip_status("lgx_head_bwd");
+}
+
+extern "C" int lgx_head_bwd(const float* d_mu, const float* d_v, const float* W4a, const float* W4c, float* A3,
+                            int64_t rows, int32_t num_actions, int32_t hidden, float* partials, void* stream) {
+  return head_bwd_launch(nullptr, d_mu, d_v, W4a, W4c, A3, rows, num_actions, hidden, partials, stream);
+}
+
+extern "C" int lgx_head_bwd_finalize(const lgx_ppo_loss_args* loss, const float* d_mu, const float* d_v,
+                                     const float* W4a, const float* W4c, float* A3, int64_t rows, int32_t num_actions,
+                                     int32_t hidden, float* partials, void* stream) {
+  if (!loss || !loss->defer_finalize || loss->rows != rows || loss->num_actions != num_actions)
+    return lgx_fail(LGX_EINVAL, "lgx_head_bwd_finalize: loss args must be the deferred-finalize lgx_ppo_loss call's");
+  return head_bwd_launch(loss, d_mu, d_v, W4a, W4c, A3, rows, num_actions, hidden, partials, stream);
 }
 
 extern "C" int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int32_t nets) {
@@ -661,7 +716,33 @@ extern "C" int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, 
     return lgx_fail(LGX_EINVAL, "lgx_adam_clip: bad args");
   hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
   int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
+  Mirrors none{};
   hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
-                     grad_scale, max_norm, lr, step, beta1, beta2, eps);
+                     grad_scale, max_norm, lr, step, beta1, beta2, eps, none);
   return lgx_hip_status("lgx_adam_clip");
+}
+
+extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
+                                    float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
+                                    float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
+                                    void* stream) {
+  if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 || nparts > 1024 || nmirrors < 0 ||
+      nmirrors > MAX_MIRRORS || (nmirrors && !mirrors))
+    return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: bad args");
+  Mirrors M{};
+  M.n = nmirrors;
+  for (int q = 0; q < nmirrors; ++q) {
+    const lgx_copy2d_job& j = mirrors[q];
+    const int64_t off = j.src - p, count = (int64_t)j.batch * j.rows * j.cols;
+    // the block must be contiguous in p (src_ld == cols, src_bs == rows * cols) and inside it
+    if (!j.dst || j.rows <= 0 || j.cols <= 0 || j.batch <= 0 || j.src_ld != j.cols ||
+        (j.batch > 1 && j.src_bs != (int64_t)j.rows * j.cols) || off < 0 || off + count > n || count >= (1LL << 31))
+      return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: mirror source must be a contiguous block of p");
+    M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose};
+  }
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
+  int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
+  hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
+                     grad_scale, max_norm, lr, step, beta1, beta2, eps, M);
+  return lgx_hip_status("lgx_adam_clip_mirror");
 }

@@ -2,7 +2,8 @@
 forward/backward over flat parameter/gradient buffers — no autograd graph, no per-op launches.
 
 Per minibatch (M rows), on one stream, no host synchronisation:
-  weight preparation (lgx_copy2d: zero-padded layer-1 weights, transposed hidden weights)
+  weight preparation (lgx_copy2d: zero-padded layer-1 weights, transposed hidden weights) on the
+  first minibatch of an update; afterwards the Adam step writes these copies (lgx_adam_clip_mirror)
   gather obs rows (lgx_ppo_gather_rows_padded, K padded to a multiple of 16)
   hidden layers: lgx_gemm_nt with the bias + ELU epilogue, {actor, critic} batched in one launch
   heads + loss: lgx_ppo_loss = output layers (in-kernel dot products), log-prob / ratio / clipped surrogate / clipped value loss / entropy
@@ -15,7 +16,7 @@ Per minibatch (M rows), on one stream, no host synchronisation:
    + lgx_bias_act / lgx_elu_bwd_colsum instead of lgx_gemm_nt)
   lgx_reduce_slices: all split-K and bias partials -> flat gradient (one launch)
   [ONE all-reduce over RCCL when data-parallel: flat gradient + the minibatch KL]
-  lgx_adam_clip: clip_grad_norm_(max_grad_norm) + Adam on the flat buffers
+  lgx_adam_clip[_mirror]: clip_grad_norm_(max_grad_norm) + Adam on the flat buffers (+ the GEMM weight copies)
 The module's nn.Parameters become views of the flat buffer, so state_dict / load_state_dict /
 the rollout's fused inference see the updated weights; the optimizer is `FlatAdam`, whose
 state_dict has torch.optim.Adam's format (checkpoints stay loadable by upstream tooling).
@@ -190,6 +191,7 @@ class FusedPPOUpdate:
         self.lgx_gemm = all(hk % abi.GEMM_TILE_N == 0 for hk in self.hidden) and mode != "lib"
         self.lgx_fwd_layers = set(range(self.L)) if mode == "lgx" else {0}
         self.norm_parts = torch.zeros(256, device=self.dev)
+        self._mirrors_valid = False
         self.stats = torch.zeros(3, device=self.dev)
         self.M = None
 
@@ -343,6 +345,7 @@ class FusedPPOUpdate:
         nmb = ppo.num_mini_batches
         M = B // nmb
         self._alloc(M)
+        self._mirrors_valid = False      # parameters may have changed since the last update
         stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
         self.optimizer.lr_dev.fill_(ppo.learning_rate)
         self.stats.zero_()
@@ -408,6 +411,7 @@ class FusedPPOUpdate:
             a.W4a, a.W4c = self.W[self.L][0].data_ptr(), self.W[self.L][1].data_ptr()
         else:
             a.head_in, a.W4a, a.W4c, a.hidden = None, None, None, 0
+        a.defer_finalize = 1     # run by lgx_head_bwd_finalize
         # single process with the adaptive schedule: the loss finalize adapts the learning rate
         # (data-parallel: lgx_ppo_adapt_lr after the all-reduce the KL rides in)
         if p.desired_kl is not None and p.schedule == "adaptive" and p.dist is None:
@@ -423,6 +427,7 @@ class FusedPPOUpdate:
         T, N = st.num_transitions_per_env, st.num_envs
         B = T * N
         self._alloc(idx.numel())
+        self._mirrors_valid = False
         stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
         obs = st.observations.view(B, -1)
         cobs = st.privileged_observations.view(B, -1) if st.privileged_observations is not None else None
@@ -473,7 +478,9 @@ class FusedPPOUpdate:
         fused = self.lgx_gemm
         X = Xc = self.X
         if fused:
-            chk(lib.lgx_copy2d(self.copy_jobs, len(self.copy_jobs), stream), "copy2d")
+            if not self._mirrors_valid:   # (afterwards lgx_adam_clip_mirror keeps the copies current)
+                chk(lib.lgx_copy2d(self.copy_jobs, len(self.copy_jobs), stream), "copy2d")
+                self._mirrors_valid = True
             if xs is None:
                 chk(lib.lgx_ppo_gather_rows_padded(_vp(obs), _vp(self.Xp), _vp(idx), M, obs.shape[1], self.Kp,
                                                    stream), "gather")
@@ -527,8 +534,9 @@ class FusedPPOUpdate:
         chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
         adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"   # (single process: in the loss call)
         # ---- backward
-        chk(lib.lgx_head_bwd(_vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc), _vp(self.Y[L - 1]), M, A, h[-1],
-                             _vp(self.head_parts), stream), "head_bwd")
+        # (+ the loss finalize on one extra workgroup of the same launch)
+        chk(lib.lgx_head_bwd_finalize(C.byref(args), _vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc),
+                                      _vp(self.Y[L - 1]), M, A, h[-1], _vp(self.head_parts), stream), "head_bwd")
         dZ = self.Y[L - 1]                           # dZ of the last hidden layer (in place)
         for k in range(L - 1, 0, -1):
             # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
@@ -557,6 +565,12 @@ class FusedPPOUpdate:
                 chk(lib.lgx_ppo_adapt_lr(C.c_void_p(self.g_comm.data_ptr() + 4 * self.n), grad_scale,
                                          _vp(self.optimizer.lr_dev), ppo.desired_kl, stream), "adapt_lr")
         o = self.optimizer
-        chk(lib.lgx_adam_clip(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n, _vp(self.norm_parts),
-                              self.norm_parts.numel(), grad_scale, ppo.max_grad_norm, _vp(o.lr_dev), _vp(o.step_dev),
-                              o.betas[0], o.betas[1], o.eps, stream), "adam")
+        if fused:   # the step also refreshes the GEMM weight copies (padded W1, transposed W2..)
+            chk(lib.lgx_adam_clip_mirror(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n,
+                                         _vp(self.norm_parts), self.norm_parts.numel(), grad_scale, ppo.max_grad_norm,
+                                         _vp(o.lr_dev), _vp(o.step_dev), o.betas[0], o.betas[1], o.eps, self.copy_jobs,
+                                         len(self.copy_jobs), stream), "adam")
+        else:
+            chk(lib.lgx_adam_clip(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n,
+                                  _vp(self.norm_parts), self.norm_parts.numel(), grad_scale, ppo.max_grad_norm,
+                                  _vp(o.lr_dev), _vp(o.step_dev), o.betas[0], o.betas[1], o.eps, stream), "adam")

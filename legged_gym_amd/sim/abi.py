@@ -106,7 +106,7 @@ class LgxPpoLossArgs(C.Structure):
         (n, C.c_void_p) for n in ("idx", "mu_raw", "v_raw", "b4a", "b4c", "std", "actions", "old_logp", "old_mu",
                                   "old_sigma", "advantages", "target_values", "returns", "d_mu", "d_v", "partials",
                                   "g_std", "g_b4a", "g_b4c", "stats", "lr")] + [("desired_kl", C.c_double)] + [
-        (n, C.c_void_p) for n in ("head_in", "W4a", "W4c")] + [("hidden", i32), ("pad_", i32)]
+        (n, C.c_void_p) for n in ("head_in", "W4a", "W4c")] + [("hidden", i32), ("defer_finalize", i32)]
 
 
 class LgxReduceJob(C.Structure):
@@ -182,6 +182,7 @@ def declare(lib, prefix="lgx"):
             "ppo_adapt_lr": (C.c_int, [vp, C.c_float, vp, C.c_double, vp]),
             "head_bwd_partials_floats": (i64, [i64, i32, i32]),
             "head_bwd": (C.c_int, [vp, vp, vp, vp, vp, i64, i32, i32, vp, vp]),
+            "head_bwd_finalize": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp, vp, vp, vp, vp, i64, i32, i32, vp, vp]),
             "colsum_partials_floats": (i64, [i64, i32, i32]),
             "elu_bwd_colsum": (C.c_int, [vp, vp, i64, i32, i32, vp, vp]),
             "reduce_slices": (C.c_int, [C.POINTER(LgxReduceJob), i32, vp]),
@@ -191,6 +192,8 @@ def declare(lib, prefix="lgx"):
             "ppo_gather_rows_padded": (C.c_int, [vp, vp, vp, i64, i32, i32, vp]),
             "adam_clip": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
                                     C.c_float, C.c_float, vp]),
+            "adam_clip_mirror": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
+                                           C.c_float, C.c_float, C.POINTER(LgxCopy2dJob), i32, vp]),
         })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}")
@@ -204,8 +207,8 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
-            "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
-            "lgx_reduce_slices", "lgx_adam_clip", "lgx_ppo_act", "lgx_ppo_store",
+            "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
+            "lgx_reduce_slices", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded"]
 
 
