@@ -214,11 +214,11 @@ def main():
     runner.learn(args.warmup)
     gc.collect()
     gc.disable()   # no collector pauses inside the timed region (host-side Python only)
-    timing_period = int(os.environ.get("LGX_BENCH_KERNEL_TIMING", "1"))   # time every k-th env step (0: off)
+    timing_period = int(os.environ.get("LGX_BENCH_KERNEL_TIMING", "8"))   # time every k-th env step (0: off)
     lib.lgx_profile_enable(handle, timing_period)
     fused = getattr(runner.alg, "_fused", None)
     if fused is not None:   # HIP events around the PPO-update GEMM launches of every k-th minibatch
-        fused.time_gemms(int(os.environ.get("LGX_BENCH_GEMM_TIMING", "5")))
+        fused.time_gemms(int(os.environ.get("LGX_BENCH_GEMM_TIMING", "7")))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
