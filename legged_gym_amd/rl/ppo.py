@@ -99,7 +99,12 @@ class PPO:
         launch_forward(descs, 2, C.c_void_p(main.cuda_stream))   # actor and critic in one launch
         if getattr(self, "_act_out", None) is None or self._act_out.shape != mean.shape:
             self._act_out = torch.empty_like(mean)
-        noise = torch.randn_like(mean)            # Normal.sample's draws (torch generator, as upstream)
+        # Normal.sample's standard-normal draws (torch generator): one launch per rollout for all
+        # of its steps instead of one per step
+        T = st.num_transitions_per_env
+        if s == 0 or getattr(self, "_noise", None) is None or self._noise.shape != (T,) + tuple(mean.shape):
+            self._noise = torch.randn((T,) + tuple(mean.shape), device=mean.device)
+        noise = self._noise[s]
         a = abi.LgxPpoActArgs()
         a.num_envs, a.num_actions, a.num_obs = mean.shape[0], mean.shape[1], obs.shape[1]
         a.mu, a.value, a.std, a.noise = mean.data_ptr(), None, self.actor_critic.std.data_ptr(), noise.data_ptr()

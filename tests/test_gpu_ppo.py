@@ -153,7 +153,7 @@ def test_fused_rollout_act_and_store(gpu):
         ac = fus.actor_critic
         mean, value = ac.actor(obs), ac.critic(obs)
         torch.manual_seed(5)
-        noise = torch.randn_like(mean)
+        noise = torch.randn((T,) + tuple(mean.shape), device=mean.device)[0]   # one draw per rollout, row 0
         ref_a = mean + ac.std * noise
         ref_logp = Normal(mean, ac.std.expand_as(mean)).log_prob(ref_a).sum(-1)
     assert torch.allclose(actions, ref_a, atol=1e-4, rtol=1e-4)
