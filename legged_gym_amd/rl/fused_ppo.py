@@ -201,7 +201,15 @@ class FusedPPOUpdate:
             return
         dev, h, A = self.dev, self.hidden, self.A
         self.M = M
-        self.S = self.SPLITS if M % self.SPLITS == 0 else 1
+        # split-K row slices of each layer's dW GEMM (library bmm over slices, partials reduced in
+        # lgx_reduce_slices): enough output tiles to fill the CUs. LGX_PPO_SPLITS="s1,s2,..." per layer
+        env = os.environ.get("LGX_PPO_SPLITS")
+        want = [int(x) for x in env.split(",")] if env else []
+        self.Sk = []
+        for k in range(self.L):
+            sk = want[k] if k < len(want) else self.SPLITS
+            self.Sk.append(sk if sk > 0 and M % sk == 0 else 1)
+        self.S = self.Sk[0]
         sep = self._separate_critic_obs()
         if self.lgx_gemm:   # K of layer 1 padded to the GEMM's K step with zero columns
             ks = abi.GEMM_K_STEP
@@ -219,9 +227,9 @@ class FusedPPOUpdate:
         self.V = torch.empty(M, 1, device=dev)
         self.dMU = torch.empty(M, A, device=dev)
         self.dV = torch.empty(M, device=dev)
-        S = self.S
-        self.P = [torch.empty(2, S, h[0], self.num_obs, device=dev)] + \
-                 [torch.empty(2 * S, h[k], h[k - 1], device=dev) for k in range(1, self.L)]
+        Sk = self.Sk
+        self.P = [torch.empty(2, Sk[0], h[0], self.num_obs, device=dev)] + \
+                 [torch.empty(2 * Sk[k], h[k], h[k - 1], device=dev) for k in range(1, self.L)]
         self.loss_parts = torch.empty(int(self.lib.lgx_ppo_loss_partials_floats(M, A)), device=dev)
         self.head_parts = torch.empty(int(self.lib.lgx_head_bwd_partials_floats(M, A, h[-1])), device=dev)
         if self.lgx_gemm:
@@ -318,10 +326,11 @@ class FusedPPOUpdate:
                 slice_stride, dst_stride
             jobs.append(j)
         n1 = h[0] * self.num_obs
-        job(self.P[0], self.Wg[0], n1, 2, S * n1, S, n1, n1)                        # dW1 (actor, critic)
+        Sk = self.Sk
+        job(self.P[0], self.Wg[0], n1, 2, Sk[0] * n1, Sk[0], n1, n1)                # dW1 (actor, critic)
         for k in range(1, self.L):
             nk = h[k] * h[k - 1]
-            job(self.P[k], self.Wg[k], nk, 2, S * nk, S, nk, nk)                    # dW_k stacked
+            job(self.P[k], self.Wg[k], nk, 2, Sk[k] * nk, Sk[k], nk, nk)            # dW_k stacked
         nh = (A + 1) * h[-1] + 2 * h[-1]
         hchunks = self.head_parts.numel() // nh                                     # per-chunk partial rows
         job(self.head_parts, self.Wg[self.L], (A + 1) * h[-1], 1, 0, hchunks, nh, 0)  # dW head (actor | critic)
@@ -540,7 +549,8 @@ class FusedPPOUpdate:
         dZ = self.Y[L - 1]                           # dZ of the last hidden layer (in place)
         for k in range(L - 1, 0, -1):
             # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
-            torch.bmm(dZ.view(2 * S, M // S, h[k]).transpose(1, 2), self.Y[k - 1].view(2 * S, M // S, h[k - 1]),
+            Sl = self.Sk[k]
+            torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2), self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]),
                       out=self.P[k])
             if fused:
                 self._gemm(self.gemm_bwd[k], stream)
