@@ -57,6 +57,7 @@ struct GemmArgs {
   const float* bias;
   const float* Y;
   float* partials;
+  int32_t prio;   // raise the wave priority while issuing a stage's MFMAs (s_setprio)
 };
 
 __device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : __expf(x) - 1.f; }  // v_exp_f32
@@ -366,7 +367,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) gemm_nt_kernel(GemmA
       float* nxt = lds + ((t + 1) & 1) * 2 * TILE_FLOATS;
       stage_load<NW>(st, A, B, o, K, (t + 1) * BK, c);
       __builtin_amdgcn_sched_barrier(0);  // loads issued before the MFMAs they overlap
+      if (g.prio) __builtin_amdgcn_s_setprio(1);
       stage_mma<NW>(cur, cur + TILE_FLOATS, wm, wn, r, h, acc);
+      if (g.prio) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       stage_store<NW>(st, nxt, nxt + TILE_FLOATS, K, (t + 1) * BK, tid);
       __syncthreads();
@@ -376,7 +379,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) gemm_nt_kernel(GemmA
       row_offs<NW>(o, g.lda, Tn.mt * BM, g.M, g.ldb, Tn.nt * BN, tid);
       stage_load<NW>(st, g.A + Tn.z * g.sa, g.B + Tn.z * g.sb, o, K, 0, c);
       __builtin_amdgcn_sched_barrier(0);
+      if (g.prio) __builtin_amdgcn_s_setprio(1);
       stage_mma<NW>(cur, cur + TILE_FLOATS, wm, wn, r, h, acc);
+      if (g.prio) __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
       __syncthreads();
     }
@@ -459,8 +464,12 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
     return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: operand too large for 32-bit row offsets");
   const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
   if (tiles > (1ll << 31) - 1) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too large");
+  static const int prio = [] {  // A/B switch LGX_GEMM_PRIO=0/1 (s_setprio around the MFMA stages)
+    const char* e = getenv("LGX_GEMM_PRIO");
+    return e ? atoi(e) : 1;
+  }();
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
-             a.partials};
+             a.partials, prio};
   // persistent: 2 workgroups per CU (LDS-bound), a multiple of 8 (XCD tile ranges)
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
