@@ -228,7 +228,11 @@ class FusedPPOUpdate:
         self.dMU = torch.empty(M, A, device=dev)
         self.dV = torch.empty(M, device=dev)
         Sk = self.Sk
-        self.P = [torch.empty(2, Sk[0], h[0], self.num_obs, device=dev)] + \
+        # layer-1 dW partials: one [2, S, h0, K] block, or (actor, critic) blocks when the critic's
+        # (privileged) input width differs
+        p0 = (torch.empty(2, Sk[0], h[0], self.num_obs, device=dev) if self.num_cobs == self.num_obs else
+              (torch.empty(Sk[0], h[0], self.num_obs, device=dev), torch.empty(Sk[0], h[0], self.num_cobs, device=dev)))
+        self.P = [p0] + \
                  [torch.empty(2 * Sk[k], h[k], h[k - 1], device=dev) for k in range(1, self.L)]
         self.loss_parts = torch.empty(int(self.lib.lgx_ppo_loss_partials_floats(M, A)), device=dev)
         self.head_parts = torch.empty(int(self.lib.lgx_head_bwd_partials_floats(M, A, h[-1])), device=dev)
@@ -327,7 +331,12 @@ class FusedPPOUpdate:
             jobs.append(j)
         n1 = h[0] * self.num_obs
         Sk = self.Sk
-        job(self.P[0], self.Wg[0], n1, 2, Sk[0] * n1, Sk[0], n1, n1)                # dW1 (actor, critic)
+        if isinstance(self.P[0], tuple):                                             # dW1 actor, critic
+            n1c = h[0] * self.num_cobs
+            job(self.P[0][0], self.Wg[0], n1, 1, 0, Sk[0], n1, 0)
+            job(self.P[0][1], self.Wg[0] + n1, n1c, 1, 0, Sk[0], n1c, 0)
+        else:
+            job(self.P[0], self.Wg[0], n1, 2, Sk[0] * n1, Sk[0], n1, n1)            # dW1 (actor, critic)
         for k in range(1, self.L):
             nk = h[k] * h[k - 1]
             job(self.P[k], self.Wg[k], nk, 2, Sk[k] * nk, Sk[k], nk, nk)            # dW_k stacked

@@ -20,9 +20,11 @@ pytestmark = pytest.mark.gpu
 T, N, OBS, ACT = 6, 1024, 235, 12
 
 
-def make_pair(schedule="adaptive"):
+def make_pair(schedule="adaptive", cobs=None):
+    """Reference (autograd) and fused PPO on identical storage; cobs = privileged critic
+    observation width (None: the critic reads the actor's observations)."""
     torch.manual_seed(0)
-    ac = ActorCritic(OBS, OBS, ACT, [512, 256, 128], [512, 256, 128])
+    ac = ActorCritic(OBS, cobs or OBS, ACT, [512, 256, 128], [512, 256, 128])
     ac2 = copy.deepcopy(ac)
     kw = dict(num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95, value_loss_coef=1.0,
               entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0, schedule=schedule, desired_kl=0.01,
@@ -31,7 +33,7 @@ def make_pair(schedule="adaptive"):
     fus = PPO(ac2, use_fused_update=True, **kw)
     assert fus._fused is not None and ref._fused is None
     for p in (ref, fus):
-        p.init_storage(N, T, [OBS], [None], [ACT])
+        p.init_storage(N, T, [OBS], [cobs], [ACT])
     g = torch.Generator(device="cuda:0").manual_seed(3)
     st = ref.storage
     st.observations.copy_(torch.randn(T, N, OBS, device="cuda:0", generator=g))
@@ -42,6 +44,9 @@ def make_pair(schedule="adaptive"):
     st.actions_log_prob.copy_(torch.randn(T, N, 1, device="cuda:0", generator=g) * 0.3 - 17)
     st.mu.copy_(torch.randn(T, N, ACT, device="cuda:0", generator=g) * 0.1)
     st.sigma.copy_(torch.rand(T, N, ACT, device="cuda:0", generator=g) * 0.5 + 0.75)
+    if cobs:
+        st.privileged_observations.copy_(torch.randn(T, N, cobs, device="cuda:0", generator=g))
+        fus.storage.privileged_observations.copy_(st.privileged_observations)
     st.step = T
     for name in ("observations", "actions", "rewards", "dones", "values", "actions_log_prob", "mu", "sigma"):
         getattr(fus.storage, name).copy_(getattr(st, name))
@@ -57,9 +62,10 @@ def autograd_grads(ref, idx):
     B = T * N
     ac = ref.actor_critic
     obs = st.observations.view(B, -1)[idx]
+    cobs = st.privileged_observations.view(B, -1)[idx] if st.privileged_observations is not None else obs
     ac.act(obs)
     logp = ac.get_actions_log_prob(st.actions.view(B, -1)[idx])
-    value = ac.evaluate(obs)
+    value = ac.evaluate(cobs)
     ent = ac.entropy
     ratio = torch.exp(logp - st.actions_log_prob.view(B)[idx])
     adv = st.advantages.view(B)[idx]
@@ -85,6 +91,16 @@ def test_fused_minibatch_gradient_matches_autograd(gpu):
         assert ((a - b).abs() <= tol).all(), (n, (a - b).abs().max().item(), b.abs().max().item())
 
 
+def test_fused_minibatch_gradient_privileged_critic(gpu):
+    ref, fus = make_pair(cobs=252)
+    idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
+    gref = autograd_grads(ref, idx)
+    fus._fused.gradients(idx)
+    for n, p in fus.actor_critic.named_parameters():
+        a, b = p.grad, gref[n]
+        assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), n
+
+
 def test_fused_minibatch_gradient_library_heads(gpu, monkeypatch):
     """The output layers on library GEMMs (LGX_PPO_HEAD_IN_LOSS=0) instead of inside lgx_ppo_loss."""
     monkeypatch.setenv("LGX_PPO_HEAD_IN_LOSS", "0")
@@ -98,9 +114,11 @@ def test_fused_minibatch_gradient_library_heads(gpu, monkeypatch):
         assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), n
 
 
-@pytest.mark.parametrize("schedule", ["adaptive", "fixed"])
-def test_fused_update_matches_autograd_update(gpu, schedule):
-    ref, fus = make_pair(schedule)
+@pytest.mark.parametrize("schedule,cobs", [("adaptive", None), ("fixed", None), ("adaptive", 252)])
+def test_fused_update_matches_autograd_update(gpu, schedule, cobs):
+    """Full update (one gather of all minibatch rows, Adam-maintained GEMM weight copies); cobs:
+    privileged critic observations of another width (two layer-1 inputs and GEMM launches)."""
+    ref, fus = make_pair(schedule, cobs)
     torch.manual_seed(11)
     vl_r, sl_r = ref.update()
     torch.manual_seed(11)
