@@ -42,7 +42,8 @@ def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
 PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
 PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_ppo_kernels.json")
 GEMM_KERNELS = {1: "gemm_nt_kernel<8, 1>", 2: "gemm_nt_kernel<8, 2>"}
-GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: layer-1 forward of actor and critic (K = num_obs padded to 256)",
+GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "
+                 "to 256, 512->256, 256->128)",
               2: "lgx_gemm_nt LGX_GEMM_DELU_COLSUM: backward dA of the hidden layers (512x256 and 256x128 weights)"}
 
 
@@ -294,10 +295,11 @@ def main():
             "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K; "
                     "HIP events around every launch of every k-th minibatch (LGX_BENCH_GEMM_TIMING); traffic = "
                     "2 FETCH_SIZE + WRITE_SIZE per launch from profiles/r01_pmc_ppo_kernels.json"})
-    kernels = {n: {"avg_ms": round(a, 4), "launches": int(c), "share_of_iteration": round(m / args.steps / it_ms, 4)}
-               for n, a, c, m in zip(names, avg, cnt, ms)}
+    kernels = {n: {"avg_ms": round(a, 4), "launches_timed": int(c),
+                   "share_of_iteration": round(a * steps_per_iter / it_ms, 4) if c else None}
+               for n, a, c in zip(names, avg, cnt)}
     # `roofline` = the lgx kernel with the largest share of the iteration (the others follow it)
-    phys_share = ms[0] / args.steps / it_ms
+    phys_share = avg[0] * steps_per_iter / it_ms      # one launch per env step (timing is sampled)
     roof["share_of_iteration"] = phys_share
     cands = [roof] + gemm_roofs
     cands.sort(key=lambda r: -r.get("share_of_iteration", 0.0))

@@ -6,6 +6,7 @@ Per minibatch (M rows), on one stream, no host synchronisation:
   first minibatch of an update; afterwards the Adam step writes these copies (lgx_adam_clip_mirror)
   gather obs rows (lgx_ppo_gather_rows_padded, K padded to a multiple of 16)
   hidden layers: lgx_gemm_nt with the bias + ELU epilogue, {actor, critic} batched in one launch
+                 (LGX_PPO_GEMM=auto: library GEMM + lgx_bias_act for layers 2..L)
   heads + loss: lgx_ppo_loss = output layers (in-kernel dot products), log-prob / ratio / clipped surrogate / clipped value loss / entropy
          / KL and the analytic gradient w.r.t. mu, value, std, head biases; its finalize applies the
          device-side adaptive schedule (data-parallel: lgx_ppo_adapt_lr after the gradient
@@ -184,10 +185,11 @@ class FusedPPOUpdate:
         params = list(ac.parameters())
         self.optimizer = FlatAdam(params, self.flat_p, self.flat_g, ppo.learning_rate)
         import os
-        # LGX_PPO_GEMM: "auto" (default) = lgx_gemm_nt where it measured faster than library GEMM +
-        # epilogue pass on MI355X (layer-1 forward, every backward dA); "lgx" = every hidden-layer
-        # GEMM; "lib" = none
-        mode = os.environ.get("LGX_PPO_GEMM", "auto")
+        # LGX_PPO_GEMM: "lgx" (default) = every hidden-layer forward and backward dA on lgx_gemm_nt
+        # (epilogues fused; measured ~1 % faster per iteration on MI355X than "auto"); "auto" =
+        # lgx_gemm_nt for the layer-1 forward and the dA products, library GEMM + lgx_bias_act for
+        # the other forwards; "lib" = none
+        mode = os.environ.get("LGX_PPO_GEMM", "lgx")
         self.lgx_gemm = all(hk % abi.GEMM_TILE_N == 0 for hk in self.hidden) and mode != "lib"
         self.lgx_fwd_layers = set(range(self.L)) if mode == "lgx" else {0}
         self.norm_parts = torch.zeros(256, device=self.dev)
@@ -306,6 +308,8 @@ class FusedPPOUpdate:
                             h[k] * h[k - 1], self.Y[k], h[k], h[k - 1], 2, abi.GEMM_BIAS_ELU,
                             bias=fp.data_ptr() + f4 * self.bo[k]))
         self.gemm_fwd = fwd
+        # algorithmic K of each launch (layer 1: the unpadded input width) for the bench's roofline
+        self.k_alg = {id(g): k for g, k in zip(fwd[0], [self.num_obs, self.num_cobs])}
         bwd = {}
         for k in range(L - 1, 0, -1):   # dZ_{k-1} = (dZ_k W_k) * elu'(Y_{k-1}); dZ_{L-1} lives in Y[L-1]
             dz = self.Y[L - 1] if k == L - 1 else self.D[k]
@@ -470,7 +474,7 @@ class FusedPPOUpdate:
         if rec:
             e1.record()
             # algorithmic FLOP: the unpadded K of layer 1 (num_obs), not the zero-padded columns
-            k = self.num_obs if g.K == self.Kp else (self.num_cobs if g.K == getattr(self, "Kcp", -1) else g.K)
+            k = self.k_alg.get(id(g), g.K)
             self._t_events.append((g.epi, 2.0 * g.M * g.N * k * g.batch, e0, e1))
 
     def gemm_timings(self):

@@ -91,6 +91,21 @@ def test_fused_minibatch_gradient_matches_autograd(gpu):
         assert ((a - b).abs() <= tol).all(), (n, (a - b).abs().max().item(), b.abs().max().item())
 
 
+@pytest.mark.parametrize("mode", ["auto", "lib"])
+def test_fused_minibatch_gradient_gemm_modes(gpu, monkeypatch, mode):
+    """LGX_PPO_GEMM=auto (library GEMM + lgx_bias_act for layers 2..L) and =lib (library GEMMs
+    with lgx_bias_act / lgx_elu_bwd_colsum everywhere) against autograd."""
+    monkeypatch.setenv("LGX_PPO_GEMM", mode)
+    ref, fus = make_pair()
+    idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
+    gref = autograd_grads(ref, idx)
+    fus._fused.gradients(idx)
+    assert fus._fused.lgx_gemm == (mode != "lib")
+    for n, p in fus.actor_critic.named_parameters():
+        a, b = p.grad, gref[n]
+        assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), (mode, n)
+
+
 def test_fused_minibatch_gradient_privileged_critic(gpu):
     ref, fus = make_pair(cobs=252)
     idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
