@@ -483,6 +483,11 @@ int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, floa
 /* lgx_ppo_gather_rows into rows of dst_ld floats, columns width .. dst_ld-1 zero-filled */
 int lgx_ppo_gather_rows_padded(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width,
                                int32_t dst_ld, void* stream);
+/* lgx_ppo_gather_rows_padded with every block of `block` rows written twice, back to back
+ * (dst = [rows / block][2][block][dst_ld]): per minibatch one [2, M, dst_ld] operand for the
+ * batched actor + critic layer-1 weight-gradient GEMM over the same input rows */
+int lgx_ppo_gather_rows_padded_dup(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width,
+                                   int32_t dst_ld, int64_t block, void* stream);
 
 #ifdef __cplusplus
 }

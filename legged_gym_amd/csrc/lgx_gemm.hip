@@ -433,16 +433,24 @@ __global__ void __launch_bounds__(256) copy2d_kernel(Copy2dJobs J) {
   }
 }
 
-// dst[r][0:width] = src[idx[r]][0:width], dst[r][width:dst_ld] = 0: one row per wave
+// dst[r][0:width] = src[idx[r]][0:width], dst[r][width:dst_ld] = 0: one row per wave.
+// dup > 0: blocks of `dup` rows are written twice, back to back (dst row (r / dup) * 2 dup +
+// r % dup and `dup` rows further): one [2, dup, dst_ld] operand per block for a batched GEMM of
+// two networks over the same rows.
 __global__ void __launch_bounds__(256) gather_rows_padded_kernel(const float* __restrict__ src, float* __restrict__ dst,
                                                                  const int64_t* __restrict__ idx, int64_t rows,
-                                                                 int32_t width, int32_t dst_ld) {
+                                                                 int32_t width, int32_t dst_ld, int64_t dup) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   if (r >= rows) return;
   const float* s = src + idx[r] * width;
-  float* d = dst + r * dst_ld;
-  for (int c = lane; c < dst_ld; c += 64) d[c] = c < width ? s[c] : 0.f;
+  const int64_t dr = dup > 0 ? (r / dup) * 2 * dup + r % dup : r;
+  float* d = dst + dr * dst_ld;
+  for (int c = lane; c < dst_ld; c += 64) {
+    const float v = c < width ? s[c] : 0.f;
+    d[c] = v;
+    if (dup > 0) d[dup * dst_ld + c] = v;
+  }
 }
 }  // namespace
 
@@ -519,6 +527,15 @@ extern "C" int lgx_ppo_gather_rows_padded(const float* src, float* dst, const in
   if (!src || !dst || !idx || rows <= 0 || width <= 0 || dst_ld < width)
     return lgx_fail(LGX_EINVAL, "lgx_ppo_gather_rows_padded: bad args");
   hipLaunchKernelGGL(gather_rows_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, LGX_STREAM(stream),
-                     src, dst, idx, rows, width, dst_ld);
+                     src, dst, idx, rows, width, dst_ld, (int64_t)0);
   return lgx_hip_status("lgx_ppo_gather_rows_padded");
+}
+
+extern "C" int lgx_ppo_gather_rows_padded_dup(const float* src, float* dst, const int64_t* idx, int64_t rows,
+                                              int32_t width, int32_t dst_ld, int64_t block, void* stream) {
+  if (!src || !dst || !idx || rows <= 0 || width <= 0 || dst_ld < width || block <= 0 || rows % block)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_gather_rows_padded_dup: bad args (rows % block)");
+  hipLaunchKernelGGL(gather_rows_padded_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, LGX_STREAM(stream),
+                     src, dst, idx, rows, width, dst_ld, block);
+  return lgx_hip_status("lgx_ppo_gather_rows_padded_dup");
 }

@@ -387,9 +387,13 @@ class FusedPPOUpdate:
         for _ in range(ppo.num_learning_epochs):
             for i in range(nmb):
                 idx = indices[i * M:(i + 1) * M]
-                self._minibatch(idx, obs, cobs, args, stream,
-                                xs=None if xs is None else tuple(x[i * M:(i + 1) * M] if x is not None else None
-                                                                 for x in xs))
+                if xs is None:
+                    mx = None
+                elif self.dw1_batched:        # [2, M, Kp] block: the same rows for actor and critic
+                    mx = (xs[0][i], None, xs[0][i])
+                else:
+                    mx = tuple(x[i * M:(i + 1) * M] if x is not None else None for x in xs)
+                self._minibatch(idx, obs, cobs, args, stream, xs=mx)
         n = ppo.num_learning_epochs * nmb
         s = self.stats.tolist()   # the one host synchronisation of the update
         ppo.learning_rate = float(self.optimizer.lr_dev.item())
@@ -397,6 +401,17 @@ class FusedPPOUpdate:
         return s[2] / n, s[1] / n
 
     def _gather_all(self, indices, obs, cobs, rows, stream):
+        # one input for both networks: rows gathered twice per minibatch ([nmb, 2, M, Kp]) so the
+        # layer-1 weight gradients of actor and critic are ONE batched split-K GEMM
+        self.dw1_batched = (cobs is None and self.num_obs == self.num_cobs and self.Xcp is None
+                            and os.environ.get("LGX_PPO_DW1_BATCHED", "1") != "0")
+        if self.dw1_batched:
+            M = self.M
+            if getattr(self, "Xall2", None) is None or self.Xall2.shape[0] * M != rows:
+                self.Xall2 = torch.zeros(rows // M, 2, M, self.Kp, device=self.dev)
+            self.check(self.lib.lgx_ppo_gather_rows_padded_dup(_vp(obs), _vp(self.Xall2), _vp(indices), rows,
+                                                               obs.shape[1], self.Kp, M, stream), "gather")
+            return self.Xall2, None
         if getattr(self, "Xall", None) is None or self.Xall.shape[0] != rows:
             self.Xall = torch.zeros(rows, self.Kp, device=self.dev)     # padding columns stay zero
             self.Xcall = torch.zeros(rows, self.Kcp, device=self.dev) if self.Xcp is not None else None
@@ -511,7 +526,9 @@ class FusedPPOUpdate:
                                                        self.Kcp, stream), "gather")
                 xp, xcp = self.Xp, self.Xcp
             else:
-                xp, xcp = xs
+                xp, xcp = xs[0], xs[1]
+                if len(xs) > 2:                 # [2, M, Kp]: net 0's copy feeds the forward
+                    xp = xs[0][0]
             X = Xc = xp[:, :self.num_obs]
             if cobs is not None:
                 Xc = xcp[:, :self.num_cobs]
@@ -572,8 +589,12 @@ class FusedPPOUpdate:
                 chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
                                            _vp(self.col_parts[k - 1]), stream), "elu_bwd")
             dZ = self.D[k - 1]
-        torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
-        torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
+        if xs is not None and len(xs) > 2:    # one batched GEMM: 2 networks x S row slices
+            x2 = xs[2].view(2 * S, M // S, self.Kp)[:, :, :self.num_obs]
+            torch.bmm(dZ.view(2 * S, M // S, h[0]).transpose(1, 2), x2, out=self.P[0].view(2 * S, h[0], self.num_obs))
+        else:
+            torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
+            torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
         chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
         if not apply:
             return

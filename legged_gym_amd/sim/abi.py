@@ -190,6 +190,7 @@ def declare(lib, prefix="lgx"):
             "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
             "copy2d": (C.c_int, [C.POINTER(LgxCopy2dJob), i32, vp]),
             "ppo_gather_rows_padded": (C.c_int, [vp, vp, vp, i64, i32, i32, vp]),
+            "ppo_gather_rows_padded_dup": (C.c_int, [vp, vp, vp, i64, i32, i32, i64, vp]),
             "adam_clip": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
                                     C.c_float, C.c_float, vp]),
             "adam_clip_mirror": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
@@ -209,7 +210,8 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
             "lgx_reduce_slices", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
-            "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded"]
+            "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
+            "lgx_ppo_gather_rows_padded_dup"]
 
 
 def check_layout(sizes_fn, n=10):
