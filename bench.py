@@ -215,7 +215,7 @@ def main():
     runner.learn(args.warmup)
     gc.collect()
     gc.disable()   # no collector pauses inside the timed region (host-side Python only)
-    timing_period = int(os.environ.get("LGX_BENCH_KERNEL_TIMING", "8"))   # time every k-th env step (0: off)
+    timing_period = int(os.environ.get("LGX_BENCH_KERNEL_TIMING", "7"))   # time every k-th env step (0: off); 7 is coprime with the 24-step rollout, so every step position (the cold first one included) is sampled in proportion
     lib.lgx_profile_enable(handle, timing_period)
     fused = getattr(runner.alg, "_fused", None)
     if fused is not None:   # HIP events around the PPO-update GEMM launches of every k-th minibatch
