@@ -309,7 +309,7 @@ int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, con
  * minibatch step.  Activations are net-major [2 (actor, critic), M, H]; the GEMMs between
  * these calls are library GEMMs issued by the host.  All pointers are device pointers. */
 #define LGX_PPO_MAX_ACTIONS 16
-#define LGX_MAX_REDUCE_JOBS 8
+#define LGX_MAX_REDUCE_JOBS 16
 
 /* PPO.act + RolloutStorage.add_transitions of one env step: actions = mu + std * noise,
  * log-prob, storage row (st_* point at row t of the [T, N, .] storage tensors). */
@@ -475,7 +475,7 @@ int lgx_copy2d(const lgx_copy2d_job* jobs, int32_t njobs, void* stream);
 
 /* lgx_adam_clip that also writes every updated parameter of the `mirrors` blocks (lgx_copy2d
  * job layout; src = a contiguous block of p) into its derived copy (zero-padded / transposed
- * GEMM operands), replacing the lgx_copy2d pass before the next minibatch; <= 8 mirrors */
+ * GEMM operands), replacing the lgx_copy2d pass before the next minibatch; <= LGX_MAX_REDUCE_JOBS mirrors */
 int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
                          float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1, float beta2,
                          float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors, void* stream);

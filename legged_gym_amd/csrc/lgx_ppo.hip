@@ -402,25 +402,31 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
   const int64_t base = (int64_t)net * rows * H + r0 * H;
   float* P = partials + (int64_t)blockIdx.x * nets * H + net * H;
   const int H4 = H >> 2;
-  // TPB threads = (row lane, column quad): rows are split over TPB / H4 lanes
+  // TPB threads = (row lane, column quad): rows are split over TPB / H4 lanes; widths whose H4
+  // does not divide TPB leave the last TPB % H4 threads idle, widths above TPB walk the column
+  // quads in uniform rounds (every thread reaches every barrier)
   const int lanes_per_row = H4 < TPB ? H4 : TPB;
   const int row_groups = TPB / lanes_per_row;
   const int cq = threadIdx.x % lanes_per_row, rg = threadIdx.x / lanes_per_row;
   __shared__ float4 red[TPB];
-  for (int c4 = cq; c4 < H4; c4 += lanes_per_row) {
+  for (int c0 = 0; c0 < H4; c0 += lanes_per_row) {
+    const int c4 = c0 + cq;
+    const bool active = c4 < H4 && rg < row_groups;
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int rr = rg; rr < nr; rr += row_groups) {
-      int64_t i = (base + (int64_t)rr * H) / 4 + c4;
-      float4 d = reinterpret_cast<float4*>(dA)[i];
-      float4 y = reinterpret_cast<const float4*>(Y)[i];
-      d.x *= elu_grad_from_out(y.x); d.y *= elu_grad_from_out(y.y);
-      d.z *= elu_grad_from_out(y.z); d.w *= elu_grad_from_out(y.w);
-      reinterpret_cast<float4*>(dA)[i] = d;
-      cs.x += d.x; cs.y += d.y; cs.z += d.z; cs.w += d.w;
+    if (active) {
+      for (int rr = rg; rr < nr; rr += row_groups) {
+        int64_t i = (base + (int64_t)rr * H) / 4 + c4;
+        float4 d = reinterpret_cast<float4*>(dA)[i];
+        float4 y = reinterpret_cast<const float4*>(Y)[i];
+        d.x *= elu_grad_from_out(y.x); d.y *= elu_grad_from_out(y.y);
+        d.z *= elu_grad_from_out(y.z); d.w *= elu_grad_from_out(y.w);
+        reinterpret_cast<float4*>(dA)[i] = d;
+        cs.x += d.x; cs.y += d.y; cs.z += d.z; cs.w += d.w;
+      }
     }
     red[threadIdx.x] = cs;
     __syncthreads();
-    if (rg == 0) {
+    if (rg == 0 && c4 < H4) {
       float4 t = red[cq];
       for (int g = 1; g < row_groups; ++g) {
         float4 u = red[g * lanes_per_row + cq];
@@ -501,7 +507,7 @@ struct Mirror {
   float* dst;
   int32_t count, rows, cols, transpose;   // count = batch * rows * cols
 };
-constexpr int MAX_MIRRORS = 8;
+constexpr int MAX_MIRRORS = LGX_MAX_REDUCE_JOBS;
 struct Mirrors {
   Mirror mj[MAX_MIRRORS];
   int32_t n;
@@ -682,9 +688,8 @@ extern "C" int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int3
 
 extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32_t hidden, int32_t nets,
                                   float* partials, void* stream) {
-  if (!dA || !Y || !partials || rows <= 0 || hidden <= 0 || hidden % 4 || nets <= 0 || nets > 2 ||
-      (hidden / 4 < TPB && TPB % (hidden / 4)) || (hidden / 4 > TPB && (hidden / 4) % TPB))
-    return lgx_fail(LGX_EINVAL, "lgx_elu_bwd_colsum: bad args (hidden % 4, hidden/4 must divide or be a multiple of 256)");
+  if (!dA || !Y || !partials || rows <= 0 || hidden <= 0 || hidden % 4 || nets <= 0 || nets > 2)
+    return lgx_fail(LGX_EINVAL, "lgx_elu_bwd_colsum: bad args (hidden % 4)");
   int chunks = (int)((rows + CHUNK - 1) / CHUNK);
   hipLaunchKernelGGL(elu_bwd_colsum_kernel, dim3(chunks, nets), dim3(TPB), 0, LGX_STREAM(stream), dA, Y, rows, hidden,
                      nets, partials);

@@ -31,23 +31,45 @@ import torch.nn as nn
 from legged_gym_amd.sim import abi
 
 
-def _use_tuned_gemms():
-    """Load the GEMM solution table tuned on MI355X for the PPO-update shapes (torch TunableOp,
-    rocBLAS / hipBLASLt solutions; regenerate with tools/tune_gemms.sh).  Read-only: shapes that
-    are not in the table run the library default.  LGX_TUNED_GEMMS=0 disables."""
-    import os
-    if os.environ.get("LGX_TUNED_GEMMS", "1") == "0":
-        return
-    import torch.cuda.tunable as tunable
-    from legged_gym_amd import LEGGED_GYM_ROOT_DIR
-    path = os.path.join(LEGGED_GYM_ROOT_DIR, "resources", "tunableop", "ppo_gemms_gfx950.csv")
-    if not os.path.exists(path) or tunable.is_enabled():
-        return
-    tunable.enable(True)
-    tunable.tuning_enable(False)
-    tunable.record_untuned_enable(False)
-    tunable.set_filename(path, insert_device_ordinal=False)
-    tunable.read_file(path)
+class _TunedGemms:
+    """The GEMM solution table tuned on MI355X for the PPO-update shapes (torch TunableOp,
+    rocBLAS / hipBLASLt solutions; regenerate with tools/tune_gemms.sh), scoped: TunableOp is
+    switched on only inside `with` blocks around the update's library GEMMs and restored to the
+    caller's setting afterwards, so other torch GEMMs of the process are unaffected.  Read-only
+    (no tuning, no recording); shapes not in the table run the library
+    default.  LGX_TUNED_GEMMS=0 disables."""
+    _loaded = None
+
+    def __init__(self):
+        self.ok = False
+        if os.environ.get("LGX_TUNED_GEMMS", "1") == "0":
+            return
+        import torch.cuda.tunable as tunable
+        from legged_gym_amd import LEGGED_GYM_ROOT_DIR
+        path = os.path.join(LEGGED_GYM_ROOT_DIR, "resources", "tunableop", "ppo_gemms_gfx950.csv")
+        if not os.path.exists(path):
+            return
+        self.tunable = tunable
+        if _TunedGemms._loaded is None:
+            prev = tunable.is_enabled()
+            tunable.enable(True)
+            tunable.tuning_enable(False)
+            tunable.record_untuned_enable(False)
+            tunable.set_filename(path, insert_device_ordinal=False)
+            _TunedGemms._loaded = bool(tunable.read_file(path))
+            tunable.enable(prev)
+        self.ok = _TunedGemms._loaded
+
+    def __enter__(self):
+        if self.ok:
+            self.prev = self.tunable.is_enabled()
+            self.tunable.enable(True)
+        return self
+
+    def __exit__(self, *exc):
+        if self.ok:
+            self.tunable.enable(self.prev)
+        return False
 
 
 def _vp(t):
@@ -126,14 +148,22 @@ class FusedPPOUpdate:
             return False
         ha = [l.out_features for l in la[:-1]]
         hc = [l.out_features for l in lc[:-1]]
+        L = len(ha)
+        # one lgx_reduce_slices launch takes every gradient block: dW1 (x2 with a privileged critic
+        # of another width), dW_2..L, the head dW, and the bias sums of every hidden layer; the
+        # weight copies the Adam step maintains: padded W1 (x2) + transposed W_2..L
+        sep = la[0].in_features != lc[0].in_features
+        jobs = 2 * L + 1 + int(sep)
+        mirrors = L + int(sep)
         return (ha == hc and all(h % 4 == 0 for h in ha) and ha[-1] <= 1024 and lc[-1].out_features == 1
-                and la[-1].out_features <= abi.PPO_MAX_ACTIONS and ac.std.dim() == 1)
+                and la[-1].out_features <= abi.PPO_MAX_ACTIONS and ac.std.dim() == 1
+                and jobs <= abi.MAX_REDUCE_JOBS and mirrors <= abi.MAX_REDUCE_JOBS)
 
     def __init__(self, ppo):
         from legged_gym_amd.sim import lib as lgxlib
         self.lib = lgxlib.load()
         self.check = lgxlib.check
-        _use_tuned_gemms()
+        self.tuned = _TunedGemms()
         self.ppo = ppo
         ac = ppo.actor_critic
         self.dev = next(ac.parameters()).device
@@ -369,7 +399,10 @@ class FusedPPOUpdate:
         self._alloc(M)
         self._mirrors_valid = False      # parameters may have changed since the last update
         stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
-        self.optimizer.lr_dev.fill_(ppo.learning_rate)
+        if ppo.desired_kl is not None and ppo.schedule == "adaptive":
+            self.optimizer.lr_dev.fill_(ppo.learning_rate)
+        # (fixed schedule: lr_dev keeps the optimizer's lr, i.e. a checkpoint's after load_state_dict,
+        # as torch.optim.Adam's param_groups do)
         self.stats.zero_()
         indices = torch.randperm(nmb * M, requires_grad=False, device=self.dev)   # as rsl_rl's generator
         obs = st.observations.view(B, -1)
@@ -396,8 +429,10 @@ class FusedPPOUpdate:
                 self._minibatch(idx, obs, cobs, args, stream, xs=mx)
         n = ppo.num_learning_epochs * nmb
         s = self.stats.tolist()   # the one host synchronisation of the update
-        ppo.learning_rate = float(self.optimizer.lr_dev.item())
-        self.optimizer.param_groups[0]["lr"] = ppo.learning_rate
+        lr = float(self.optimizer.lr_dev.item())
+        if ppo.desired_kl is not None and ppo.schedule == "adaptive":
+            ppo.learning_rate = lr
+        self.optimizer.param_groups[0]["lr"] = lr
         return s[2] / n, s[1] / n
 
     def _gather_all(self, indices, obs, cobs, rows, stream):
@@ -504,6 +539,10 @@ class FusedPPOUpdate:
 
     @torch.no_grad()
     def _minibatch(self, idx, obs, cobs, args, stream, apply=True, xs=None):
+        with self.tuned:     # TunableOp table on for the library GEMMs of this minibatch only
+            self._minibatch_body(idx, obs, cobs, args, stream, apply, xs)
+
+    def _minibatch_body(self, idx, obs, cobs, args, stream, apply=True, xs=None):
         """One minibatch: rows `idx` of the storage; `xs` = their padded layer-1 inputs already
         gathered (slices of _gather_all's buffers), None = gather here."""
         lib, chk = self.lib, self.check

@@ -10,6 +10,8 @@ global mean, so every rank applies the identical Adam step and N ranks x B envs 
 """
 import ctypes as C
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.optim as optim
@@ -99,12 +101,19 @@ class PPO:
         launch_forward(descs, 2, C.c_void_p(main.cuda_stream))   # actor and critic in one launch
         if getattr(self, "_act_out", None) is None or self._act_out.shape != mean.shape:
             self._act_out = torch.empty_like(mean)
-        # Normal.sample's standard-normal draws (torch generator): one launch per rollout for all
-        # of its steps instead of one per step
+        # Normal.sample's standard-normal draws from torch's generator.  Default: one [N, A] draw
+        # per step, the RNG consumption of rsl_rl's Normal.sample (torch.normal(mu, std) =
+        # normal_(0, 1) * std + mu), so seeded runs draw the same noise as upstream.
+        # LGX_BATCHED_NOISE=1: one [T, N, A] draw per rollout (one launch instead of T; same
+        # distribution, different RNG stream, T*N*A floats kept)
         T = st.num_transitions_per_env
-        if s == 0 or getattr(self, "_noise", None) is None or self._noise.shape != (T,) + tuple(mean.shape):
-            self._noise = torch.randn((T,) + tuple(mean.shape), device=mean.device)
-        noise = self._noise[s]
+        if os.environ.get("LGX_BATCHED_NOISE", "0") == "1":
+            if s == 0 or getattr(self, "_noise", None) is None or self._noise.shape != (T,) + tuple(mean.shape):
+                self._noise = torch.randn((T,) + tuple(mean.shape), device=mean.device)
+            noise = self._noise[s]
+        else:
+            noise = torch.randn(mean.shape, device=mean.device)
+            self._noise = noise   # keep it alive until the act kernel has read it
         a = abi.LgxPpoActArgs()
         a.num_envs, a.num_actions, a.num_obs = mean.shape[0], mean.shape[1], obs.shape[1]
         a.mu, a.value, a.std, a.noise = mean.data_ptr(), None, self.actor_critic.std.data_ptr(), noise.data_ptr()

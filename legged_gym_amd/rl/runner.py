@@ -156,6 +156,9 @@ class OnPolicyRunner:
             self.alg.actor_critic.invalidate_fused()
         if load_optimizer:
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
+            # continue from the checkpoint's learning rate (the adaptive schedule adapts from it;
+            # a fixed schedule keeps it, as torch.optim.Adam's restored param_groups do)
+            self.alg.learning_rate = float(self.alg.optimizer.param_groups[0]["lr"])
         self.current_learning_iteration = d["iter"]
         return d["infos"]
 

@@ -138,7 +138,7 @@ class LgxCopy2dJob(C.Structure):
 
 
 PPO_MAX_ACTIONS = 16
-MAX_REDUCE_JOBS = 8
+MAX_REDUCE_JOBS = 16
 GEMM_PLAIN, GEMM_BIAS_ELU, GEMM_DELU_COLSUM = 0, 1, 2
 GEMM_TILE_M, GEMM_TILE_N, GEMM_K_STEP = 128, 128, 32   # K step: layer-1 rows padded to 1024 B (aligned 128-B lines)
 

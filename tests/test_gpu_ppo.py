@@ -20,11 +20,11 @@ pytestmark = pytest.mark.gpu
 T, N, OBS, ACT = 6, 1024, 235, 12
 
 
-def make_pair(schedule="adaptive", cobs=None):
+def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128)):
     """Reference (autograd) and fused PPO on identical storage; cobs = privileged critic
     observation width (None: the critic reads the actor's observations)."""
     torch.manual_seed(0)
-    ac = ActorCritic(OBS, cobs or OBS, ACT, [512, 256, 128], [512, 256, 128])
+    ac = ActorCritic(OBS, cobs or OBS, ACT, list(hidden), list(hidden))
     ac2 = copy.deepcopy(ac)
     kw = dict(num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95, value_loss_coef=1.0,
               entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0, schedule=schedule, desired_kl=0.01,
@@ -106,6 +106,27 @@ def test_fused_minibatch_gradient_gemm_modes(gpu, monkeypatch, mode):
         assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), (mode, n)
 
 
+@pytest.mark.parametrize("hidden", [(512, 256, 128, 64), (400, 300), (256, 256, 128, 128, 64, 64, 32)])
+def test_fused_other_hidden_stacks(gpu, hidden):
+    """Deeper stacks (more reduction jobs / weight mirrors) and widths that are not multiples of
+    the GEMM tile (library GEMMs + lgx_elu_bwd_colsum at h/4 = 100, 75): minibatch gradient and
+    a full update against autograd."""
+    ref, fus = make_pair(hidden=hidden)
+    idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
+    gref = autograd_grads(ref, idx)
+    fus._fused.gradients(idx)
+    for n, p in fus.actor_critic.named_parameters():
+        a, b = p.grad, gref[n]
+        assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), (hidden, n, (a - b).abs().max().item())
+    ref, fus = make_pair(hidden=hidden)
+    torch.manual_seed(11)
+    vl_r, sl_r = ref.update()
+    torch.manual_seed(11)
+    vl_f, sl_f = fus.update()
+    assert fus.learning_rate == ref.learning_rate
+    assert abs(vl_f - vl_r) <= 1e-4 * abs(vl_r) + 1e-6 and abs(sl_f - sl_r) <= 1e-4 * abs(sl_r) + 1e-6
+
+
 def test_fused_minibatch_gradient_privileged_critic(gpu):
     ref, fus = make_pair(cobs=252)
     idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
@@ -166,9 +187,31 @@ def test_fused_checkpoint_roundtrip(gpu, tmp_path):
     assert torch.equal(fus.optimizer.m, fus2.optimizer.m) and torch.equal(fus.optimizer.v, fus2.optimizer.v)
 
 
-def test_fused_rollout_act_and_store(gpu):
-    """lgx_ppo_act / lgx_ppo_store == PPO.act + process_env_step + add_transitions (torch)."""
+def test_fused_fixed_schedule_keeps_checkpoint_lr(gpu):
+    """schedule='fixed': a restored optimizer lr is the one the next update steps with (as
+    torch.optim.Adam's param_groups after load_state_dict), not the config value."""
+    ref, fus = make_pair("fixed")
+    for p in (ref, fus):
+        sd = p.optimizer.state_dict()
+        sd["param_groups"][0]["lr"] = 3e-4
+        p.optimizer.load_state_dict(sd)
+    torch.manual_seed(11)
+    ref.update()
+    torch.manual_seed(11)
+    fus.update()
+    assert fus.optimizer.param_groups[0]["lr"] == ref.optimizer.param_groups[0]["lr"] == 3e-4
+    assert float(fus._fused.optimizer.lr_dev.item()) == 3e-4
+    for a, b in zip(fus.actor_critic.parameters(), ref.actor_critic.parameters()):
+        assert (a - b).abs().max().item() <= 2 * 8 * 3e-4
+
+
+@pytest.mark.parametrize("batched", [False, True])
+def test_fused_rollout_act_and_store(gpu, monkeypatch, batched):
+    """lgx_ppo_act / lgx_ppo_store == PPO.act + process_env_step + add_transitions (torch).
+    Default: the per-step draw of rsl_rl's Normal.sample (torch.normal(mu, std)), same seed ->
+    same actions; LGX_BATCHED_NOISE=1: one draw per rollout."""
     from torch.distributions import Normal
+    monkeypatch.setenv("LGX_BATCHED_NOISE", "1" if batched else "0")
     _, fus = make_pair()
     st = fus.storage
     st.clear()
@@ -186,8 +229,11 @@ def test_fused_rollout_act_and_store(gpu):
         ac = fus.actor_critic
         mean, value = ac.actor(obs), ac.critic(obs)
         torch.manual_seed(5)
-        noise = torch.randn((T,) + tuple(mean.shape), device=mean.device)[0]   # one draw per rollout, row 0
-        ref_a = mean + ac.std * noise
+        if batched:
+            noise = torch.randn((T,) + tuple(mean.shape), device=mean.device)[0]   # one draw per rollout, row 0
+            ref_a = mean + ac.std * noise
+        else:   # upstream ActorCritic.act: Normal(mean, std).sample()
+            ref_a = Normal(mean, mean * 0. + ac.std).sample()
         ref_logp = Normal(mean, ac.std.expand_as(mean)).log_prob(ref_a).sum(-1)
     assert torch.allclose(actions, ref_a, atol=1e-4, rtol=1e-4)
     assert torch.allclose(st.actions[0], actions)

@@ -13,6 +13,8 @@ import torch
 
 from oracle_backend import make_env
 
+from legged_gym_amd.sim import abi
+
 MASS = {"a1": 12.454, "a1_src": 13.741, "aliengo": 20.638, "anymal_b": 30.6214}
 OBS = {"a1": 235, "a1_src": 235, "aliengo": 48, "anymal_b": 235}
 EXPERIMENT = {"a1": "rough_a1", "a1_src": "rough_a1_src", "aliengo": "rough_aliengo", "anymal_b": "rough_anymal_b"}
@@ -64,3 +66,15 @@ def test_pd_standing(task, lo, hi):
     assert ((z > lo) & (z < hi)).all(), z
     assert (env.projected_gravity[:, 2] < -0.99).all()
     assert not env.reset_buf.any()
+
+
+def test_anymal_refuses_explicit_torques_with_lstm():
+    """explicit_torques + use_actuator_network on ANYmal would be the reference's SEA-LSTM
+    _compute_torques (anymal.py:62-78), which the step kernel does not run: refused loudly."""
+    from types import SimpleNamespace
+    from legged_gym_amd.envs.anymal_c.anymal import Anymal
+    ctl = SimpleNamespace(explicit_torques=True, use_actuator_network=True, control_type="P")
+    with pytest.raises(ValueError):
+        Anymal._control_type(SimpleNamespace(cfg=SimpleNamespace(control=ctl)))
+    ctl.use_actuator_network = False
+    assert Anymal._control_type(SimpleNamespace(cfg=SimpleNamespace(control=ctl))) == abi.CTRL["P"]
