@@ -444,6 +444,14 @@ int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* part
  *                         partials[t][z*N + n] = sum of C over rows 128t .. 128t+127
  * Requirements: N % 128 == 0, K % 4 == 0, A/B 16-byte aligned with lda, ldb, sa, sb % 4 == 0
  * (pad K with zero columns).  sa may be 0 (one input shared by the batch). */
+/* algo: LGX_GEMM_ALGO_DEFAULT = the process default (env LGX_GEMM_ALGO = "split" | "f32",
+ * "split" when unset); LGX_GEMM_ALGO_F32 = v_mfma_f32_32x32x2_f32 (exact f32 fmaf chain);
+ * LGX_GEMM_ALGO_SPLIT_BF16 = each f32 operand split into three RNE bf16 limbs, the six limb
+ * products of order <= 2 on v_mfma_f32_32x32x16_bf16 with f32 accumulation (f32-accurate:
+ * dropped terms and split residues <= ~2^-25 |a b|, below one f32 product rounding) */
+#define LGX_GEMM_ALGO_DEFAULT 0
+#define LGX_GEMM_ALGO_F32 1
+#define LGX_GEMM_ALGO_SPLIT_BF16 2
 #define LGX_GEMM_PLAIN 0
 #define LGX_GEMM_BIAS_ELU 1
 #define LGX_GEMM_DELU_COLSUM 2
@@ -459,9 +467,14 @@ typedef struct lgx_gemm_args {
   const float* bias;            /* [batch][N] (BIAS_ELU) */
   const float* Y;               /* like C (DELU_COLSUM) */
   float* partials;              /* [lgx_gemm_partials_floats(M, N, batch)] (DELU_COLSUM) */
+  int32_t algo;                 /* LGX_GEMM_ALGO_*: how the f32 products are evaluated */
+  int32_t reserved;
+  const uint16_t* Bs;           /* split-bf16 only, optional: B pre-split by lgx_split_bf16 into
+                                   [batch][N][ceil(K/32)][3 limbs][32] bf16 (then B is not read) */
 } lgx_gemm_args;
 int64_t lgx_gemm_partials_floats(int64_t M, int32_t N, int32_t batch);
 int lgx_gemm_nt(const lgx_gemm_args* args, void* stream);
+
 
 /* weight preparation for lgx_gemm_nt: dst[b][r][c] = src[b][r][c] (transpose 0) or
  * dst[b][c][r] = src[b][r][c] (transpose 1), r < rows, c < cols; dst padding is untouched */
@@ -473,9 +486,18 @@ typedef struct lgx_copy2d_job {
 } lgx_copy2d_job;
 int lgx_copy2d(const lgx_copy2d_job* jobs, int32_t njobs, void* stream);
 
+/* GEMM operand pre-split for the split-bf16 path: per job (lgx_copy2d_job), the logical operand
+ * out[b][n][k] = transpose ? src[b][k][n] : src[b][n][k] (bit 0 of `transpose`) written as RNE
+ * bf16 limbs x0 + x1 + x2 at dst[b*dst_bs + n*dst_ld + (k/32)*96 + limb*32 + k%32] (uint16
+ * units; dst_ld >= lgx_split_bf16_elems(1, K)), zero-filled for K <= k < ceil(K/32)*32 */
+int64_t lgx_split_bf16_elems(int32_t n, int32_t k);
+int lgx_split_bf16(const lgx_copy2d_job* jobs, int32_t njobs, void* stream);
+
 /* lgx_adam_clip that also writes every updated parameter of the `mirrors` blocks (lgx_copy2d
  * job layout; src = a contiguous block of p) into its derived copy (zero-padded / transposed
- * GEMM operands), replacing the lgx_copy2d pass before the next minibatch; <= LGX_MAX_REDUCE_JOBS mirrors */
+ * GEMM operands), replacing the lgx_copy2d pass before the next minibatch; <= LGX_MAX_REDUCE_JOBS mirrors.
+ * A mirror with bit 1 of `transpose` set writes the lgx_split_bf16 limb layout instead (bit 0:
+ * transposed), keeping pre-split split-bf16 GEMM operands current */
 int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
                          float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1, float beta2,
                          float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors, void* stream);

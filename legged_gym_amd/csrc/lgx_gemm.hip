@@ -34,100 +34,18 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "lgx_gemm_common.h"
 #include "lgx_internal.h"
 
 #define LGX_STREAM(s) reinterpret_cast<hipStream_t>(s)
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-constexpr int BM = 128;     // rows per workgroup tile
-constexpr int BN = 128;     // columns per workgroup tile
-
-struct GemmArgs {
-  int64_t M;
-  int32_t N, K, batch, epi;
-  const float* A;
-  int64_t lda, sa;
-  const float* B;
-  int64_t ldb, sb;
-  float* C;
-  int64_t ldc, sc;
-  const float* bias;
-  const float* Y;
-  float* partials;
-  int32_t prio;   // raise the wave priority while issuing a stage's MFMAs (s_setprio)
-};
-
-__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : __expf(x) - 1.f; }  // v_exp_f32
-__device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-
-constexpr int BK = 32;              // K per LDS stage
 constexpr int LDS_LD = BK + 4;      // row stride (floats): 16-B shift per row, conflict-free b128 reads
 constexpr int TILE_FLOATS = BM * LDS_LD;
 
 __device__ __forceinline__ float comp(const float4& q, int s) {
   return s == 0 ? q.x : s == 1 ? q.y : s == 2 ? q.z : q.w;
-}
-
-// Wave layouts of the 128 x 128 workgroup tile (template NW = waves per workgroup):
-//   NW = 4: 2 x 2 waves of 64 x 64 (2 x 2 accumulator tiles of 32 x 32, 64 floats per lane);
-//   NW = 8: 2 x 4 waves of 64 x 32 (2 x 1 tiles): half the accumulators per wave, 4 waves per
-//           SIMD at 2 workgroups per CU, so one workgroup's epilogue and barriers are covered by
-//           the other's MFMAs.
-template <int NW>
-struct Cfg {
-  static constexpr int GT = 64 * NW;            // threads per workgroup
-  static constexpr int WI = 2;                  // 32-row accumulator tiles per wave
-  static constexpr int WJ = NW == 4 ? 2 : 1;    // 32-column accumulator tiles per wave
-  static constexpr int WGN = BN / (32 * WJ);    // waves along N
-  static constexpr int WGM = NW / WGN;          // waves along M
-  static constexpr int NL = 1024 / GT;          // float4 per thread per operand per K stage
-  static constexpr int RSTEP = GT / 8;          // row step between a thread's float4s
-  static_assert(WGM * 32 * WI == BM, "wave grid covers the tile rows");
-};
-
-// One K stage of the global -> LDS copy: 128 rows x 32 k of A and of B (8 threads per 128-byte
-// row segment: coalesced).  Thread t copies rows (t >> 3) + RSTEP i at columns c = (t & 7) * 4;
-// its row offsets are 32-bit (the caller checks that every operand has < 2^30 floats: 32-bit
-// byte offsets), so the loads address from the uniform base pointer (SGPRs) plus one VGPR
-// offset instead of a 64-bit VGPR address per load.  k >= K is zero-filled.
-template <int NW>
-struct Stage {
-  float4 a[Cfg<NW>::NL], b[Cfg<NW>::NL];
-};
-template <int NW>
-struct RowOffs {
-  uint32_t a[Cfg<NW>::NL], b[Cfg<NW>::NL];
-};
-
-template <int NW>
-__device__ __forceinline__ void row_offs(RowOffs<NW>& o, int64_t lda, int64_t m_base, int64_t M, int64_t ldb,
-                                         int n_base, int tid) {
-#pragma unroll
-  for (int i = 0; i < Cfg<NW>::NL; ++i) {
-    const int row = (tid >> 3) + Cfg<NW>::RSTEP * i;
-    const int64_t m = min(m_base + row, M - 1);  // rows past M load row M-1 (results discarded)
-    o.a[i] = (uint32_t)(m * lda);
-    o.b[i] = (uint32_t)((int64_t)(n_base + row) * ldb);
-  }
-}
-
-template <int NW>
-__device__ __forceinline__ void stage_load(Stage<NW>& st, const float* __restrict__ A, const float* __restrict__ B,
-                                           const RowOffs<NW>& o, int K, int k0, int c) {
-  // branch-free tail: past K, load the last valid float4 (zeroed in stage_store)
-  const uint32_t kc = (uint32_t)min(k0 + c, K - 4);
-  const char* Ab = reinterpret_cast<const char*>(A);
-  const char* Bb = reinterpret_cast<const char*>(B);
-#pragma unroll
-  for (int i = 0; i < Cfg<NW>::NL; ++i) {  // 32-bit byte offsets: base (SGPR) + offset (VGPR)
-    st.a[i] = *reinterpret_cast<const float4*>(Ab + (uint32_t)((o.a[i] + kc) * 4u));
-    st.b[i] = *reinterpret_cast<const float4*>(Bb + (uint32_t)((o.b[i] + kc) * 4u));
-  }
 }
 
 template <int NW>
@@ -162,9 +80,6 @@ template <int NW>
 struct LdsFrag {
   float4 a[Cfg<NW>::WI], b[Cfg<NW>::WJ];
 };
-
-template <int NW>
-using Acc = f32x16[Cfg<NW>::WI][Cfg<NW>::WJ];
 
 template <int NW>
 __device__ __forceinline__ void frag_read(LdsFrag<NW>& f, const float* __restrict__ la, const float* __restrict__ lb,
@@ -204,118 +119,6 @@ __device__ __forceinline__ void stage_mma(const float* __restrict__ la, const fl
     __builtin_amdgcn_sched_barrier(0);
     frag_mma<NW>(f1, acc);
     __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-struct TileId {
-  int64_t mt;
-  int nt, z;
-};
-
-__device__ __forceinline__ TileId decode_tile(int64_t tile, int ntn, int batch) {
-  TileId t;
-  t.nt = (int)(tile % ntn);
-  const int64_t rest = tile / ntn;
-  t.z = (int)(rest % batch);
-  t.mt = rest / batch;
-  return t;
-}
-
-// ---- epilogue: acc[i][j][e] is C[m0 + 32i + (e & 3) + 8(e >> 2) + 4h][n0 + 32j + r].
-// Every store / load addresses a wave-uniform row pointer (SGPRs) plus ONE per-lane 32-bit
-// byte offset (4h rows + r columns), so no per-row 64-bit addresses live in VGPRs; whole tiles
-// (every tile when M % 128 == 0) store without row guards.
-__device__ __forceinline__ int acc_row(int i, int e) { return 32 * i + (e & 3) + 8 * (e >> 2); }
-
-template <typename T>
-__device__ __forceinline__ T* at_bytes(T* p, uint32_t off) {
-  return reinterpret_cast<T*>(reinterpret_cast<typename std::conditional<std::is_const<T>::value, const char, char>::type*>(p) + off);
-}
-
-template <int NW, int EPI, bool FULL>
-__device__ __forceinline__ void epilogue_rows(const GemmArgs& g, const Acc<NW>& acc, int64_t m0, int n0, int z, int r,
-                                              int h, float (&cs)[Cfg<NW>::WJ]) {
-  constexpr int WI = Cfg<NW>::WI, WJ = Cfg<NW>::WJ;
-  float* C = g.C + z * g.sc + m0 * g.ldc + n0;
-  const int64_t ldc = g.ldc;
-  const int rows = (int)min<int64_t>(32 * WI, g.M - m0);
-  const uint32_t lo = (uint32_t)((4 * h * ldc + r) * 4);  // this lane's byte offset from a row pointer
-  if (EPI == LGX_GEMM_DELU_COLSUM) {
-    const float* Y = g.Y + z * g.sc + m0 * g.ldc + n0;
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int e0 = 0; e0 < 16; e0 += 4) {   // 4 * WJ loads of Y in flight, then the stores
-        float y[4][WJ];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int j = 0; j < WJ; ++j) {
-            const int rr = acc_row(i, e0 + e);
-            y[e][j] = (FULL || rr + 4 * h < rows) ? *at_bytes(Y + rr * ldc + 32 * j, lo) : 0.f;
-          }
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int j = 0; j < WJ; ++j) {
-            const int rr = acc_row(i, e0 + e);
-            const float d = acc[i][j][e0 + e] * elu_grad_from_out(y[e][j]);
-            if (FULL || rr + 4 * h < rows) {
-              *at_bytes(C + rr * ldc + 32 * j, lo) = d;
-              cs[j] += d;
-            }
-          }
-      }
-  } else {
-    float bj[WJ];
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) bj[j] = EPI == LGX_GEMM_BIAS_ELU ? g.bias[(int64_t)z * g.N + n0 + 32 * j + r] : 0.f;
-#pragma unroll
-    for (int i = 0; i < WI; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-#pragma unroll
-        for (int j = 0; j < WJ; ++j) {
-          const int rr = acc_row(i, e);
-          float v = acc[i][j][e];
-          if (EPI == LGX_GEMM_BIAS_ELU) v = elu_f(v + bj[j]);
-          if (FULL || rr + 4 * h < rows) *at_bytes(C + rr * ldc + 32 * j, lo) = v;
-        }
-  }
-}
-
-template <int NW, int EPI>
-__device__ __forceinline__ void epilogue(const GemmArgs& g, const Acc<NW>& acc, const TileId& T, int wm, int wn, int r,
-                                         int h) {
-  constexpr int WI = Cfg<NW>::WI, WJ = Cfg<NW>::WJ, WGM = Cfg<NW>::WGM;
-  const int64_t m0 = T.mt * BM + wm * 32 * WI;
-  const int n0 = T.nt * BN + wn * 32 * WJ;
-  float cs[WJ];
-#pragma unroll
-  for (int j = 0; j < WJ; ++j) cs[j] = 0.f;
-  if (T.mt * BM + BM <= g.M) epilogue_rows<NW, EPI, true>(g, acc, m0, n0, T.z, r, h, cs);
-  else if (m0 < g.M) epilogue_rows<NW, EPI, false>(g, acc, m0, n0, T.z, r, h, cs);
-  if (EPI == LGX_GEMM_DELU_COLSUM) {
-    // column sums: lane halves hold different rows of the same column, then the wave rows
-    __shared__ float red[WGM][BN];  // [wave row][column within the tile]
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) cs[j] += __shfl_xor(cs[j], 32);
-    const int cl = wn * 32 * WJ;  // the wave's first column within the tile
-    if (h == 0) {
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) red[wm][cl + 32 * j + r] = cs[j];
-    }
-    __syncthreads();
-    if (wm == 0 && h == 0) {
-      float* P = g.partials + T.mt * ((int64_t)g.batch * g.N) + (int64_t)T.z * g.N;
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        float v = 0.f;
-#pragma unroll
-        for (int w = 0; w < WGM; ++w) v += red[w][cl + 32 * j + r];   // fixed order
-        P[n0 + 32 * j + r] = v;
-      }
-    }
   }
 }
 
@@ -392,6 +195,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 8 ? 4 : 2) gemm_nt_kernel(GemmA
   }
 }
 
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------- copy2d
@@ -461,15 +265,27 @@ extern "C" int64_t lgx_gemm_partials_floats(int64_t M, int32_t N, int32_t batch)
 extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
   if (!args) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: null args");
   const lgx_gemm_args& a = *args;
-  const bool aligned = ((uintptr_t)a.A & 15) == 0 && ((uintptr_t)a.B & 15) == 0 && a.lda % 4 == 0 &&
-                       a.ldb % 4 == 0 && a.sa % 4 == 0 && a.sb % 4 == 0;
-  if (!a.A || !a.B || !a.C || a.M <= 0 || a.N <= 0 || a.N % BN || a.K <= 0 || a.K % 4 || a.batch <= 0 ||
-      a.batch > 65535 || !aligned || a.lda < a.K || a.ldb < a.K || a.ldc < a.N || a.ldc > (1 << 22) || a.epi < 0 || a.epi > 2 ||
-      (a.epi == LGX_GEMM_BIAS_ELU && !a.bias) || (a.epi == LGX_GEMM_DELU_COLSUM && (!a.Y || !a.partials)))
+  static const int default_algo = [] {
+    const char* e = getenv("LGX_GEMM_ALGO");
+    return e && e[0] == 'f' ? LGX_GEMM_ALGO_F32 : LGX_GEMM_ALGO_SPLIT_BF16;
+  }();
+  if (a.algo < 0 || a.algo > LGX_GEMM_ALGO_SPLIT_BF16) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: bad algo");
+  const int algo = a.algo == LGX_GEMM_ALGO_DEFAULT ? default_algo : a.algo;
+  const bool presplit = algo == LGX_GEMM_ALGO_SPLIT_BF16 && a.Bs;   // B is not read
+  const bool aligned = ((uintptr_t)a.A & 15) == 0 && a.lda % 4 == 0 && a.sa % 4 == 0 &&
+                       (presplit || (((uintptr_t)a.B & 15) == 0 && a.ldb % 4 == 0 && a.sb % 4 == 0));
+  if (!a.A || (!a.B && !presplit) || !a.C || a.M <= 0 || a.N <= 0 || a.N % BN || a.K <= 0 || a.K % 4 ||
+      a.batch <= 0 || a.batch > 65535 || !aligned || a.lda < a.K || (!presplit && a.ldb < a.K) || a.ldc < a.N ||
+      a.ldc > (1 << 22) || a.epi < 0 || a.epi > 2 || (a.epi == LGX_GEMM_BIAS_ELU && !a.bias) ||
+      (a.epi == LGX_GEMM_DELU_COLSUM && (!a.Y || !a.partials)))
     return lgx_fail(LGX_EINVAL,
                     "lgx_gemm_nt: bad args (N % 128, K % 4, 16-byte aligned A/B rows, epilogue operands)");
-  if (a.M * a.lda >= (1ll << 30) || (int64_t)a.N * a.ldb >= (1ll << 30))
+  if (a.M * a.lda >= (1ll << 30) || (!presplit && (int64_t)a.N * a.ldb >= (1ll << 30)))
     return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: operand too large for 32-bit row offsets");
+  if (algo == LGX_GEMM_ALGO_SPLIT_BF16 &&   // 16-byte epilogue vectors
+      (((uintptr_t)a.C & 15) || a.ldc % 4 || a.sc % 4 || (a.bias && ((uintptr_t)a.bias & 15)) ||
+       (a.Y && ((uintptr_t)a.Y & 15))))
+    return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: split-bf16 path needs 16-byte aligned C / Y / bias rows");
   const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
   if (tiles > (1ll << 31) - 1) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too large");
   static const int prio = [] {  // A/B switch LGX_GEMM_PRIO=0/1 (s_setprio around the MFMA stages)
@@ -477,11 +293,12 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
     return e ? atoi(e) : 1;
   }();
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
-             a.partials, prio};
-  // persistent: 2 workgroups per CU (LDS-bound), a multiple of 8 (XCD tile ranges)
+             a.partials, prio, nullptr};
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
+  if (algo == LGX_GEMM_ALGO_SPLIT_BF16) return lgx_gemm_nt_split(a, cus, stream);
+  // persistent: 2 workgroups per CU (LDS-bound), a multiple of 8 (XCD tile ranges)
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, 2 * cus / 8));
   const dim3 grid((unsigned)wgs);
   const char* ew = getenv("LGX_GEMM_WAVES");  // A/B switch: 4 or 8 waves per 128 x 128 tile

@@ -59,6 +59,8 @@ extern thread_local lgx_timing_slot lgx_timing;
 
 // error reporting shared by the translation units (thread-local message, lgx_last_error)
 int lgx_fail(int code, const char* msg);
+// lgx_gemm_split.hip: the split-bf16 path of lgx_gemm_nt (arguments already checked)
+int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream);
 int lgx_hip_status(const char* what);  // LGX_OK or LGX_EHIP from hipGetLastError()
 
 // a batch of reduction jobs passed by value to one launch (lgx_reduce_slices)

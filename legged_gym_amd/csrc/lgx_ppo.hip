@@ -502,6 +502,13 @@ sumsq_kernel(const float* __restrict__ g, int64_t n, float scale, float* __restr
 // Mirrors: derived copies of parameter blocks that the next minibatch's GEMMs read (zero-padded
 // layer-1 weights, transposed hidden weights; lgx_copy2d job layout with src inside p) written
 // with the updated value, so no weight-preparation pass runs between minibatches.
+// round-to-nearest-even bf16 (as v_cvt_pk_bf16_f32, finite inputs)
+__device__ __forceinline__ uint16_t bf16_rne(float x) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float fx2_t __attribute__((ext_vector_type(2)));
+  return (uint16_t)__builtin_bit_cast(uint32_t, __builtin_convertvector((fx2_t){x, 0.f}, bf16x2_t));
+}
+
 struct Mirror {
   int64_t off, dst_ld, dst_bs;  // off: first flat index of the block in p
   float* dst;
@@ -556,7 +563,19 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
       if (li < (uint64_t)J.count) {
         const int32_t l = (int32_t)li, rc = J.rows * J.cols;
         const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
-        J.dst[b * J.dst_bs + (J.transpose ? (int64_t)cc * J.dst_ld + rr : (int64_t)rr * J.dst_ld + cc)] = pi;
+        if (J.transpose & 2) {   // bf16 limb layout of lgx_split_bf16 (split-bf16 GEMM operand)
+          const int32_t nn = (J.transpose & 1) ? cc : rr, kk = (J.transpose & 1) ? rr : cc;
+          uint16_t* d = reinterpret_cast<uint16_t*>(J.dst) + b * J.dst_bs + (int64_t)nn * J.dst_ld + (kk >> 5) * 96 +
+                        (kk & 31);
+          const uint16_t l0 = bf16_rne(pi);
+          const float r1 = pi - __uint_as_float((uint32_t)l0 << 16);
+          const uint16_t l1 = bf16_rne(r1);
+          d[0] = l0;
+          d[32] = l1;
+          d[64] = bf16_rne(r1 - __uint_as_float((uint32_t)l1 << 16));
+        } else {
+          J.dst[b * J.dst_bs + (J.transpose ? (int64_t)cc * J.dst_ld + rr : (int64_t)rr * J.dst_ld + cc)] = pi;
+        }
       }
     }
   }

@@ -154,7 +154,7 @@ class FusedPPOUpdate:
         # weight copies the Adam step maintains: padded W1 (x2) + transposed W_2..L
         sep = la[0].in_features != lc[0].in_features
         jobs = 2 * L + 1 + int(sep)
-        mirrors = L + int(sep)
+        mirrors = 2 * L - 1 + int(sep)     # split-bf16 limb copies: W_1 (x2), W_k and W_k^T
         return (ha == hc and all(h % 4 == 0 for h in ha) and ha[-1] <= 1024 and lc[-1].out_features == 1
                 and la[-1].out_features <= abi.PPO_MAX_ACTIONS and ac.std.dim() == 1
                 and jobs <= abi.MAX_REDUCE_JOBS and mirrors <= abi.MAX_REDUCE_JOBS)
@@ -222,6 +222,9 @@ class FusedPPOUpdate:
         mode = os.environ.get("LGX_PPO_GEMM", "lgx")
         self.lgx_gemm = all(hk % abi.GEMM_TILE_N == 0 for hk in self.hidden) and mode != "lib"
         self.lgx_fwd_layers = set(range(self.L)) if mode == "lgx" else {0}
+        # LGX_GEMM_ALGO: "split" (default) = lgx_gemm_nt's split-bf16 products (f32-accurate, bf16
+        # MFMA) with pre-split weights; "f32" = the exact-f32 MFMA path with f32 weight copies
+        self.split = os.environ.get("LGX_GEMM_ALGO", "split") != "f32"
         self.norm_parts = torch.zeros(256, device=self.dev)
         self._mirrors_valid = False
         self.stats = torch.zeros(3, device=self.dev)
@@ -294,24 +297,51 @@ class FusedPPOUpdate:
             j.rows, j.cols, j.batch, j.transpose = rows, cols, batch, int(transpose)
             copies.append(j)
         w1 = fp.data_ptr() + f4 * self.Wg[0]
-        if shared:
-            self.W1p = torch.zeros(2, h[0], self.Kp, device=dev)
-            copy(w1, self.W1p, h[0], self.num_obs, 2, False, self.num_obs, self.Kp)
+        nl = [None] * (L + 1)   # split-bf16: limb copies of W_1 / W_k (forward) and W_k^T (backward dA)
+        nlt = [None] * (L + 1)
+        if self.split:
+            # the B operands pre-split into bf16 limbs (lgx_split_bf16 before an update's first
+            # minibatch, then kept current by the Adam step's limb mirrors: transpose bit 1)
+            def limbs(src_ptr, rows, cols, batch, transpose):
+                nout, kout = (cols, rows) if transpose else (rows, cols)
+                ld = int(self.lib.lgx_split_bf16_elems(1, kout))
+                buf = torch.zeros(batch * nout * ld, dtype=torch.int16, device=dev)
+                j = abi.LgxCopy2dJob()
+                j.src, j.dst = src_ptr, buf.data_ptr()
+                j.src_ld, j.src_bs, j.dst_ld, j.dst_bs = cols, rows * cols, ld, nout * ld
+                j.rows, j.cols, j.batch, j.transpose = rows, cols, batch, int(transpose) | 2
+                copies.append(j)
+                return buf
+            if shared:
+                nl[0] = (limbs(w1, h[0], self.num_obs, 2, False),)
+            else:
+                nl[0] = (limbs(w1, h[0], self.num_obs, 1, False),
+                         limbs(w1 + f4 * h[0] * self.num_obs, h[0], self.num_cobs, 1, False))
+            for k in range(1, L):
+                wk = fp.data_ptr() + f4 * self.Wg[k]
+                nl[k] = limbs(wk, h[k], h[k - 1], 2, False)
+                nlt[k] = limbs(wk, h[k], h[k - 1], 2, True)
+            self.limb_bufs = (nl, nlt)
         else:
-            self.W1p = torch.zeros(h[0], self.Kp, device=dev)
-            self.W1pc = torch.zeros(h[0], self.Kcp, device=dev)
-            copy(w1, self.W1p, h[0], self.num_obs, 1, False, self.num_obs, self.Kp)
-            copy(w1 + f4 * h[0] * self.num_obs, self.W1pc, h[0], self.num_cobs, 1, False, self.num_cobs, self.Kcp)
-        self.WT = [None]
-        for k in range(1, L):   # W_k [2, h_k, h_{k-1}] -> W_k^T [2, h_{k-1}, h_k]
-            wt = torch.empty(2, h[k - 1], h[k], device=dev)
-            copy(fp.data_ptr() + f4 * self.Wg[k], wt, h[k], h[k - 1], 2, True, h[k - 1], h[k])
-            self.WT.append(wt)
+            if shared:
+                self.W1p = torch.zeros(2, h[0], self.Kp, device=dev)
+                copy(w1, self.W1p, h[0], self.num_obs, 2, False, self.num_obs, self.Kp)
+            else:
+                self.W1p = torch.zeros(h[0], self.Kp, device=dev)
+                self.W1pc = torch.zeros(h[0], self.Kcp, device=dev)
+                copy(w1, self.W1p, h[0], self.num_obs, 1, False, self.num_obs, self.Kp)
+                copy(w1 + f4 * h[0] * self.num_obs, self.W1pc, h[0], self.num_cobs, 1, False, self.num_cobs, self.Kcp)
+            self.WT = [None]
+            for k in range(1, L):   # W_k [2, h_k, h_{k-1}] -> W_k^T [2, h_{k-1}, h_k]
+                wt = torch.empty(2, h[k - 1], h[k], device=dev)
+                copy(fp.data_ptr() + f4 * self.Wg[k], wt, h[k], h[k - 1], 2, True, h[k - 1], h[k])
+                self.WT.append(wt)
         if len(copies) > abi.MAX_REDUCE_JOBS:
             raise RuntimeError("too many weight-preparation jobs for one launch")
         self.copy_jobs = (abi.LgxCopy2dJob * len(copies))(*copies)
+        algo = abi.GEMM_ALGO_SPLIT_BF16 if self.split else abi.GEMM_ALGO_F32
 
-        def gemm(A, lda, sa, B, ldb, sb, C, N, K, batch, epi, bias=None, Y=None, parts=None):
+        def gemm(A, lda, sa, B, ldb, sb, C, N, K, batch, epi, bias=None, Y=None, parts=None, Bs=None):
             g = abi.LgxGemmArgs()
             g.M, g.N, g.K, g.batch, g.epi = M, N, K, batch, epi
             g.A, g.lda, g.sa = A, lda, sa
@@ -320,31 +350,36 @@ class FusedPPOUpdate:
             g.bias = bias
             g.Y = Y.data_ptr() if Y is not None else None
             g.partials = parts.data_ptr() if parts is not None else None
+            g.algo = algo
+            g.Bs = Bs.data_ptr() if Bs is not None else None
             return g
         fwd = [[]]
         b0 = fp.data_ptr() + f4 * self.bo[0]
         self.fwd0_src = ["x"] if shared else ["x", "xc"]
+        w1p = None if self.split else self.W1p.data_ptr()
         if shared:   # one input for both networks: batch stride 0
-            fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, self.W1p.data_ptr(), self.Kp, h[0] * self.Kp, self.Y[0],
-                            h[0], self.Kp, 2, abi.GEMM_BIAS_ELU, bias=b0))
+            fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, w1p, self.Kp, h[0] * self.Kp, self.Y[0],
+                               h[0], self.Kp, 2, abi.GEMM_BIAS_ELU, bias=b0, Bs=nl[0][0] if self.split else None))
         else:
-            fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, self.W1p.data_ptr(), self.Kp, 0, self.Y[0][0], h[0],
-                               self.Kp, 1, abi.GEMM_BIAS_ELU, bias=b0))
+            fwd[0].append(gemm(self.Xp.data_ptr(), self.Kp, 0, w1p, self.Kp, 0, self.Y[0][0], h[0],
+                               self.Kp, 1, abi.GEMM_BIAS_ELU, bias=b0, Bs=nl[0][0] if self.split else None))
             xc = self.Xcp if self.Xcp is not None else self.Xp
-            fwd[0].append(gemm(xc.data_ptr(), self.Kcp, 0, self.W1pc.data_ptr(), self.Kcp, 0, self.Y[0][1], h[0],
-                            self.Kcp, 1, abi.GEMM_BIAS_ELU, bias=b0 + f4 * h[0]))
+            fwd[0].append(gemm(xc.data_ptr(), self.Kcp, 0, None if self.split else self.W1pc.data_ptr(), self.Kcp, 0,
+                               self.Y[0][1], h[0], self.Kcp, 1, abi.GEMM_BIAS_ELU, bias=b0 + f4 * h[0],
+                               Bs=nl[0][1] if self.split else None))
         for k in range(1, L):
             fwd.append(gemm(self.Y[k - 1].data_ptr(), h[k - 1], M * h[k - 1], fp.data_ptr() + f4 * self.Wg[k], h[k - 1],
                             h[k] * h[k - 1], self.Y[k], h[k], h[k - 1], 2, abi.GEMM_BIAS_ELU,
-                            bias=fp.data_ptr() + f4 * self.bo[k]))
+                            bias=fp.data_ptr() + f4 * self.bo[k], Bs=nl[k]))
         self.gemm_fwd = fwd
         # algorithmic K of each launch (layer 1: the unpadded input width) for the bench's roofline
         self.k_alg = {id(g): k for g, k in zip(fwd[0], [self.num_obs, self.num_cobs])}
         bwd = {}
         for k in range(L - 1, 0, -1):   # dZ_{k-1} = (dZ_k W_k) * elu'(Y_{k-1}); dZ_{L-1} lives in Y[L-1]
             dz = self.Y[L - 1] if k == L - 1 else self.D[k]
-            bwd[k] = gemm(dz.data_ptr(), h[k], M * h[k], self.WT[k].data_ptr(), h[k], h[k - 1] * h[k], self.D[k - 1],
-                          h[k - 1], h[k], 2, abi.GEMM_DELU_COLSUM, Y=self.Y[k - 1], parts=self.col_parts[k - 1])
+            bwd[k] = gemm(dz.data_ptr(), h[k], M * h[k], None if self.split else self.WT[k].data_ptr(), h[k],
+                          h[k - 1] * h[k], self.D[k - 1], h[k - 1], h[k], 2, abi.GEMM_DELU_COLSUM, Y=self.Y[k - 1],
+                          parts=self.col_parts[k - 1], Bs=nlt[k])
         self.gemm_bwd = bwd
 
     def _separate_critic_obs(self):
@@ -555,7 +590,10 @@ class FusedPPOUpdate:
         X = Xc = self.X
         if fused:
             if not self._mirrors_valid:   # (afterwards lgx_adam_clip_mirror keeps the copies current)
-                chk(lib.lgx_copy2d(self.copy_jobs, len(self.copy_jobs), stream), "copy2d")
+                if self.split:
+                    chk(lib.lgx_split_bf16(self.copy_jobs, len(self.copy_jobs), stream), "split_bf16")
+                else:
+                    chk(lib.lgx_copy2d(self.copy_jobs, len(self.copy_jobs), stream), "copy2d")
                 self._mirrors_valid = True
             if xs is None:
                 chk(lib.lgx_ppo_gather_rows_padded(_vp(obs), _vp(self.Xp), _vp(idx), M, obs.shape[1], self.Kp,

@@ -129,7 +129,7 @@ class LgxGemmArgs(C.Structure):
     _fields_ = [("M", i64), ("N", i32), ("K", i32), ("batch", i32), ("epi", i32),
                 ("A", C.c_void_p), ("lda", i64), ("sa", i64), ("B", C.c_void_p), ("ldb", i64), ("sb", i64),
                 ("C", C.c_void_p), ("ldc", i64), ("sc", i64), ("bias", C.c_void_p), ("Y", C.c_void_p),
-                ("partials", C.c_void_p)]
+                ("partials", C.c_void_p), ("algo", i32), ("reserved", i32), ("Bs", C.c_void_p)]
 
 
 class LgxCopy2dJob(C.Structure):
@@ -140,6 +140,7 @@ class LgxCopy2dJob(C.Structure):
 PPO_MAX_ACTIONS = 16
 MAX_REDUCE_JOBS = 16
 GEMM_PLAIN, GEMM_BIAS_ELU, GEMM_DELU_COLSUM = 0, 1, 2
+GEMM_ALGO_DEFAULT, GEMM_ALGO_F32, GEMM_ALGO_SPLIT_BF16 = 0, 1, 2
 GEMM_TILE_M, GEMM_TILE_N, GEMM_K_STEP = 128, 128, 32   # K step: layer-1 rows padded to 1024 B (aligned 128-B lines)
 
 
@@ -189,6 +190,8 @@ def declare(lib, prefix="lgx"):
             "gemm_partials_floats": (i64, [i64, i32, i32]),
             "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
             "copy2d": (C.c_int, [C.POINTER(LgxCopy2dJob), i32, vp]),
+            "split_bf16_elems": (i64, [i32, i32]),
+            "split_bf16": (C.c_int, [C.POINTER(LgxCopy2dJob), i32, vp]),
             "ppo_gather_rows_padded": (C.c_int, [vp, vp, vp, i64, i32, i32, vp]),
             "ppo_gather_rows_padded_dup": (C.c_int, [vp, vp, vp, i64, i32, i32, i64, vp]),
             "adam_clip": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
@@ -211,7 +214,7 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
             "lgx_reduce_slices", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
-            "lgx_ppo_gather_rows_padded_dup"]
+            "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16"]
 
 
 def check_layout(sizes_fn, n=10):

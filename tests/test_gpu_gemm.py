@@ -1,8 +1,11 @@
-"""GPU: the hand-written f32-MFMA GEMMs of the PPO update (lgx_gemm_nt with its three epilogues,
-lgx_copy2d, lgx_ppo_gather_rows_padded) against float64 torch references of the same ops.
+"""GPU: the hand-written GEMMs of the PPO update (lgx_gemm_nt with its three epilogues, both
+product algorithms: exact f32 MFMA and the split-bf16 evaluation; lgx_copy2d,
+lgx_ppo_gather_rows_padded) against float64 torch references of the same ops.
 
-Tolerance: exact-f32 MFMA products with f32 accumulation over K <= 512 of O(1) operands:
+Tolerance: f32-accurate products with f32 accumulation over K <= 512 of O(1) operands:
 |C - C64| <= 2e-5 * sqrt(K) * max|C64| + 1e-6 (the k order differs from a sequential sum).
+test_split_bf16_is_f32_accurate additionally bounds the split-bf16 error by the exact-f32
+MFMA's own error on the same data (max and mean, x1.25).
 """
 import ctypes as C
 
@@ -23,7 +26,31 @@ def _stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
-def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0):
+ALGOS = [abi.GEMM_ALGO_F32, abi.GEMM_ALGO_SPLIT_BF16]
+
+
+def _presplit(B, transpose=False):
+    """lgx_split_bf16 of a [batch, rows, cols] f32 operand (transpose: of its [cols, rows] view)."""
+    batch, rows, cols = B.shape
+    nout, kout = (cols, rows) if transpose else (rows, cols)
+    ld = _lib().lgx_split_bf16_elems(1, kout)
+    Bs = torch.full((batch * nout * ld,), -1, dtype=torch.int16, device=B.device)
+    j = abi.LgxCopy2dJob()
+    j.src, j.dst = B.data_ptr(), Bs.data_ptr()
+    j.src_ld, j.src_bs, j.dst_ld, j.dst_bs = cols, rows * cols, ld, nout * ld
+    j.rows, j.cols, j.batch, j.transpose = rows, cols, batch, int(transpose)
+    lgxlib.check(_lib().lgx_split_bf16((abi.LgxCopy2dJob * 1)(j), 1, _stream()), "split_bf16")
+    return Bs
+
+
+def _limbs_to_f32(Bs, batch, nout, kout):
+    ld = _lib().lgx_split_bf16_elems(1, kout)
+    u = Bs.view(batch, nout, ld // 96, 3, 32).to(torch.int32) & 0xFFFF
+    f = (u << 16).view(torch.float32).double()
+    return f.sum(3).reshape(batch, nout, -1)
+
+
+def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0, algo=abi.GEMM_ALGO_DEFAULT, presplit=False):
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(seed)
     lda = K + lda_pad
@@ -40,6 +67,10 @@ def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0):
     a.B, a.ldb, a.sb = B.data_ptr(), K, N * K
     a.C, a.ldc, a.sc = Cout.data_ptr(), N, M * N
     a.bias, a.Y, a.partials = bias.data_ptr(), Y.data_ptr(), parts.data_ptr()
+    a.algo = algo
+    if presplit:
+        Bs = _presplit(B)
+        a.Bs = Bs.data_ptr()
     assert _lib().lgx_gemm_partials_floats(M, N, batch) == parts.numel()
     rc = _lib().lgx_gemm_nt(C.byref(a), _stream())
     lgxlib.check(rc, "lgx_gemm_nt")
@@ -55,7 +86,7 @@ def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0):
         ref = acc
     tol = 2e-5 * K ** 0.5 * ref.abs().max().item() + 1e-6
     err = (Cout.double() - ref).abs().max().item()
-    assert err <= tol, f"M={M} N={N} K={K} batch={batch} epi={epi}: max err {err:.3e} > {tol:.3e}"
+    assert err <= tol, f"M={M} N={N} K={K} batch={batch} epi={epi} algo={algo}: max err {err:.3e} > {tol:.3e}"
     if epi == abi.GEMM_DELU_COLSUM:
         pad = mtiles * abi.GEMM_TILE_M - M
         r = torch.nn.functional.pad(ref, (0, 0, 0, pad)).view(batch, mtiles, abi.GEMM_TILE_M, N).sum(2)
@@ -63,21 +94,92 @@ def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0):
         assert perr <= tol * abi.GEMM_TILE_M ** 0.5, f"colsum partials: max err {perr:.3e}"
 
 
+@pytest.mark.parametrize("algo", ALGOS)
 @pytest.mark.parametrize("epi", [abi.GEMM_PLAIN, abi.GEMM_BIAS_ELU, abi.GEMM_DELU_COLSUM])
-def test_gemm_epilogues(gpu, epi):
-    _run(384, 256, 256, 2, epi)
+def test_gemm_epilogues(gpu, epi, algo):
+    _run(384, 256, 256, 2, epi, algo=algo)
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 128, 240), (129, 512, 16), (1, 128, 32), (4096, 256, 512)])
-def test_gemm_shapes(gpu, M, N, K):
-    # ragged M (row guards), odd K-step counts (240 = 15 steps, 16 = 1 step), one row
-    _run(M, N, K, 2, abi.GEMM_BIAS_ELU, seed=M)
-    _run(M, N, K, 1, abi.GEMM_DELU_COLSUM, seed=M + 1)
+@pytest.mark.parametrize("epi", [abi.GEMM_PLAIN, abi.GEMM_BIAS_ELU, abi.GEMM_DELU_COLSUM])
+@pytest.mark.parametrize("M,N,K", [(384, 256, 256), (300, 128, 240), (1, 128, 36), (4096, 512, 512)])
+def test_gemm_presplit_weights(gpu, epi, M, N, K):
+    """Split-bf16 path with B pre-split by lgx_split_bf16 (the weights of the PPO GEMMs)."""
+    _run(M, N, K, 2, epi, seed=M + K, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
 
 
-def test_gemm_shared_input_and_padded_rows(gpu):
+@pytest.mark.parametrize("transpose", [False, True])
+def test_split_bf16_limbs(gpu, transpose):
+    """lgx_split_bf16: limbs are RNE bf16 (x0 = bf16(x), |x1| <= 2^-9|x|, |x2| <= 2^-18|x|),
+    their sum reproduces x to 2^-26 relative, padding to the 32-k block is zero."""
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    B = torch.randn(2, 70, 45, device="cuda:0", generator=g) * torch.exp2(
+        torch.randint(-20, 20, (2, 70, 45), device="cuda:0", generator=g).float())
+    Bs = _presplit(B, transpose)
+    torch.cuda.synchronize()
+    ref = (B.transpose(1, 2) if transpose else B).double()
+    nout, kout = ref.shape[1], ref.shape[2]
+    rec = _limbs_to_f32(Bs, 2, nout, kout)
+    assert torch.all(rec[..., kout:] == 0)
+    rec = rec[..., :kout]
+    assert bool(((rec - ref).abs() <= 2.0 ** -26 * ref.abs()).all())
+    ld = _lib().lgx_split_bf16_elems(1, kout)
+    x0 = ((Bs.view(2, nout, ld // 96, 3, 32)[:, :, :, 0].to(torch.int32) & 0xFFFF) << 16).view(torch.float32)
+    x0 = x0.reshape(2, nout, -1)[..., :kout]
+    assert torch.equal(x0, (B.transpose(1, 2) if transpose else B).to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+@pytest.mark.parametrize("M,N,K", [(300, 128, 240), (129, 512, 16), (1, 128, 32), (4096, 256, 512), (257, 384, 36)])
+def test_gemm_shapes(gpu, M, N, K, algo):
+    # ragged M (row guards), odd K-step counts (240 = 15 steps, 16 = 1 step, 36 = a 4-wide tail
+    # stage), one row
+    _run(M, N, K, 2, abi.GEMM_BIAS_ELU, seed=M, algo=algo)
+    _run(M, N, K, 1, abi.GEMM_DELU_COLSUM, seed=M + 1, algo=algo)
+
+
+@pytest.mark.parametrize("algo", ALGOS)
+def test_gemm_shared_input_and_padded_rows(gpu, algo):
     # layer-1 form: one input for both networks (batch stride 0), rows padded beyond K
-    _run(512, 512, 240, 2, abi.GEMM_BIAS_ELU, shared_a=True, lda_pad=16)
+    _run(512, 512, 240, 2, abi.GEMM_BIAS_ELU, shared_a=True, lda_pad=16, algo=algo)
+
+
+def _plain(A, B, algo):
+    batch, M, K = A.shape
+    N = B.shape[1]
+    Cout = torch.full((batch, M, N), float("nan"), device=A.device)
+    a = abi.LgxGemmArgs()
+    a.M, a.N, a.K, a.batch, a.epi = M, N, K, batch, abi.GEMM_PLAIN
+    a.A, a.lda, a.sa = A.data_ptr(), K, M * K
+    a.B, a.ldb, a.sb = B.data_ptr(), K, N * K
+    a.C, a.ldc, a.sc = Cout.data_ptr(), N, M * N
+    a.algo = algo
+    lgxlib.check(_lib().lgx_gemm_nt(C.byref(a), _stream()), "lgx_gemm_nt")
+    torch.cuda.synchronize()
+    return Cout
+
+
+@pytest.mark.parametrize("spread", [0, 12])
+def test_split_bf16_is_f32_accurate(gpu, spread):
+    """The split-bf16 products are f32-accurate: against float64, the max and mean absolute
+    errors stay within 1.25x those of the exact-f32 MFMA (fmaf chain) on the same operands,
+    including operands whose magnitudes spread over 2^+-spread (limb exponents follow each
+    element); every element's error is within the classic f32 dot-product bound
+    K * 2^-24 * sum_k |a b| (recursive summation, gamma_K)."""
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(17 + spread)
+    M, N, K = 2048, 256, 512
+    A = torch.randn(2, M, K, device=dev, generator=g)
+    B = torch.randn(2, N, K, device=dev, generator=g)
+    if spread:
+        A = A * torch.exp2(torch.randint(-spread, spread + 1, A.shape, device=dev, generator=g).float())
+        B = B * torch.exp2(torch.randint(-spread, spread + 1, B.shape, device=dev, generator=g).float())
+    ref = torch.bmm(A.double(), B.double().transpose(1, 2))
+    scale = torch.bmm(A.double().abs(), B.double().abs().transpose(1, 2))
+    e32 = (_plain(A, B, abi.GEMM_ALGO_F32).double() - ref).abs()
+    esp = (_plain(A, B, abi.GEMM_ALGO_SPLIT_BF16).double() - ref).abs()
+    assert esp.max().item() <= 1.25 * e32.max().item(), (esp.max().item(), e32.max().item())
+    assert esp.mean().item() <= 1.25 * e32.mean().item(), (esp.mean().item(), e32.mean().item())
+    assert bool((esp <= K * 2.0 ** -24 * scale).all())
 
 
 def test_gemm_rejects_bad_shapes(gpu):

@@ -91,16 +91,21 @@ def test_fused_minibatch_gradient_matches_autograd(gpu):
         assert ((a - b).abs() <= tol).all(), (n, (a - b).abs().max().item(), b.abs().max().item())
 
 
-@pytest.mark.parametrize("mode", ["auto", "lib"])
+@pytest.mark.parametrize("mode", ["auto", "lib", "f32"])
 def test_fused_minibatch_gradient_gemm_modes(gpu, monkeypatch, mode):
-    """LGX_PPO_GEMM=auto (library GEMM + lgx_bias_act for layers 2..L) and =lib (library GEMMs
-    with lgx_bias_act / lgx_elu_bwd_colsum everywhere) against autograd."""
-    monkeypatch.setenv("LGX_PPO_GEMM", mode)
+    """LGX_PPO_GEMM=auto (library GEMM + lgx_bias_act for layers 2..L), =lib (library GEMMs
+    with lgx_bias_act / lgx_elu_bwd_colsum everywhere) and the exact-f32 MFMA GEMMs
+    (LGX_GEMM_ALGO=f32 instead of the default split-bf16 products) against autograd."""
+    if mode == "f32":
+        monkeypatch.setenv("LGX_GEMM_ALGO", "f32")
+    else:
+        monkeypatch.setenv("LGX_PPO_GEMM", mode)
     ref, fus = make_pair()
     idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
     gref = autograd_grads(ref, idx)
     fus._fused.gradients(idx)
     assert fus._fused.lgx_gemm == (mode != "lib")
+    assert fus._fused.split == (mode != "f32")
     for n, p in fus.actor_critic.named_parameters():
         a, b = p.grad, gref[n]
         assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), (mode, n)
@@ -150,10 +155,13 @@ def test_fused_minibatch_gradient_library_heads(gpu, monkeypatch):
         assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), n
 
 
-@pytest.mark.parametrize("schedule,cobs", [("adaptive", None), ("fixed", None), ("adaptive", 252)])
-def test_fused_update_matches_autograd_update(gpu, schedule, cobs):
+@pytest.mark.parametrize("schedule,cobs,algo", [("adaptive", None, "split"), ("fixed", None, "split"),
+                                                ("adaptive", 252, "split"), ("adaptive", None, "f32")])
+def test_fused_update_matches_autograd_update(gpu, monkeypatch, schedule, cobs, algo):
     """Full update (one gather of all minibatch rows, Adam-maintained GEMM weight copies); cobs:
-    privileged critic observations of another width (two layer-1 inputs and GEMM launches)."""
+    privileged critic observations of another width (two layer-1 inputs and GEMM launches);
+    algo: the split-bf16 GEMM products with Adam-maintained limb copies, or exact f32."""
+    monkeypatch.setenv("LGX_GEMM_ALGO", algo)
     ref, fus = make_pair(schedule, cobs)
     torch.manual_seed(11)
     vl_r, sl_r = ref.update()

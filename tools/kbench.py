@@ -154,10 +154,20 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
         a.A, a.lda, a.sa, a.B, a.ldb, a.sb = A.data_ptr(), k_, M * k_, B.data_ptr(), k_, n_ * k_
         a.C, a.ldc, a.sc, a.bias, a.Y, a.partials = Cc.data_ptr(), n_, M * n_, bias.data_ptr(), Y.data_ptr(), parts.data_ptr()
         f = 2.0 * 2 * M * n_ * k_
-        for waves in ("4", "8"):
+        algos = [int(x) for x in os.environ.get("KB_ALGOS", "1,2,3").split(",")]
+        ld = lib.lgx_split_bf16_elems(1, k_)
+        Bs = torch.zeros(2 * n_ * ld, dtype=torch.int16, device=dev)
+        j = abi.LgxCopy2dJob()
+        j.src, j.dst, j.src_ld, j.src_bs, j.dst_ld, j.dst_bs = B.data_ptr(), Bs.data_ptr(), k_, n_ * k_, ld, n_ * ld
+        j.rows, j.cols, j.batch, j.transpose = n_, k_, 2, 0
+        lgxlib.check(lib.lgx_split_bf16((abi.LgxCopy2dJob * 1)(j), 1, stream), "split")
+        for algo, waves in [(al, "8") for al in algos]:   # 3 = split-bf16 with pre-split B
             os.environ["LGX_GEMM_WAVES"] = waves
+            a.algo = min(algo, 2)
+            a.Bs = Bs.data_ptr() if algo == 3 else None
             t1 = timeit(lambda: lib.lgx_gemm_nt(C.byref(a), stream), iters=iters)
-            print(f"gemm M={M} N={n_} K={k_} epi={epi} waves={waves}: lgx {t1*1e3:.1f} us {f/t1/1e9:.1f} TF/s", flush=True)
+            print(f"gemm M={M} N={n_} K={k_} epi={epi} algo={algo} waves={waves}: lgx {t1*1e3:.1f} us "
+                  f"{f/t1/1e9:.1f} TF/s", flush=True)
         os.environ.pop("LGX_GEMM_WAVES")
         if torch_too:
             t2 = timeit(lambda: torch.bmm(A, B.transpose(1, 2), out=Cc), iters=iters)
