@@ -40,8 +40,19 @@ def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
 
 
 PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
-PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_ppo_kernels.json")
-GEMM_KERNELS = {1: "gemm_nt_kernel<8, 1>", 2: "gemm_nt_kernel<8, 2>"}
+PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_ppo_kernels.json")
+MI355X_BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
+SPLIT_PRODUCTS = 6                  # split-bf16: six bf16 limb products per f32 product (lgx_gemm_split.hip)
+
+
+def gemm_kernel_info(epi, split):
+    """(kernel name as rocprof reports it, compute pipe, peak in f32-product TFLOP/s) of the PPO
+    GEMM instantiation with epilogue `epi`."""
+    if split:
+        return (f"gemm_nt_x3p_kernel<{epi}, *, 8>",
+                "bf16 MFMA (v_mfma_f32_32x32x16_bf16), split-bf16: 6 limb products per f32 product",
+                MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS)
+    return f"gemm_nt_kernel<8, {epi}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
 GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "
                  "to 256, 512->256, 256->128)",
               2: "lgx_gemm_nt LGX_GEMM_DELU_COLSUM: backward dA of the hidden layers (512x256 and 256x128 weights)"}
@@ -49,10 +60,18 @@ GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor 
 
 def pmc_ppo_traffic_bytes(kernel):
     """HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KB) of a PPO-update kernel from the PMC
-    passes over one bench iteration (tools/pmc_ppo.sh)."""
+    passes over one bench iteration (tools/pmc_ppo.sh); `kernel` may hold '*' wildcards (e.g. the
+    K-specialised instantiations of one epilogue): dispatch-weighted mean over the matches."""
+    import fnmatch
     try:
         p = json.load(open(PPO_PMC_FILE))["passes"]
-        return int((2 * p["fetch"][kernel]["FETCH_SIZE"] + p["write"][kernel]["WRITE_SIZE"]) * 1024)
+        tot = n = 0.0
+        for name in p["fetch"]:
+            if fnmatch.fnmatchcase(name, kernel) and name in p["write"]:
+                d = p["fetch"][name].get("dispatches", 1)
+                tot += d * (2 * p["fetch"][name]["FETCH_SIZE"] + p["write"][name]["WRITE_SIZE"]) * 1024
+                n += d
+        return int(tot / n) if n else None
     except (OSError, KeyError, ValueError):
         return None
 ACT_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_actuator_ws_kernel", "fetch_sep", "write_sep")
@@ -77,22 +96,27 @@ def iteration_roofline(runner, env, N, it_ms):
         st.observations, st.actions, st.rewards, st.dones, st.values, st.returns, st.advantages,
         st.actions_log_prob, st.mu, st.sigma)) / st.num_envs   # storage row bytes per sample
     decim = env.cfg.control.decimation
+    # f32-accurate MFMA work is priced at the split-bf16 rate (bf16 dense peak / 6 limb products:
+    # 417 TF/s of f32 products, above the 157 TF/s f32 MFMA), the physics at the FP32 VALU peak
+    split_peak = MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     phases = {
         "physics (fp32 VALU)": (samples * decim * physics_flop_per_env_substep(
             env._lgx_model.num_points, 4.0, env.cfg.terrain.mesh_type in ("heightfield", "trimesh")),
-            samples * ENV_BYTES_PER_ENV_STEP),
-        "actuator net (f32 MFMA)": (samples * ACT_MLP_FLOP_PER_ENV_STEP if hasattr(env, "_actuator_dvel") else 0, 0),
-        "rollout policy forward (f32 MFMA)": (samples * fwd, 0),
-        "PPO update (f32 MFMA)": (alg.num_learning_epochs * samples * epoch,
-                                  samples * row_bytes * (1 + alg.num_learning_epochs)),
+            samples * ENV_BYTES_PER_ENV_STEP, MI355X_F32_PEAK_TFLOPS),
+        "actuator net (f32-accurate MFMA)": (samples * ACT_MLP_FLOP_PER_ENV_STEP if hasattr(env, "_actuator_dvel")
+                                             else 0, 0, split_peak),
+        "rollout policy forward (f32-accurate MFMA)": (samples * fwd, 0, split_peak),
+        "PPO update (f32-accurate MFMA)": (alg.num_learning_epochs * samples * epoch,
+                                           samples * row_bytes * (1 + alg.num_learning_epochs), split_peak),
     }
     out, t_roof = {}, 0.0
-    for name, (flop, nbytes) in phases.items():
-        t = max(flop / (MI355X_F32_PEAK_TFLOPS * 1e12), nbytes / (MI355X_HBM_PEAK_GBS * 1e9)) * 1e3
+    for name, (flop, nbytes, peak) in phases.items():
+        t = max(flop / (peak * 1e12), nbytes / (MI355X_HBM_PEAK_GBS * 1e9)) * 1e3
         out[name] = {"flop": flop, "hbm_bytes": int(nbytes), "t_roof_ms": round(t, 4)}
         t_roof += t
     return {"t_roof_ms": round(t_roof, 3), "t_measured_ms": round(it_ms, 3), "frac": t_roof / it_ms,
-            "peaks": {"f32_tflops": MI355X_F32_PEAK_TFLOPS, "hbm_gbs": MI355X_HBM_PEAK_GBS}, "phases": out}
+            "peaks": {"f32_tflops": MI355X_F32_PEAK_TFLOPS, "split_bf16_f32_product_tflops": split_peak,
+                      "hbm_gbs": MI355X_HBM_PEAK_GBS}, "phases": out}
 
 
 BASELINE_METRIC = "env-steps/sec (whole node), Go1 rough-terrain 4096 envs/GPU at 1/2/4/8 GPUs"
@@ -285,16 +309,17 @@ def main():
     for epi, (n, t_ms, flop, mbs) in sorted(gemm_t.items()):
         if not n or not mbs:
             continue
-        kname = GEMM_KERNELS.get(epi, f"gemm_nt_kernel<8, {epi}>")
+        kname, pipe, peak = gemm_kernel_info(epi, getattr(fused, "split", False))
         gemm_roofs.append({
-            "kernel": kname, "bound": "mfma", "compute_pipe": "f32 MFMA (v_mfma_f32_32x32x2_f32)",
-            "achieved": flop / (t_ms * 1e-3) / 1e12, "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": flop / (t_ms * 1e-3) / 1e12 / MI355X_F32_PEAK_TFLOPS,
+            "kernel": kname, "bound": "mfma", "compute_pipe": pipe,
+            "achieved": flop / (t_ms * 1e-3) / 1e12, "peak": peak, "unit": "TFLOP/s",
+            "frac": flop / (t_ms * 1e-3) / 1e12 / peak,
             "traffic": pmc_ppo_traffic_bytes(kname), "algorithmic_per_launch": flop / n, "avg_ms": t_ms / n,
             "launches_timed": n, "share_of_iteration": (t_ms / mbs) * mb_per_iter / it_ms,
-            "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K; "
-                    "HIP events around every launch of every k-th minibatch (LGX_BENCH_GEMM_TIMING); traffic = "
-                    "2 FETCH_SIZE + WRITE_SIZE per launch from profiles/r01_pmc_ppo_kernels.json"})
+            "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K "
+                    "(f32 products; the split-bf16 peak is the bf16 dense MFMA peak / 6 limb products); HIP events "
+                    "around every launch of every k-th minibatch (LGX_BENCH_GEMM_TIMING); traffic = 2 FETCH_SIZE + "
+                    f"WRITE_SIZE per launch from {os.path.relpath(PPO_PMC_FILE, ROOT)}"})
     kernels = {n: {"avg_ms": round(a, 4), "launches_timed": int(c),
                    "share_of_iteration": round(a * steps_per_iter / it_ms, 4) if c else None}
                for n, a, c in zip(names, avg, cnt)}

@@ -3,16 +3,17 @@
 //
 // Every f32 operand is split, round-to-nearest, into three bf16 limbs
 //   x = x0 + x1 + x2 + e,   x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1),
-//   |x1| <= 2^-9 |x|, |x2| <= 2^-18 |x|, |e| <= 2^-27 |x|   (both subtractions are exact in f32),
+//   |x1| <= 2^-8 |x0|, |x2| <= 2^-8 |x1|, |e| <= 2^-24 |x|   (both subtractions are exact in f32),
 // and a*b is evaluated as the six limb products of order <= 2,
 //   a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0),
 // each product of two bf16 limbs exact in the f32 accumulator.  The dropped terms (a1 b2, a2 b1,
-// a2 b2) and the split residues are <= ~2^-25 |a b|, below the 2^-24 rounding of one f32 product
-// in the f32-MFMA (fmaf chain) path, and each 16-k MFMA rounds the accumulator once per limb
-// product (6 roundings per 16 k against 16 for the fmaf chain): the result is f32-accurate
-// (tests/test_gpu_gemm.py: max / mean error vs float64 within 1.25x of the exact-f32 MFMA's on the
-// same operands).  6 MFMAs at 1/16 the cost of the f32 MFMA's 8 per 16 k: a 2.67x higher
-// arithmetic roof (417 TF/s of f32 products against 157 TF/s).
+// a2 b2) and the split residues are at the level of one f32 product rounding (2^-24 |a b|; a few
+// times that in the worst case, far less on average since the limb ratios are spread over the
+// half-ulp range), and each 16-k MFMA rounds the accumulator once per limb product (6 roundings
+// per 16 k against 16 for the fmaf chain): the result is f32-accurate (tests/test_gpu_gemm.py:
+// max / mean error vs float64 within 1.25x of the exact-f32 MFMA's on the same operands).
+// 6 MFMAs at 1/16 the cost of the f32 MFMA's 8 per 16 k: a 2.67x higher arithmetic roof
+// (417 TF/s of f32 products against 157 TF/s).
 //
 // Same argument block, tile order (persistent workgroups, XCD-contiguous tile ranges) and fused
 // epilogues as gemm_nt_kernel (lgx_gemm_common.h).  Differences:
@@ -21,7 +22,7 @@
 //     32x32x16 MFMA reads k = 8h .. 8h+7 of its row (A) / column (B): one ds_read_b128 per limb;
 //   * the A operand (activations) is split once per element on its way into LDS
 //     (v_cvt_pk_bf16_f32 + exact f32 subtractions); the B operand (weights) comes pre-split from
-//     HBM ([n][k/32][limb][32] bf16, lgx_split_bf16 / the Adam step's limb mirrors) and is copied
+//     HBM (x3_limb_off layout, lgx_split_bf16 / the Adam step's limb mirrors) and is copied
 //     into LDS as 16-byte chunks - splitting B in the kernel would redo it for every one of the
 //     M / 128 row tiles;
 //   * 106 KB of LDS (two stages): one workgroup of 8 waves per CU; a three-slot software pipeline
@@ -92,11 +93,12 @@ __device__ __forceinline__ void offs_x(OffsX<BS>& o, const GemmArgs& g, int64_t 
     const int row = (tid >> 3) + Cfg<NWX>::RSTEP * i;
     o.a[i] = (uint32_t)(min(m_base + row, g.M - 1) * g.lda);   // rows past M load row M-1 (discarded)
   }
-  if (BS) {
+  if (BS) {   // tiled pre-split layout (x3_limb_off): limb cc / 4, 16-byte k-chunk cc % 4 of row n
 #pragma unroll
     for (int i = 0; i < BCH; ++i) {
       const int ch = tid + 64 * NWX * i, row = ch / 12, cc = ch - 12 * row;
-      o.b[i] = (uint32_t)(((n_base + row) * kb) * (LIMB_ROW * 2) + cc * 16);
+      o.b[i] = (uint32_t)((n_base / BN) * kb * (BN * LIMB_ROW * 2) + (cc >> 2) * (BN * BK * 2) + row * (BK * 2) +
+                          (((cc & 3) ^ ((row >> 2) & 3)) << 4));
     }
   } else {
 #pragma unroll
@@ -113,7 +115,7 @@ __device__ __forceinline__ void load_x(StageX<BS>& st, const GemmArgs& g, int z,
   for (int i = 0; i < Cfg<NWX>::NL; ++i) st.a[i] = *reinterpret_cast<const float4*>(Ab + (uint32_t)((o.a[i] + kc) * 4u));
   if constexpr (BS) {
     const int kb = (K + BK - 1) / BK;
-    const char* Bb = reinterpret_cast<const char*>(g.Bs) + (int64_t)z * g.N * kb * (LIMB_ROW * 2) + t * (LIMB_ROW * 2);
+    const char* Bb = reinterpret_cast<const char*>(g.Bs) + (int64_t)z * g.N * kb * (LIMB_ROW * 2) + t * (BN * LIMB_ROW * 2);
 #pragma unroll
     for (int i = 0; i < BCH; ++i) st.b[i] = *reinterpret_cast<const uint4*>(Bb + o.b[i]);
   } else {
@@ -393,18 +395,23 @@ __global__ void __launch_bounds__(256) split_rows_kernel(SplitJobs J) {
   const int b = (int)(l / nout);
   float x = 0.f;
   if (k < kout) x = jb.src[b * jb.src_bs + (tr ? (int64_t)k * jb.src_ld + n : (int64_t)n * jb.src_ld + k)];
-  uint16_t* d = reinterpret_cast<uint16_t*>(jb.dst) + b * jb.dst_bs + (int64_t)n * jb.dst_ld + (k / BK) * LIMB_ROW + k % BK;
+  uint16_t* d = reinterpret_cast<uint16_t*>(jb.dst) + b * jb.dst_bs + x3_limb_off(n, k, 0, kp / BK);
   uint32_t l0, l1, l2;
   split2(x, 0.f, l0, l1, l2);
-  d[0] = (uint16_t)l0;
-  d[BK] = (uint16_t)l1;
-  d[2 * BK] = (uint16_t)l2;
+  d[0] = (uint16_t)l0;                 // limb l at + l * 128 * 32 (x3_limb_off)
+  d[BN * BK] = (uint16_t)l1;
+  d[2 * BN * BK] = (uint16_t)l2;
 }
 
 }  // namespace
 
 // lgx_gemm_nt's split-bf16 path (lgx_gemm.hip checks the common arguments first)
 int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream_) {
+  static const bool pipelined = [] {   // A/B switch: LGX_GEMM_X3P=0 keeps the register-staged kernel
+    const char* e = getenv("LGX_GEMM_X3P");
+    return !(e && e[0] == '0');
+  }();
+  if (a.Bs && a.K % BK == 0 && pipelined) return lgx_gemm_nt_x3p(a, cus, stream_);
   const hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
              a.partials, 0, a.Bs};
@@ -452,9 +459,9 @@ extern "C" int lgx_split_bf16(const lgx_copy2d_job* jobs, int32_t njobs, void* s
     const lgx_copy2d_job& j = jobs[i];
     const int tr = j.transpose & 1;
     const int nout = tr ? j.cols : j.rows, kout = tr ? j.rows : j.cols;
-    if (!j.src || !j.dst || j.rows <= 0 || j.cols <= 0 || j.batch <= 0 || j.src_ld < j.cols ||
-        j.dst_ld < lgx_split_bf16_elems(1, kout) || j.dst_bs < (int64_t)nout * j.dst_ld)
-      return lgx_fail(LGX_EINVAL, "lgx_split_bf16: bad job");
+    if (!j.src || !j.dst || j.rows <= 0 || j.cols <= 0 || j.batch <= 0 || j.src_ld < j.cols || nout % BN ||
+        j.dst_bs < lgx_split_bf16_elems(nout, kout))
+      return lgx_fail(LGX_EINVAL, "lgx_split_bf16: bad job (output rows % 128, dst_bs)");
     J.job[i] = j;
     J.start[i] = total;
     total += (int64_t)j.batch * nout * ((kout + BK - 1) / BK * BK);

@@ -1,0 +1,652 @@
+// Pipelined split-bf16 GEMM of the PPO update (lgx_gemm_nt with a pre-split B operand):
+//   C[z][m][n] = epi( sum_k A[z][m][k] * B[z][n][k] ),  K % 32 == 0, N % 128 == 0.
+//
+// Same arithmetic as gemm_nt_x3_kernel (lgx_gemm_split.hip: three RNE bf16 limbs per f32
+// operand, the six limb products of order <= 2 on v_mfma_f32_32x32x16_bf16, f32 accumulation),
+// restructured around the load pipeline, which is what bounded that kernel: with one K stage of
+// register-staged prefetch and a barrier pair per 32-k stage, its loads were exposed once per
+// stage (measured: the kernel without its MFMAs took as long as the MFMA floor).
+//
+//   * 256 x 128 output tile per workgroup; one workgroup per CU (149 KB of LDS), persistent over
+//     XCD-contiguous tile ranges (consecutive tiles share A rows: L2 reuse on one XCD).  Wave
+//     layouts (template NWV): 4 waves = one per SIMD, 64 x 128 each (2 x 4 transposed 32x32
+//     accumulators) - no second wave competes for the SIMD's issue, so the barrier that closes
+//     every 32-k slot does not wait on a starved wave; 8 waves = two per SIMD, 64 x 64 each
+//     (measured with s_memtime stamps: the younger wave of each SIMD loses issue arbitration
+//     and the older one idles ~35 % of every slot at the barrier);
+//   * every global -> LDS copy is an LDS-DMA load (global_load_lds_dwordx4): no staging
+//     registers, no LDS write pass.  A (f32 activations) goes through a 3-deep ring of 32 KB
+//     stages, its 16-byte chunks placed at chunk ^ ((row >> 1) & 7) by the per-lane SOURCE
+//     address (the DMA writes lane-linear); B (pre-split weights, L2-resident) through a 2-deep
+//     ring of 24 KB stages copied verbatim - lgx_split_bf16 / the Adam limb mirrors already write
+//     the LDS image (x3_limb_off).  The A load of slot q+2 and the B load of slot q+1 are issued
+//     while slot q computes, across tile boundaries; one raw s_barrier per 32-k slot, counted
+//     vmcnt (the A stage still in flight stays in flight across the barrier); the DMA is
+//     inline asm, invisible to the compiler's own waits (which would otherwise drain it);
+//   * A is split into its limbs after the fragment read (8 floats per lane per 16 k: 12
+//     v_cvt_pk_bf16_f32 + exact f32 subtractions);
+//   * epilogues: bias + ELU / plain deferred into the next tile's slots (16-byte row stores of the
+//     transposed accumulators, a few per slot, under the MFMAs); ELU' + per-128-row column-sum
+//     partials at the tile's end (fixed summation order: bitwise reproducible).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "lgx_gemm_common.h"
+#include "lgx_internal.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float fx2 __attribute__((ext_vector_type(2)));
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+
+constexpr int PM = 256, PN = 128, PK = 32;
+constexpr int A_ST = PM * PK * 4;            // 32 KB: f32 A stage (256 rows x 128 B)
+constexpr int B_ST = 3 * PN * PK * 2;        // 24 KB: limb B stage ([limb][128 n][64 B])
+constexpr int NSA = 3, NSB = 2;              // ring depths
+constexpr int OFF_B = NSA * A_ST;
+constexpr int OFF_RED = OFF_B + NSB * B_ST;     // [4 wave rows][128] column partials
+constexpr int OFF_BIAS = OFF_RED + 4 * PN * 4;  // 3 x 1 KB: bias of the pending / current / next tile
+constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 152,576 B
+constexpr int B_BLK = 3 * 128 * 32;             // bf16 per pre-split (128 n x 32 k) block
+
+template <int NWV>
+struct XC {
+  static constexpr int WGN = NWV == 8 ? 2 : 1;          // waves along N
+  static constexpr int WGM = NWV / WGN;                  // waves along M (4)
+  static constexpr int WI = PM / WGM / 32;               // 32-row accumulator tiles per wave (2)
+  static constexpr int WJ = PN / WGN / 32;               // 32-column accumulator tiles per wave (2 | 4)
+  static constexpr int PT = 64 * NWV;
+  static constexpr int A_GL = A_ST / (PT * 16);          // LDS-DMA loads per thread per A stage (4 | 8)
+  static constexpr int B_GL = B_ST / (PT * 16);          // per B stage (3 | 6)
+  static constexpr int GROUPS = WI * WJ * 4;             // float4 output runs per lane (16 | 32)
+  static_assert(WGM == 4 && WI == 2, "column-sum pairing and A offsets assume 4 wave rows of 64");
+};
+
+struct PArgs {
+  int64_t M;
+  int32_t N, K, batch, kb;   // kb = K / 32
+  const float* A;
+  int64_t lda, sa;
+  const uint16_t* Bs;
+  int64_t sbs;               // batch stride of Bs (bf16 elements)
+  float* C;
+  int64_t ldc, sc;
+  const float* bias;
+  const float* Y;
+  float* partials;
+  int32_t tiles, ntn;
+};
+
+struct PTile {
+  int32_t mt, nt, z;
+};
+
+__device__ __forceinline__ PTile ptile(const PArgs& g, int32_t t) {
+  PTile T;
+  T.nt = t % g.ntn;
+  const int32_t r = t / g.ntn;
+  T.z = r % g.batch;
+  T.mt = r / g.batch;
+  return T;
+}
+
+// vmcnt-only waits (expcnt / lgkmcnt left alone)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void p_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// three RNE bf16 limbs of two floats, packed (low half = first element); both subtractions exact
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
+  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){x0, x1}, bf16x2));
+  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
+  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+  r0 -= __uint_as_float(l1 << 16);
+  r1 -= __uint_as_float(l1 & 0xffff0000u);
+  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+}
+
+__device__ __forceinline__ void split8(const float4& x, const float4& y, bf16x8 (&o)[3]) {
+  uint4 u0, u1, u2;
+  split2(x.x, x.y, u0.x, u1.x, u2.x);
+  split2(x.z, x.w, u0.y, u1.y, u2.y);
+  split2(y.x, y.y, u0.z, u1.z, u2.z);
+  split2(y.z, y.w, u0.w, u1.w, u2.w);
+  o[0] = __builtin_bit_cast(bf16x8, u0);
+  o[1] = __builtin_bit_cast(bf16x8, u1);
+  o[2] = __builtin_bit_cast(bf16x8, u2);
+}
+
+// One LDS-DMA load (global_load_lds_dwordx4): 16 bytes per lane from base + voff to LDS address
+// lds + 16 * lane.  Inline asm, so the compiler neither orders nor waits on it (its own waits
+// would drain the ring: it treats every later LDS-DMA / LDS read as aliasing a pending one);
+// the kernel counts vmcnt itself.  M0 is saved and restored around it.
+__device__ __forceinline__ void glds16(const char* base, uint32_t voff, uint32_t lds) {
+  uint32_t sv;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %2, %3\n\ts_mov_b32 m0, %0"
+               : "=&s"(sv)
+               : "s"(lds), "v"(voff), "s"(base)
+               : "memory");
+}
+
+__device__ __forceinline__ const char* uniform_ptr(const void* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return reinterpret_cast<const char*>(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const char* p) {
+  return (uint32_t)reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) const char*)(p));
+}
+
+// Per-lane A source offsets (bytes from the batch entry's base) of one tile's DMA loads: LDS
+// block b = A_GL * wave + i (1 KB) holds tile rows 8b .. 8b + 7; lane l writes row 8b + l / 8 at
+// chunk l % 8, which holds k-chunk (l % 8) ^ ((row >> 1) & 7).
+template <int NWV>
+struct AOffs {
+  uint32_t o[XC<NWV>::A_GL];
+};
+
+template <int NWV>
+__device__ __forceinline__ void a_offs(AOffs<NWV>& a, const PArgs& g, int32_t mt, int tid) {
+  constexpr int AG = XC<NWV>::A_GL;
+  const int w = tid >> 6, lane = tid & 63;
+#pragma unroll
+  for (int i = 0; i < AG; ++i) {
+    const int r = 8 * (AG * w + i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    const int64_t m = min((int64_t)mt * PM + r, g.M - 1);   // rows past M load row M-1 (never stored)
+    a.o[i] = (uint32_t)((m * g.lda + 4 * c) * 4);
+  }
+}
+
+// A / B stage issue split into its single loads: prepare once (uniform addresses), then load(i)
+struct DmaPlan {
+  const char* src;
+  uint32_t dst;
+};
+
+template <int NWV>
+__device__ __forceinline__ DmaPlan plan_a(uint32_t lds0, int buf, const PArgs& g, int z, int ks, int tid) {
+  constexpr int AG = XC<NWV>::A_GL;
+  return DmaPlan{uniform_ptr(reinterpret_cast<const char*>(g.A + z * g.sa) + ks * (PK * 4)),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + buf * A_ST + (tid >> 6) * (AG * 1024))};
+}
+
+template <int NWV>
+__device__ __forceinline__ DmaPlan plan_b(uint32_t lds0, int buf, const PArgs& g, const PTile& T, int ks, int tid) {
+  constexpr int BG = XC<NWV>::B_GL;
+  return DmaPlan{uniform_ptr(reinterpret_cast<const char*>(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb + ks) * B_BLK) +
+                             (tid >> 6) * (BG * 1024)),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + OFF_B + buf * B_ST + (tid >> 6) * (BG * 1024))};
+}
+
+template <int NWV>
+__device__ __forceinline__ void issue_a(uint32_t lds0, int buf, const PArgs& g, const AOffs<NWV>& a, int z, int ks,
+                                        int tid) {
+  constexpr int AG = XC<NWV>::A_GL;
+  const char* src = uniform_ptr(reinterpret_cast<const char*>(g.A + z * g.sa) + ks * (PK * 4));
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * A_ST + (tid >> 6) * (AG * 1024));
+#pragma unroll
+  for (int i = 0; i < AG; ++i) glds16(src, a.o[i], dst + i * 1024);
+}
+
+// B stage of slot (T, ks); with `bias` (BIAS_ELU, a tile's first stage, wave 0 only) also the
+// tile's 128 bias values into bias buffer `bbuf` (lanes 32-63 duplicate lanes 0-31).  The extra
+// load is issued with the B stage, so every vmcnt count of the pipeline stays the same.
+template <int NWV>
+__device__ __forceinline__ void issue_b(uint32_t lds0, int buf, const PArgs& g, const PTile& T, int ks, int tid,
+                                        bool bias, int bbuf) {
+  constexpr int BG = XC<NWV>::B_GL;
+  const int w = tid >> 6, lane = tid & 63;
+  const char* src = uniform_ptr(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb + ks) * B_BLK);
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + OFF_B + buf * B_ST + w * (BG * 1024));
+#pragma unroll
+  for (int i = 0; i < BG; ++i) glds16(src, (uint32_t)(w * (BG * 1024) + i * 1024 + lane * 16), dst + i * 1024);
+  if (bias)
+    glds16(uniform_ptr(g.bias + (int64_t)T.z * g.N + T.nt * PN), (uint32_t)((lane & 31) * 16),
+           __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
+}
+
+// One 32-k slot of a wave's WI x WJ accumulators: per 16-k half, its A row tiles are read (f32)
+// and split into limbs, its B column tiles read (limbs), 6 MFMAs per accumulator (small limb
+// products first).  Conflict-free reads: A chunk c of row R at c ^ ((R >> 1) & 7); B chunk c of
+// column n at c ^ ((n >> 2) & 3).
+//
+// side(b) runs after accumulator block b (b = 0 .. 2 WI WJ - 1 in issue order): the slot's DMA
+// issues and deferred stores are spread between the MFMA blocks, where a DMA issue that waits for
+// the texture unit to accept it costs no MFMA time (issued in one burst before the compute, the 14
+// DMA loads of a 4-wave slot took ~950 cycles of the wave's ~5600).
+template <int NWV, typename Side>
+__device__ __forceinline__ void compute_slot(const char* __restrict__ la, const char* __restrict__ lb, int wm, int wn,
+                                             int r, int h, f32x16v (&acc)[2][XC<NWV>::WJ], Side&& side) {
+  constexpr int WI = XC<NWV>::WI, WJ = XC<NWV>::WJ;
+  const int sa = (r >> 1) & 7, sb = (r >> 2) & 3;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int ca = 4 * s + 2 * h, cb = 2 * s + h;
+    bf16x8 a[WI][3], b[WJ][3];
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+      const char* row = la + (wm * 32 * WI + 32 * i + r) * (PK * 4);
+      const float4 x = *reinterpret_cast<const float4*>(row + 16 * (ca ^ sa));
+      const float4 y = *reinterpret_cast<const float4*>(row + 16 * ((ca + 1) ^ sa));
+#ifndef X3P_NO_SPLIT
+      split8(x, y, a[i]);
+#else   // A/B: raw bits as limbs (wrong results; measures the split's VALU cost)
+      a[i][0] = __builtin_bit_cast(bf16x8, x);
+      a[i][1] = __builtin_bit_cast(bf16x8, y);
+      a[i][2] = __builtin_bit_cast(bf16x8, x);
+#endif
+    }
+#pragma unroll
+    for (int j = 0; j < WJ; ++j)
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+        b[j][l] =
+            *reinterpret_cast<const bf16x8*>(lb + l * (PN * 64) + (wn * 32 * WJ + 32 * j + r) * 64 + 16 * (cb ^ sb));
+#pragma unroll
+    for (int i = 0; i < WI; ++i)
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) {
+#ifdef X3P_NO_MFMA   // A/B: keep the fragment reads / split alive, no MFMA
+        acc[i][j][0] += (float)a[i][0][0] + (float)a[i][1][1] + (float)a[i][2][2] + (float)b[j][0][0] +
+                        (float)b[j][1][3] + (float)b[j][2][5];
+        continue;
+#endif
+        f32x16v c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][2], a[i][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][1], a[i][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][1], a[i][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][0], c, 0, 0, 0);
+        acc[i][j] = c;
+        side((s * WI + i) * WJ + j);
+      }
+  }
+}
+
+__device__ __forceinline__ float4 q4(const f32x16v& v, int q) {
+  return make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+}
+
+// acc[i][j][4q + e] = C[m0 + 32i + r][n0 + 32j + 8q + 4h + e]: the ELU' + column-sum epilogue at
+// the tile's end (Y rows past M are read from row M-1 and discarded).
+template <int NWV>
+__device__ __forceinline__ void p_epilogue_delu(const PArgs& g, const f32x16v (&acc)[2][XC<NWV>::WJ], const PTile& T,
+                                                int wm, int wn, int r, int h, float* red) {
+  constexpr int WJ = XC<NWV>::WJ;
+  const int64_t m0 = (int64_t)T.mt * PM + wm * 64;
+  const int n0 = T.nt * PN + wn * 32 * WJ;
+  const int64_t ldc = g.ldc;
+  float* C = g.C + T.z * g.sc + n0 + 4 * h;
+  const float* Y = g.Y + T.z * g.sc + n0 + 4 * h;
+  float4 cs[WJ][4];
+#pragma unroll
+  for (int j = 0; j < WJ; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cs[j][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const bool ok = m0 + 32 * i + r < g.M;
+    const int64_t ro = min(m0 + 32 * i + r, g.M - 1) * ldc;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) {
+      float4 y[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = *reinterpret_cast<const float4*>(Y + ro + 32 * j + 8 * q);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 d = q4(acc[i][j], q);
+        d.x *= elu_grad_from_out(y[q].x);
+        d.y *= elu_grad_from_out(y[q].y);
+        d.z *= elu_grad_from_out(y[q].z);
+        d.w *= elu_grad_from_out(y[q].w);
+        if (ok) {
+          *reinterpret_cast<float4*>(C + ro + 32 * j + 8 * q) = d;
+          cs[j][q].x += d.x;
+          cs[j][q].y += d.y;
+          cs[j][q].z += d.z;
+          cs[j][q].w += d.w;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int sh = 1; sh < 32; sh <<= 1)
+#pragma unroll
+    for (int j = 0; j < WJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        cs[j][q].x += __shfl_xor(cs[j][q].x, sh);
+        cs[j][q].y += __shfl_xor(cs[j][q].y, sh);
+        cs[j][q].z += __shfl_xor(cs[j][q].z, sh);
+        cs[j][q].w += __shfl_xor(cs[j][q].w, sh);
+      }
+  const int cl = wn * 32 * WJ + 4 * h;
+  if (r == 0) {
+#pragma unroll
+    for (int j = 0; j < WJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(red + wm * PN + cl + 32 * j + 8 * q) = cs[j][q];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  p_barrier();
+  // partial row t = 128-row chunk: wave rows (0, 1) -> 2 mt, (2, 3) -> 2 mt + 1, summed in order
+  if ((wm & 1) == 0 && h == 0) {
+    const int64_t t = 2 * (int64_t)T.mt + (wm >> 1);
+    if (t * 128 < g.M) {
+      float* P = g.partials + t * ((int64_t)g.batch * g.N) + (int64_t)T.z * g.N + T.nt * PN;
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) {
+        const int col = wn * 32 * WJ + 32 * j + r;
+        P[col] = red[wm * PN + col] + red[(wm + 1) * PN + col];
+      }
+    }
+  }
+}
+
+// Bias + ELU (or plain) output of float4 run gi = (i, j, q), gi = 4 (WJ i + j) + q, of a lane.
+template <int EPI, int NWV>
+__device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pend)[2][XC<NWV>::WJ], const PTile& T,
+                                              int wm, int wn, int r, int h, const float* bias_lds, int gi) {
+  constexpr int WJ = XC<NWV>::WJ;
+  const int q = gi & 3, j = (gi >> 2) % WJ, i = (gi >> 2) / WJ;
+  const int64_t row = (int64_t)T.mt * PM + wm * 64 + 32 * i + r;
+  const int cn = wn * 32 * WJ + 32 * j + 8 * q + 4 * h;
+  float4 v = q4(pend[i][j], q);
+  if (EPI == LGX_GEMM_BIAS_ELU) {
+    const float4 bq = *reinterpret_cast<const float4*>(bias_lds + cn);
+    v.x = elu_f(v.x + bq.x);
+    v.y = elu_f(v.y + bq.y);
+    v.z = elu_f(v.z + bq.z);
+    v.w = elu_f(v.w + bq.w);
+  }
+  if (row < g.M) *reinterpret_cast<float4*>(g.C + T.z * g.sc + row * g.ldc + T.nt * PN + cn) = v;
+}
+
+#ifdef X3P_CLOCK   // A/B instrumentation: per-slot s_memtime stamps of workgroup 0 into g.partials
+#define X3P_STAMP(e) \
+  if (clk && q < 32) clk[(wave * 32 + q) * 8 + (e)] = __builtin_amdgcn_s_memtime()
+#else
+#define X3P_STAMP(e)
+#endif
+
+// Slot q = (the workgroup's j-th tile, K stage k), q = j * kb + k.  Iteration q: wait for slot q's
+// A and B stages (the A stage of slot q+1, issued after them, and the deferred stores issued after
+// that, stay in flight: vmcnt is an in-order count), barrier (every wave's DMA for slot q landed;
+// every wave is done with slot q-1's buffers), issue B(q+1) and A(q+2) into the buffers slot q-1
+// used, write this slot's share of the previous tile's output, compute slot q.
+//
+// KBT > 0: K = 32 KBT known at compile time, the k loop unrolled and the BIAS_ELU / PLAIN
+// epilogue deferred into the next tile's slots (GROUPS / KBT store runs per slot: constant
+// register indices).  KBT == 0, or the column-sum epilogue: the epilogue runs at the tile's end
+// (after waiting for the next slot's stages, so its stores do not sit in front of them).
+template <int EPI, int KBT, int NWV>
+__global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
+  using X = XC<NWV>;
+  constexpr int WJ = X::WJ, AG = X::A_GL;
+  extern __shared__ __attribute__((aligned(16))) char plds[];
+  constexpr bool DEFER = KBT > 0 && EPI != LGX_GEMM_DELU_COLSUM;
+  constexpr int GPS = DEFER ? X::GROUPS / KBT : 0;     // deferred store runs per slot
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave / X::WGN, wn = wave % X::WGN;
+  const int xcd = blockIdx.x & 7;
+  const int32_t stride = gridDim.x >> 3;   // grid is a multiple of 8
+  const int32_t lo = (int32_t)((int64_t)xcd * g.tiles / 8), hi = (int32_t)((int64_t)(xcd + 1) * g.tiles / 8);
+  const int32_t t0 = lo + (blockIdx.x >> 3);
+  if (t0 >= hi) return;
+  const int32_t ntiles = (hi - t0 + stride - 1) / stride;
+  const int kb = KBT > 0 ? KBT : g.kb;
+  const int32_t nslots = ntiles * kb;
+  const uint32_t lds0 = lds_addr(plds);
+#ifdef X3P_CLOCK
+  uint64_t* clk = (blockIdx.x == 0 && lane == 0) ? reinterpret_cast<uint64_t*>(g.partials) : nullptr;
+#endif
+
+  // A issue iterator (runs 2 slots ahead), B issue iterator (1 slot ahead)
+  int32_t ja = 0, jb = 0;
+  PTile Ta = ptile(g, t0), Tb = Ta;
+  int ka = 0, kbb = 0;
+  AOffs<NWV> ao;
+  a_offs<NWV>(ao, g, Ta.mt, tid);
+  auto next_a = [&]() {
+    if (++ka == kb) {
+      ka = 0;
+      Ta = ptile(g, t0 + (++ja) * stride);
+      a_offs<NWV>(ao, g, Ta.mt, tid);
+    }
+  };
+  auto next_b = [&]() {
+    if (++kbb == kb) {
+      kbb = 0;
+      Tb = ptile(g, t0 + (++jb) * stride);
+    }
+  };
+  // prologue: A(0), B(0), A(1)
+  constexpr bool BIAS = EPI == LGX_GEMM_BIAS_ELU;
+  const bool w0 = __builtin_amdgcn_readfirstlane(wave) == 0;
+  issue_a<NWV>(lds0, 0, g, ao, Ta.z, ka, tid);
+  next_a();
+  issue_b<NWV>(lds0, 0, g, Tb, kbb, tid, BIAS && w0, 0);
+  next_b();
+  if (nslots > 1) {
+    issue_a<NWV>(lds0, 1, g, ao, Ta.z, ka, tid);
+    next_a();
+  }
+
+  f32x16v acc[2][WJ], pend[2][WJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < WJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = pend[i][j][e] = 0.f;
+  PTile Tp{0, 0, 0};           // tile whose output is pending (DEFER)
+  bool pending = false, pend_full = false;
+  int32_t q = 0;
+  bool waited = false;         // (!DEFER) the epilogue already waited for the next slot's stages
+  bool stores = false;         // (DEFER) GPS deferred stores issued in the previous iteration
+  for (int32_t tj = 0; tj < ntiles; ++tj) {
+    const PTile T = ptile(g, t0 + tj * stride);
+#pragma unroll(KBT > 0 ? KBT : 1)
+    for (int k = 0; k < kb; ++k, ++q) {
+      X3P_STAMP(0);
+      if (!waited) {
+        // slot q's stages; A(q+1) (AG loads) and last iteration's stores may stay in flight
+        if (q + 1 < nslots) {
+          if (DEFER && stores) wait_vm<AG + GPS>();
+          else wait_vm<AG>();
+        } else {
+          if (DEFER && stores) wait_vm<GPS>();
+          else wait_vm<0>();
+        }
+      }
+      waited = false;
+      X3P_STAMP(1);
+      p_barrier();
+      X3P_STAMP(2);
+      // slot q+1's B stage and slot q+2's A stage (same order as always: B, bias, A), and this
+      // slot's share of the pending output, spread over the MFMA blocks of compute(q)
+      const bool do_b = q + 1 < nslots, do_a = q + 2 < nslots;
+      const bool do_bias = BIAS && w0 && kbb == 0 && do_b;
+      const int bbuf = jb % 3;
+      DmaPlan pb{nullptr, 0}, pa{nullptr, 0};
+      int za = 0;
+      if (do_b) pb = plan_b<NWV>(lds0, (q + 1) % NSB, g, Tb, kbb, tid);
+      const PTile Tbias = Tb;
+      if (do_a) {
+        pa = plan_a<NWV>(lds0, (q + 2) % NSA, g, Ta.z, ka, tid);
+        za = Ta.z;
+      }
+      (void)za;
+      const AOffs<NWV> aoq = ao;
+      if (do_b) next_b();
+      if (do_a) next_a();
+      X3P_STAMP(3);
+      const bool st_now = DEFER && pending && k * GPS < X::GROUPS;
+      stores = DEFER && st_now && pend_full;
+      const float* bias_prev = reinterpret_cast<const float*>(plds + OFF_BIAS + ((tj + 2) % 3) * 1024);
+      constexpr int BG = X::B_GL;
+      auto side = [&](int blk) {
+        // blocks 0 .. BG-1: B loads; BG: bias; BG+1 .. BG+AG: A loads; then the stores
+        if (blk < BG) {
+          if (do_b) glds16(pb.src, (uint32_t)(lane * 16 + blk * 1024), pb.dst + blk * 1024);
+        } else if (blk == BG) {
+          if (do_bias)
+            glds16(uniform_ptr(g.bias + (int64_t)Tbias.z * g.N + Tbias.nt * PN), (uint32_t)((lane & 31) * 16),
+                   __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
+        } else if (blk <= BG + AG) {
+          if (do_a) glds16(pa.src, aoq.o[blk - BG - 1], pa.dst + (blk - BG - 1) * 1024);
+        }
+        if constexpr (DEFER) {
+          constexpr int NB = 2 * X::WI * X::WJ;   // MFMA blocks per slot (2 halves)
+          static_assert(NB >= GPS && NB > BG + AG, "every DMA load and store run gets a block");
+          // the stores after the last GPS blocks (they may interleave with A(q+2)'s loads: the
+          // next wait only needs B(q+1), which precedes both)
+          const int u = blk - (NB - GPS);
+          if (st_now && u >= 0 && u < GPS)
+            p_store_group<EPI, NWV>(g, pend, Tp, wm, wn, r, h, bias_prev, k * GPS + u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      X3P_STAMP(4);
+#ifndef X3P_NO_COMPUTE
+      compute_slot<NWV>(plds + (q % NSA) * A_ST, plds + OFF_B + (q % NSB) * B_ST, wm, wn, r, h, acc, side);
+#else
+      for (int blk = 0; blk < 2 * X::WI * X::WJ; ++blk) side(blk);
+#endif
+      X3P_STAMP(5);
+    }
+    // ---- tile end
+    if constexpr (DEFER) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) pend[i][j] = acc[i][j];
+      Tp = T;
+      pending = true;
+      pend_full = (int64_t)T.mt * PM + PM <= g.M;
+    } else {
+      if (q + 1 < nslots) wait_vm<AG>();   // (q = the next slot) its stages; A(q+1) may stay in flight
+      else wait_vm<0>();
+      waited = true;
+#ifndef X3P_NO_EPI
+      if constexpr (EPI == LGX_GEMM_DELU_COLSUM) {
+        p_epilogue_delu<NWV>(g, acc, T, wm, wn, r, h, reinterpret_cast<float*>(plds + OFF_RED));
+      } else {
+#pragma unroll
+        for (int gi = 0; gi < X::GROUPS; ++gi)
+          p_store_group<EPI, NWV>(g, acc, T, wm, wn, r, h,
+                                  reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
+      }
+#else
+      if (acc[0][0][0] == 1234.5f) g.C[tid] = acc[1][1][3] + acc[0][1][2] + acc[1][0][1];
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < WJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  }
+  if constexpr (DEFER) {   // the last tile's output (no further slots to spread it over)
+#ifndef X3P_NO_EPI
+#pragma unroll
+    for (int gi = 0; gi < X::GROUPS; ++gi)
+      p_store_group<EPI, NWV>(g, pend, Tp, wm, wn, r, h,
+                              reinterpret_cast<const float*>(plds + OFF_BIAS + ((ntiles - 1) % 3) * 1024), gi);
+#else
+    if (pend[0][0][0] == 1234.5f) g.C[tid] = pend[1][1][3] + pend[0][1][2] + pend[1][0][1];
+#endif
+  }
+}
+
+typedef void (*x3p_fn)(PArgs);
+
+// [epilogue][KBT index: 0 (runtime K), 4, 8, 16]
+template <int NWV>
+struct X3PTable {
+  static constexpr x3p_fn k[3][4] = {
+      {&gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 0, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 4, NWV>,
+       &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 16, NWV>},
+      {&gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 0, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 4, NWV>,
+       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV>},
+      {&gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 0, NWV>, nullptr, nullptr, nullptr}};
+};
+
+template <int NWV>
+bool x3p_attrs() {
+  bool ok = true;
+  for (const auto& row : X3PTable<NWV>::k)
+    for (x3p_fn f : row)
+      if (f)
+        ok &= hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  P_LDS) == hipSuccess;
+  return ok;
+}
+
+}  // namespace
+
+// lgx_gemm_nt with a pre-split B (x3_limb_off layout), K % 32 == 0 (checked by the caller)
+int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
+  const hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+  PArgs g;
+  g.M = a.M;
+  g.N = a.N;
+  g.K = a.K;
+  g.batch = a.batch;
+  g.kb = a.K / PK;
+  g.A = a.A;
+  g.lda = a.lda;
+  g.sa = a.sa;
+  g.Bs = a.Bs;
+  g.sbs = (int64_t)a.N * g.kb * 96;
+  g.C = a.C;
+  g.ldc = a.ldc;
+  g.sc = a.sc;
+  g.bias = a.bias;
+  g.Y = a.Y;
+  g.partials = a.partials;
+  g.ntn = a.N / PN;
+  const int64_t tiles = ((a.M + PM - 1) / PM) * g.ntn * a.batch;
+  if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too many tiles");
+  g.tiles = (int32_t)tiles;
+  if (((uintptr_t)a.Bs & 15) || a.M * a.lda * 4 >= (1ll << 32))
+    return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: pre-split B must be 16-byte aligned; A < 4 GB per batch entry");
+  // K = 128 / 256 / 512 (the PPO-update layers): the k loop unrolled, BIAS_ELU / PLAIN epilogue
+  // deferred into the next tile; other K: the runtime loop with the epilogue at the tile's end.
+  // A/B switches: LGX_GEMM_DEFER=0, LGX_GEMM_X3P_WAVES=4 (8 measured 2-8 % faster on the update shapes)
+  static const bool defer = [] {
+    const char* e = getenv("LGX_GEMM_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  static const int nwv = [] {
+    const char* e = getenv("LGX_GEMM_X3P_WAVES");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  static const bool attrs = x3p_attrs<4>() && x3p_attrs<8>();
+  if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_nt: hipFuncSetAttribute (dynamic LDS) failed");
+  const int kbt = (defer && a.epi != LGX_GEMM_DELU_COLSUM && (g.kb == 4 || g.kb == 8 || g.kb == 16)) ? g.kb : 0;
+  const int ki = kbt == 0 ? 0 : kbt == 4 ? 1 : kbt == 8 ? 2 : 3;
+  const x3p_fn f = nwv == 8 ? X3PTable<8>::k[a.epi][ki] : X3PTable<4>::k[a.epi][ki];
+  // persistent: one workgroup per CU, a multiple of 8 (XCD tile ranges)
+  const int64_t per_xcd = (g.tiles + 7) / 8;
+  const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
+  LGX_LAUNCH(f, dim3((unsigned)wgs), dim3(64 * nwv), P_LDS, stream, g);
+  return lgx_hip_status("lgx_gemm_nt");
+}

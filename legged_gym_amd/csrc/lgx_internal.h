@@ -57,10 +57,23 @@ extern thread_local lgx_timing_slot lgx_timing;
     }                                                                                            \
   } while (0)
 
+// Pre-split (split-bf16) GEMM operand layout: the LDS image of every 128-column x 32-k block,
+// [n / 128][k / 32][limb][n % 128][32 k], the four 16-byte k-chunks of a 64-byte row stored at
+// chunk ^ ((n >> 2) & 3) so the 32x32x16 fragment reads (ds_read_b128) are bank-conflict free.
+// Offset (bf16 units) of element (n, k) limb `limb` within one batch entry; kb = ceil(K / 32).
+// One batch entry holds N * kb * 96 elements (lgx_split_bf16_elems); N % 128 == 0.
+__host__ __device__ inline int64_t x3_limb_off(int n, int k, int limb, int kb) {
+  const int nn = n & 127, kk = k & 31;
+  return ((int64_t)((n >> 7) * kb + (k >> 5)) * 3 + limb) * (128 * 32) + nn * 32 +
+         ((((kk >> 3) ^ ((nn >> 2) & 3))) << 3) + (kk & 7);
+}
+
 // error reporting shared by the translation units (thread-local message, lgx_last_error)
 int lgx_fail(int code, const char* msg);
 // lgx_gemm_split.hip: the split-bf16 path of lgx_gemm_nt (arguments already checked)
 int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream);
+// lgx_gemm_x3p.hip: pipelined split-bf16 path (pre-split B, K % 32 == 0)
+int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream);
 int lgx_hip_status(const char* what);  // LGX_OK or LGX_EHIP from hipGetLastError()
 
 // a batch of reduction jobs passed by value to one launch (lgx_reduce_slices)

@@ -565,14 +565,14 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
         const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
         if (J.transpose & 2) {   // bf16 limb layout of lgx_split_bf16 (split-bf16 GEMM operand)
           const int32_t nn = (J.transpose & 1) ? cc : rr, kk = (J.transpose & 1) ? rr : cc;
-          uint16_t* d = reinterpret_cast<uint16_t*>(J.dst) + b * J.dst_bs + (int64_t)nn * J.dst_ld + (kk >> 5) * 96 +
-                        (kk & 31);
+          const int32_t kout = (J.transpose & 1) ? J.rows : J.cols;
+          uint16_t* d = reinterpret_cast<uint16_t*>(J.dst) + b * J.dst_bs + x3_limb_off(nn, kk, 0, (kout + 31) >> 5);
           const uint16_t l0 = bf16_rne(pi);
           const float r1 = pi - __uint_as_float((uint32_t)l0 << 16);
           const uint16_t l1 = bf16_rne(r1);
-          d[0] = l0;
-          d[32] = l1;
-          d[64] = bf16_rne(r1 - __uint_as_float((uint32_t)l1 << 16));
+          d[0] = l0;                   // limb l at + l * 128 * 32
+          d[4096] = l1;
+          d[8192] = bf16_rne(r1 - __uint_as_float((uint32_t)l1 << 16));
         } else {
           J.dst[b * J.dst_bs + (J.transpose ? (int64_t)cc * J.dst_ld + rr : (int64_t)rr * J.dst_ld + cc)] = pi;
         }
@@ -762,6 +762,8 @@ extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int6
     if (!j.dst || j.rows <= 0 || j.cols <= 0 || j.batch <= 0 || j.src_ld != j.cols ||
         (j.batch > 1 && j.src_bs != (int64_t)j.rows * j.cols) || off < 0 || off + count > n || count >= (1LL << 31))
       return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: mirror source must be a contiguous block of p");
+    if ((j.transpose & 2) && (((j.transpose & 1) ? j.cols : j.rows) % 128))   // x3_limb_off: N % 128
+      return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: a limb mirror needs output rows % 128 == 0");
     M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose};
   }
   hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);

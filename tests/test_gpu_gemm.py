@@ -43,11 +43,27 @@ def _presplit(B, transpose=False):
     return Bs
 
 
-def _limbs_to_f32(Bs, batch, nout, kout):
+def _limb_index(nout, kout, device):
+    """x3_limb_off (lgx_internal.h): [3, nout, kb*32] offsets of the tiled pre-split layout."""
+    kb = -(-kout // 32)
+    n = torch.arange(nout, device=device)[:, None]
+    k = torch.arange(kb * 32, device=device)[None, :]
+    nn, kk = n & 127, k & 31
+    base = (n >> 7) * kb + (k >> 5)
+    inner = nn * 32 + (((kk >> 3) ^ ((nn >> 2) & 3)) << 3) + (kk & 7)
+    return torch.stack([(base * 3 + l) * 4096 + inner for l in range(3)])
+
+
+def _limbs(Bs, batch, nout, kout):
+    """[batch, 3, nout, kb*32] limbs as float64 from the tiled pre-split layout."""
     ld = _lib().lgx_split_bf16_elems(1, kout)
-    u = Bs.view(batch, nout, ld // 96, 3, 32).to(torch.int32) & 0xFFFF
-    f = (u << 16).view(torch.float32).double()
-    return f.sum(3).reshape(batch, nout, -1)
+    idx = _limb_index(nout, kout, Bs.device)
+    u = Bs.view(batch, nout * ld)[:, idx].to(torch.int32) & 0xFFFF
+    return (u << 16).view(torch.float32).double()
+
+
+def _limbs_to_f32(Bs, batch, nout, kout):
+    return _limbs(Bs, batch, nout, kout).sum(1)
 
 
 def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0, algo=abi.GEMM_ALGO_DEFAULT, presplit=False):
@@ -101,31 +117,57 @@ def test_gemm_epilogues(gpu, epi, algo):
 
 
 @pytest.mark.parametrize("epi", [abi.GEMM_PLAIN, abi.GEMM_BIAS_ELU, abi.GEMM_DELU_COLSUM])
-@pytest.mark.parametrize("M,N,K", [(384, 256, 256), (300, 128, 240), (1, 128, 36), (4096, 512, 512)])
+@pytest.mark.parametrize("M,N,K", [(384, 256, 256), (300, 128, 240), (1, 128, 36), (4096, 512, 512), (300, 128, 256),
+                                   (1, 128, 32), (257, 384, 64), (513, 256, 128)])
 def test_gemm_presplit_weights(gpu, epi, M, N, K):
-    """Split-bf16 path with B pre-split by lgx_split_bf16 (the weights of the PPO GEMMs)."""
+    """Split-bf16 path with B pre-split by lgx_split_bf16 (the weights of the PPO GEMMs): K % 32 == 0
+    runs the pipelined LDS-DMA kernel (gemm_nt_x3p_kernel; ragged M, 1 row, several N tiles),
+    other K the register-staged one; both read the tiled x3_limb_off layout."""
     _run(M, N, K, 2, epi, seed=M + K, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+
+
+@pytest.mark.parametrize("epi", [abi.GEMM_BIAS_ELU, abi.GEMM_DELU_COLSUM])
+def test_gemm_presplit_update_shape(gpu, epi):
+    """The PPO-update shape (24,576 rows, 512 outputs, K 256; layer 1 with one input shared by
+    actor and critic): every persistent workgroup walks several tiles, so the load ring runs
+    across tile boundaries and the bias / column-sum epilogues of consecutive tiles."""
+    _run(24576, 512, 256, 2, epi, shared_a=epi == abi.GEMM_BIAS_ELU, seed=11, algo=abi.GEMM_ALGO_SPLIT_BF16,
+         presplit=True)
 
 
 @pytest.mark.parametrize("transpose", [False, True])
 def test_split_bf16_limbs(gpu, transpose):
-    """lgx_split_bf16: limbs are RNE bf16 (x0 = bf16(x), |x1| <= 2^-9|x|, |x2| <= 2^-18|x|),
-    their sum reproduces x to 2^-26 relative, padding to the 32-k block is zero."""
+    """lgx_split_bf16: limbs are RNE bf16 (x0 = bf16(x), |x1| <= 2^-8|x0|, |x2| <= 2^-8|x1|),
+    their sum reproduces x to 2^-26 relative, padding to the 32-k block is zero; every element
+    of the buffer is written (tiled x3_limb_off layout)."""
     g = torch.Generator(device="cuda:0").manual_seed(2)
-    B = torch.randn(2, 70, 45, device="cuda:0", generator=g) * torch.exp2(
-        torch.randint(-20, 20, (2, 70, 45), device="cuda:0", generator=g).float())
+    shape = (2, 45, 256) if transpose else (2, 256, 45)
+    B = torch.randn(*shape, device="cuda:0", generator=g) * torch.exp2(
+        torch.randint(-20, 20, shape, device="cuda:0", generator=g).float())
     Bs = _presplit(B, transpose)
     torch.cuda.synchronize()
+    assert not bool((Bs == -1).any())
     ref = (B.transpose(1, 2) if transpose else B).double()
     nout, kout = ref.shape[1], ref.shape[2]
-    rec = _limbs_to_f32(Bs, 2, nout, kout)
+    limbs = _limbs(Bs, 2, nout, kout)
+    rec = limbs.sum(1)
     assert torch.all(rec[..., kout:] == 0)
     rec = rec[..., :kout]
     assert bool(((rec - ref).abs() <= 2.0 ** -26 * ref.abs()).all())
-    ld = _lib().lgx_split_bf16_elems(1, kout)
-    x0 = ((Bs.view(2, nout, ld // 96, 3, 32)[:, :, :, 0].to(torch.int32) & 0xFFFF) << 16).view(torch.float32)
-    x0 = x0.reshape(2, nout, -1)[..., :kout]
+    x0 = limbs[:, 0, :, :kout].float()
     assert torch.equal(x0, (B.transpose(1, 2) if transpose else B).to(torch.bfloat16).float())
+    assert bool((limbs[:, 1].abs() <= 2.0 ** -8 * limbs[:, 0].abs()).all())   # half a bf16 ulp
+    assert bool((limbs[:, 2].abs() <= 2.0 ** -8 * limbs[:, 1].abs()).all())
+
+
+def test_split_bf16_rejects_ragged_rows(gpu):
+    B = torch.zeros(1, 100, 64, device="cuda:0")
+    j = abi.LgxCopy2dJob()
+    Bs = torch.zeros(1 << 16, dtype=torch.int16, device="cuda:0")
+    j.src, j.dst = B.data_ptr(), Bs.data_ptr()
+    j.src_ld, j.src_bs, j.dst_ld, j.dst_bs = 64, 6400, 192, 100 * 192
+    j.rows, j.cols, j.batch, j.transpose = 100, 64, 1, 0
+    assert _lib().lgx_split_bf16((abi.LgxCopy2dJob * 1)(j), 1, _stream()) != 0
 
 
 @pytest.mark.parametrize("algo", ALGOS)

@@ -166,6 +166,19 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
             a.algo = min(algo, 2)
             a.Bs = Bs.data_ptr() if algo == 3 else None
             t1 = timeit(lambda: lib.lgx_gemm_nt(C.byref(a), stream), iters=iters)
+            if os.environ.get("KB_CLOCK"):   # X3P_CLOCK build: per-slot stamps of workgroup 0
+                parts.zero_()
+                lgxlib.check(lib.lgx_gemm_nt(C.byref(a), stream), "gemm")
+                torch.cuda.synchronize()
+                st = parts.view(torch.int64)[:8 * 32 * 8].view(8, 32, 8).double().cpu()
+                valid = (st[:, :, 5] > 0) & (st[:, :, 0] > 0)
+                for w in range(8):
+                    v = valid[w]
+                    d = st[w][v]
+                    seg = [(d[:, e + 1] - d[:, e]).mean().item() for e in range(5)]
+                    tot = (d[1:, 0] - d[:-1, 0]).mean().item() if v.sum() > 1 else 0
+                    print(f"  wave {w}: slots {int(v.sum())} per-slot cycles {tot:.0f}: wait {seg[0]:.0f} "
+                          f"barrier {seg[1]:.0f} issue {seg[2]:.0f} stores {seg[3]:.0f} compute {seg[4]:.0f}", flush=True)
             print(f"gemm M={M} N={n_} K={k_} epi={epi} algo={algo} waves={waves}: lgx {t1*1e3:.1f} us "
                   f"{f/t1/1e9:.1f} TF/s", flush=True)
         os.environ.pop("LGX_GEMM_WAVES")

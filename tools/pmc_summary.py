@@ -34,6 +34,7 @@ for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv")))
             for d, v in vals:
                 per[d] += v
             res[k][c] = sum(per.values()) / len(per)
+            res[k]["dispatches"] = len(per)
     out["passes"][name] = res
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out["passes"], indent=1)[:3000])
