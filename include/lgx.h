@@ -200,9 +200,9 @@ int lgx_version(void);
 
 /* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers), sizeof(lgx_mlp_desc),
  * sizeof(lgx_ppo_loss_args), sizeof(lgx_reduce_job), sizeof(lgx_ppo_act_args),
- * sizeof(lgx_ppo_store_args), sizeof(lgx_gemm_args), sizeof(lgx_copy2d_job): lets bindings
- * verify layout */
-void lgx_struct_sizes(int64_t out[10]);
+ * sizeof(lgx_ppo_store_args), sizeof(lgx_gemm_args), sizeof(lgx_copy2d_job),
+ * sizeof(lgx_gemm_tn_args): lets bindings verify layout */
+void lgx_struct_sizes(int64_t out[11]);
 
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
@@ -475,6 +475,25 @@ typedef struct lgx_gemm_args {
 int64_t lgx_gemm_partials_floats(int64_t M, int32_t N, int32_t batch);
 int lgx_gemm_nt(const lgx_gemm_args* args, void* stream);
 
+
+/* Weight-gradient GEMM of the PPO update (the dW_k = dZ_k^T Y_{k-1} products of rsl_rl's
+ * backward, legged_robot_config.py:226-239), split-K over row slices, split-bf16 products
+ * (f32-accurate, as LGX_GEMM_ALGO_SPLIT_BF16):
+ *   C[((z * slices + s) * R + n) * ldc + c] = sum_{m = s Ms}^{(s+1) Ms - 1} A[z*sa + m*lda + n] * B[z*sb + m*ldb + c]
+ * for z < batch, s < slices, n < R, c < Cc, Ms = M / slices.  Requirements: Ms % 32 == 0,
+ * R % 128 == 0, ldb >= Cc rounded up to 128 (the padding columns are read, not stored), A/B
+ * 16-byte aligned with lda, ldb, sa, sb % 4 == 0.  lgx_reduce_slices then sums the slices. */
+typedef struct lgx_gemm_tn_args {
+  int64_t M;                    /* rows per batch entry */
+  int32_t R, Cc, slices, batch;
+  const float* A;
+  int64_t lda, sa;
+  const float* B;
+  int64_t ldb, sb;
+  float* C;
+  int64_t ldc;
+} lgx_gemm_tn_args;
+int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream);
 
 /* weight preparation for lgx_gemm_nt: dst[b][r][c] = src[b][r][c] (transpose 0) or
  * dst[b][c][r] = src[b][r][c] (transpose 1), r < rows, c < cols; dst padding is untouched */

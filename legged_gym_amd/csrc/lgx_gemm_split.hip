@@ -411,7 +411,10 @@ int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream_) {
     const char* e = getenv("LGX_GEMM_X3P");
     return !(e && e[0] == '0');
   }();
-  if (a.Bs && a.K % BK == 0 && pipelined) return lgx_gemm_nt_x3p(a, cus, stream_);
+
+  // the pipelined kernel for the bias + ELU / plain epilogues; the column-sum epilogue runs here
+  // (its x3p form, without deferral, measured equal or slower: dA3 48 vs 43 us)
+  if (a.Bs && a.K % BK == 0 && pipelined && a.epi != LGX_GEMM_DELU_COLSUM) return lgx_gemm_nt_x3p(a, cus, stream_);
   const hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
              a.partials, 0, a.Bs};

@@ -1,0 +1,248 @@
+// Weight-gradient GEMM of the PPO update (rsl_rl PPO.update backward, legged_robot_config.py:226-239),
+// split-K over row slices:
+//   C[z][s][n][c] = sum_{m in slice s} A[z][m][n] * B[z][m][c],   slice s = rows [s Ms, (s+1) Ms)
+// i.e. dW_k = dZ_k^T Y_{k-1} per network z (actor, critic) and row slice s; lgx_reduce_slices sums
+// the slices into the flat gradient.  Replaces the library f32 bmm over slices.
+//
+// Same f32-accurate arithmetic as the split-bf16 path of lgx_gemm_nt (lgx_gemm_split.hip): both
+// operands split into three RNE bf16 limbs, six limb products on v_mfma_f32_32x32x16_bf16.
+// Both operands are row-major in m (the reduction index), so the MFMA fragments (8 consecutive m
+// of one column per lane) are column reads of the staged tiles:
+//   * each 32-row stage of A (128 columns n) and B (128 columns c) is loaded as f32 (16-byte row
+//     segments, coalesced), split in registers and written as limb images [limb][32 m][128 cols]
+//     bf16 (8-byte stores of 4 columns; the 8-byte unit u of row m sits at u ^ 8 (m & 3));
+//   * fragments come back with ds_read_b64_tr_b16 (the gfx950 transposing LDS read): a 16-lane
+//     group reads a 4 m x 16 column block and lane i receives column i's four m values; two reads
+//     give the 8 m of a 32x32x16 operand.  The XOR makes both the stores and the transposed reads
+//     bank-conflict free;
+//   * 128 x 128 output tile per workgroup, 4 waves (one per SIMD) of 64 x 64; register-staged
+//     prefetch of stage t+2 while stage t computes, two LDS buffers, one barrier per stage;
+//     persistent workgroups over XCD-contiguous tile ranges (column tiles of one (n, s, z) adjacent:
+//     the A rows stay in that XCD's L2).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "lgx_internal.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float fx2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int TT = 128;                   // output tile (n and c)
+constexpr int TK = 32;                    // rows m per stage
+constexpr int TW = 4;                     // waves (2 x 2 of 64 x 64)
+constexpr int IMG = 3 * TK * TT * 2;      // one operand's limb image per stage: 24 KB
+constexpr int STAGE = 2 * IMG;            // A and B
+constexpr int TN_LDS = 2 * STAGE;         // two buffers: 96 KB
+
+struct TnArgs {
+  int64_t Ms;            // rows per slice (% 32 == 0)
+  int32_t R, Cc, S, batch;
+  const float* A;
+  int64_t lda, sa;
+  const float* B;
+  int64_t ldb, sb;
+  float* C;
+  int64_t ldc;
+  int32_t rt, ct, tiles;
+};
+
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
+  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){x0, x1}, bf16x2));
+  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
+  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+  r0 -= __uint_as_float(l1 << 16);
+  r1 -= __uint_as_float(l1 & 0xffff0000u);
+  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+}
+
+// staged registers of one stage: 4 rows x 4 columns of A and of B per thread
+struct TnStage {
+  float4 a[4], b[4];
+};
+
+// thread t: column quad cq = t % 32 (columns 4cq .. 4cq+3), rows 4 mq .. 4 mq + 3 (mq = t / 32)
+__device__ __forceinline__ void tn_load(TnStage& st, const char* __restrict__ Ab, const char* __restrict__ Bb,
+                                        uint32_t oa, uint32_t ob, uint32_t sta, uint32_t stb) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    st.a[i] = *reinterpret_cast<const float4*>(Ab + oa + i * sta);
+    st.b[i] = *reinterpret_cast<const float4*>(Bb + ob + i * stb);
+  }
+}
+
+__device__ __forceinline__ void tn_store_img(char* img, const float4 (&v)[4], int cq, int mq) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint2 l0, l1, l2;
+    split2(v[i].x, v[i].y, l0.x, l1.x, l2.x);
+    split2(v[i].z, v[i].w, l0.y, l1.y, l2.y);
+    const int m = 4 * mq + i;
+    char* row = img + m * (TT * 2) + ((cq ^ (8 * i)) << 3);   // unit cq at cq ^ 8 (m & 3)
+    *reinterpret_cast<uint2*>(row) = l0;
+    *reinterpret_cast<uint2*>(row + TK * TT * 2) = l1;
+    *reinterpret_cast<uint2*>(row + 2 * TK * TT * 2) = l2;
+  }
+}
+
+__device__ __forceinline__ s16x4 tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// fragment of 32 columns (column block a) for 16-k half s: limb l = two transposed reads
+// (m = 16s + 8h + 0..3 and + 4..7)
+__device__ __forceinline__ bf16x8 tn_frag(const char* img, int l, int s, int lane_off, int xa) {
+  const char* p = img + l * (TK * TT * 2) + s * (16 * TT * 2) + lane_off + xa;
+  const s16x4 lo = tr_read(p), hi = tr_read(p + 4 * TT * 2);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+__global__ void __launch_bounds__(64 * TW, 1) gemm_tn_x3_kernel(TnArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char tlds[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int cq = tid & 31, mq = tid >> 5;
+  // transposed-read lane offset: row 8h + q (+ 4 e), 8-byte unit 8 (a ^ q) + 4 gb + p
+  const int q = (lane >> 2) & 3, p = lane & 3, gb = (lane >> 4) & 1;
+  const int lane_off = (8 * h + q) * (TT * 2) + (4 * gb + p) * 8;
+  int xa[2], xb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    xa[i] = 64 * ((2 * wm + i) ^ q);
+    xb[i] = 64 * ((2 * wn + i) ^ q);
+  }
+  const int xcd = blockIdx.x & 7;
+  const int32_t stride = gridDim.x >> 3;
+  const int32_t lo = (int32_t)((int64_t)xcd * g.tiles / 8), hi = (int32_t)((int64_t)(xcd + 1) * g.tiles / 8);
+  const int nst = (int)(g.Ms / TK);
+  const uint32_t sta = (uint32_t)(g.lda * 4), stb = (uint32_t)(g.ldb * 4);
+  for (int32_t tile = lo + (blockIdx.x >> 3); tile < hi; tile += stride) {
+    int32_t t = tile;
+    const int ctile = t % g.ct;
+    t /= g.ct;
+    const int ntile = t % g.rt;
+    t /= g.rt;
+    const int s = t % g.S;
+    const int z = t / g.S;
+    const int64_t m0 = (int64_t)s * g.Ms;
+    const char* Ab = reinterpret_cast<const char*>(g.A + z * g.sa + m0 * g.lda + ntile * TT);
+    const char* Bb = reinterpret_cast<const char*>(g.B + z * g.sb + m0 * g.ldb + ctile * TT);
+    const uint32_t oa = (4 * mq) * sta + cq * 16, ob = (4 * mq) * stb + cq * 16;
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    TnStage st;
+    tn_load(st, Ab, Bb, oa, ob, sta, stb);
+    __syncthreads();   // (previous tile's last reads of buffer 0 are done)
+    tn_store_img(tlds, st.a, cq, mq);
+    tn_store_img(tlds + IMG, st.b, cq, mq);
+    if (nst > 1) tn_load(st, Ab, Bb, oa + TK * sta, ob + TK * stb, sta, stb);
+    __syncthreads();
+    for (int k = 0; k < nst; ++k) {
+      const char* ia = tlds + (k & 1) * STAGE;
+      const char* ib = ia + IMG;
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int l = 0; l < 3; ++l) {
+            fa[i][l] = tn_frag(ia, l, hs, lane_off, xa[i]);
+            fb[i][l] = tn_frag(ib, l, hs, lane_off, xb[i]);
+          }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            f32x16 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+            acc[i][j] = c;
+          }
+      }
+      if (k + 1 < nst) {   // buffer (k+1)&1 was last read at stage k-1, before the last barrier
+        char* nb = tlds + ((k + 1) & 1) * STAGE;
+        tn_store_img(nb, st.a, cq, mq);
+        tn_store_img(nb + IMG, st.b, cq, mq);
+        if (k + 2 < nst) tn_load(st, Ab, Bb, oa + (k + 2) * TK * sta, ob + (k + 2) * TK * stb, sta, stb);
+      }
+      __syncthreads();
+    }
+    // acc[i][j][e] = C[n0 + 32i + 8(e >> 2) + 4h + (e & 3)][c0 + 32j + r]: 32 lanes store one
+    // 128-byte row segment per element
+    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * TT + wm * 64) * g.ldc;
+    const int c0 = ctile * TT + wn * 64 + r;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c0 + 32 * j;
+      if (c >= g.Cc) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+          Cb[(int64_t)n * g.ldc + c] = acc[i][j][e];
+        }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
+  if (!args) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: null args");
+  const lgx_gemm_tn_args& a = *args;
+  if (!a.A || !a.B || !a.C || a.M <= 0 || a.slices <= 0 || a.M % a.slices || (a.M / a.slices) % TK || a.R <= 0 ||
+      a.R % TT || a.Cc <= 0 || a.batch <= 0 || a.lda < a.R || a.ldb < (a.Cc + TT - 1) / TT * TT || a.ldc < a.Cc ||
+      a.lda % 4 || a.ldb % 4 || a.sa % 4 || a.sb % 4 || ((uintptr_t)a.A & 15) || ((uintptr_t)a.B & 15))
+    return lgx_fail(LGX_EINVAL,
+                    "lgx_gemm_tn: bad args (M / slices % 32, R % 128, ldb >= Cc rounded up to 128, 16-byte aligned "
+                    "A/B rows)");
+  if ((a.M / a.slices + TK) * std::max(a.lda, a.ldb) * 4 >= (1ll << 32))
+    return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: row slice too large for 32-bit offsets");
+  TnArgs g;
+  g.Ms = a.M / a.slices;
+  g.R = a.R;
+  g.Cc = a.Cc;
+  g.S = a.slices;
+  g.batch = a.batch;
+  g.A = a.A;
+  g.lda = a.lda;
+  g.sa = a.sa;
+  g.B = a.B;
+  g.ldb = a.ldb;
+  g.sb = a.sb;
+  g.C = a.C;
+  g.ldc = a.ldc;
+  g.rt = a.R / TT;
+  g.ct = (a.Cc + TT - 1) / TT;
+  const int64_t tiles = (int64_t)g.rt * g.ct * a.slices * a.batch;
+  if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: too many tiles");
+  g.tiles = (int32_t)tiles;
+  static const bool attrs =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x3_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TN_LDS) == hipSuccess;
+  if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t per_xcd = (tiles + 7) / 8;
+  const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
+  LGX_LAUNCH(gemm_tn_x3_kernel, dim3((unsigned)wgs), dim3(64 * TW), TN_LDS, reinterpret_cast<hipStream_t>(stream), g);
+  return lgx_hip_status("lgx_gemm_tn");
+}

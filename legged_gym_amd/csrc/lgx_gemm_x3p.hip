@@ -26,8 +26,7 @@
 //   * A is split into its limbs after the fragment read (8 floats per lane per 16 k: 12
 //     v_cvt_pk_bf16_f32 + exact f32 subtractions);
 //   * epilogues: bias + ELU / plain deferred into the next tile's slots (16-byte row stores of the
-//     transposed accumulators, a few per slot, under the MFMAs); ELU' + per-128-row column-sum
-//     partials at the tile's end (fixed summation order: bitwise reproducible).
+//     transposed accumulators, a few per slot, under the MFMAs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -48,9 +47,8 @@ constexpr int A_ST = PM * PK * 4;            // 32 KB: f32 A stage (256 rows x 1
 constexpr int B_ST = 3 * PN * PK * 2;        // 24 KB: limb B stage ([limb][128 n][64 B])
 constexpr int NSA = 3, NSB = 2;              // ring depths
 constexpr int OFF_B = NSA * A_ST;
-constexpr int OFF_RED = OFF_B + NSB * B_ST;     // [4 wave rows][128] column partials
-constexpr int OFF_BIAS = OFF_RED + 4 * PN * 4;  // 3 x 1 KB: bias of the pending / current / next tile
-constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 152,576 B
+constexpr int OFF_BIAS = OFF_B + NSB * B_ST;   // 3 x 1 KB: bias of the pending / current / next tile
+constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 150,528 B
 constexpr int B_BLK = 3 * 128 * 32;             // bf16 per pre-split (128 n x 32 k) block
 
 template <int NWV>
@@ -282,82 +280,6 @@ __device__ __forceinline__ float4 q4(const f32x16v& v, int q) {
   return make_float4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
 }
 
-// acc[i][j][4q + e] = C[m0 + 32i + r][n0 + 32j + 8q + 4h + e]: the ELU' + column-sum epilogue at
-// the tile's end (Y rows past M are read from row M-1 and discarded).
-template <int NWV>
-__device__ __forceinline__ void p_epilogue_delu(const PArgs& g, const f32x16v (&acc)[2][XC<NWV>::WJ], const PTile& T,
-                                                int wm, int wn, int r, int h, float* red) {
-  constexpr int WJ = XC<NWV>::WJ;
-  const int64_t m0 = (int64_t)T.mt * PM + wm * 64;
-  const int n0 = T.nt * PN + wn * 32 * WJ;
-  const int64_t ldc = g.ldc;
-  float* C = g.C + T.z * g.sc + n0 + 4 * h;
-  const float* Y = g.Y + T.z * g.sc + n0 + 4 * h;
-  float4 cs[WJ][4];
-#pragma unroll
-  for (int j = 0; j < WJ; ++j)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) cs[j][q] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const bool ok = m0 + 32 * i + r < g.M;
-    const int64_t ro = min(m0 + 32 * i + r, g.M - 1) * ldc;
-#pragma unroll
-    for (int j = 0; j < WJ; ++j) {
-      float4 y[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) y[q] = *reinterpret_cast<const float4*>(Y + ro + 32 * j + 8 * q);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float4 d = q4(acc[i][j], q);
-        d.x *= elu_grad_from_out(y[q].x);
-        d.y *= elu_grad_from_out(y[q].y);
-        d.z *= elu_grad_from_out(y[q].z);
-        d.w *= elu_grad_from_out(y[q].w);
-        if (ok) {
-          *reinterpret_cast<float4*>(C + ro + 32 * j + 8 * q) = d;
-          cs[j][q].x += d.x;
-          cs[j][q].y += d.y;
-          cs[j][q].z += d.z;
-          cs[j][q].w += d.w;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int sh = 1; sh < 32; sh <<= 1)
-#pragma unroll
-    for (int j = 0; j < WJ; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        cs[j][q].x += __shfl_xor(cs[j][q].x, sh);
-        cs[j][q].y += __shfl_xor(cs[j][q].y, sh);
-        cs[j][q].z += __shfl_xor(cs[j][q].z, sh);
-        cs[j][q].w += __shfl_xor(cs[j][q].w, sh);
-      }
-  const int cl = wn * 32 * WJ + 4 * h;
-  if (r == 0) {
-#pragma unroll
-    for (int j = 0; j < WJ; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(red + wm * PN + cl + 32 * j + 8 * q) = cs[j][q];
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  p_barrier();
-  // partial row t = 128-row chunk: wave rows (0, 1) -> 2 mt, (2, 3) -> 2 mt + 1, summed in order
-  if ((wm & 1) == 0 && h == 0) {
-    const int64_t t = 2 * (int64_t)T.mt + (wm >> 1);
-    if (t * 128 < g.M) {
-      float* P = g.partials + t * ((int64_t)g.batch * g.N) + (int64_t)T.z * g.N + T.nt * PN;
-#pragma unroll
-      for (int j = 0; j < WJ; ++j) {
-        const int col = wn * 32 * WJ + 32 * j + r;
-        P[col] = red[wm * PN + col] + red[(wm + 1) * PN + col];
-      }
-    }
-  }
-}
-
 // Bias + ELU (or plain) output of float4 run gi = (i, j, q), gi = 4 (WJ i + j) + q, of a lane.
 template <int EPI, int NWV>
 __device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pend)[2][XC<NWV>::WJ], const PTile& T,
@@ -392,15 +314,18 @@ __device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pe
 //
 // KBT > 0: K = 32 KBT known at compile time, the k loop unrolled and the BIAS_ELU / PLAIN
 // epilogue deferred into the next tile's slots (GROUPS / KBT store runs per slot: constant
-// register indices).  KBT == 0, or the column-sum epilogue: the epilogue runs at the tile's end
-// (after waiting for the next slot's stages, so its stores do not sit in front of them).
+// register indices).  KBT == 0: the epilogue runs at the tile's end (after waiting for the next
+// slot's stages, so its stores do not sit in front of them).  (ELU' + column sums: the
+// register-staged gemm_nt_x3_kernel, measured equal or faster for the dA shapes.)
 template <int EPI, int KBT, int NWV>
 __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   using X = XC<NWV>;
   constexpr int WJ = X::WJ, AG = X::A_GL;
   extern __shared__ __attribute__((aligned(16))) char plds[];
-  constexpr bool DEFER = KBT > 0 && EPI != LGX_GEMM_DELU_COLSUM;
+  static_assert(EPI != LGX_GEMM_DELU_COLSUM, "the column-sum epilogue runs on gemm_nt_x3_kernel");
+  constexpr bool DEFER = KBT > 0;
   constexpr int GPS = DEFER ? X::GROUPS / KBT : 0;     // deferred store runs per slot
+  constexpr int UNR = KBT > 0 ? KBT : 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int wm = wave / X::WGN, wn = wave % X::WGN;
@@ -462,7 +387,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   bool stores = false;         // (DEFER) GPS deferred stores issued in the previous iteration
   for (int32_t tj = 0; tj < ntiles; ++tj) {
     const PTile T = ptile(g, t0 + tj * stride);
-#pragma unroll(KBT > 0 ? KBT : 1)
+#pragma unroll UNR
     for (int k = 0; k < kb; ++k, ++q) {
       X3P_STAMP(0);
       if (!waited) {
@@ -545,14 +470,10 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       else wait_vm<0>();
       waited = true;
 #ifndef X3P_NO_EPI
-      if constexpr (EPI == LGX_GEMM_DELU_COLSUM) {
-        p_epilogue_delu<NWV>(g, acc, T, wm, wn, r, h, reinterpret_cast<float*>(plds + OFF_RED));
-      } else {
 #pragma unroll
-        for (int gi = 0; gi < X::GROUPS; ++gi)
-          p_store_group<EPI, NWV>(g, acc, T, wm, wn, r, h,
-                                  reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
-      }
+      for (int gi = 0; gi < X::GROUPS; ++gi)
+        p_store_group<EPI, NWV>(g, acc, T, wm, wn, r, h,
+                                reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
 #else
       if (acc[0][0][0] == 1234.5f) g.C[tid] = acc[1][1][3] + acc[0][1][2] + acc[1][0][1];
 #endif
@@ -578,15 +499,14 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 
 typedef void (*x3p_fn)(PArgs);
 
-// [epilogue][KBT index: 0 (runtime K), 4, 8, 16]
+// [epilogue (PLAIN, BIAS_ELU)][KBT index: 0 (runtime K), 4, 8, 16]
 template <int NWV>
 struct X3PTable {
-  static constexpr x3p_fn k[3][4] = {
+  static constexpr x3p_fn k[2][4] = {
       {&gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 0, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 4, NWV>,
        &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 16, NWV>},
       {&gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 0, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 4, NWV>,
-       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV>},
-      {&gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 0, NWV>, nullptr, nullptr, nullptr}};
+       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV>}};
 };
 
 template <int NWV>
@@ -641,7 +561,8 @@ int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
   }();
   static const bool attrs = x3p_attrs<4>() && x3p_attrs<8>();
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_nt: hipFuncSetAttribute (dynamic LDS) failed");
-  const int kbt = (defer && a.epi != LGX_GEMM_DELU_COLSUM && (g.kb == 4 || g.kb == 8 || g.kb == 16)) ? g.kb : 0;
+  if (a.epi == LGX_GEMM_DELU_COLSUM) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt_x3p: no column-sum epilogue");
+  const int kbt = (defer && (g.kb == 4 || g.kb == 8 || g.kb == 16)) ? g.kb : 0;
   const int ki = kbt == 0 ? 0 : kbt == 4 ? 1 : kbt == 8 ? 2 : 3;
   const x3p_fn f = nwv == 8 ? X3PTable<8>::k[a.epi][ki] : X3PTable<4>::k[a.epi][ki];
   // persistent: one workgroup per CU, a multiple of 8 (XCD tile ranges)

@@ -225,6 +225,10 @@ class FusedPPOUpdate:
         # LGX_GEMM_ALGO: "split" (default) = lgx_gemm_nt's split-bf16 products (f32-accurate, bf16
         # MFMA) with pre-split weights; "f32" = the exact-f32 MFMA path with f32 weight copies
         self.split = os.environ.get("LGX_GEMM_ALGO", "split") != "f32"
+        # LGX_PPO_DW: "lgx" (default with split-bf16 GEMMs) = weight gradients on lgx_gemm_tn
+        # (split-bf16, transposed LDS reads); "lib" = library f32 bmm over row slices
+        self.tn = self.lgx_gemm and self.split and os.environ.get("LGX_PPO_DW", "lgx") != "lib"
+        self.gemm_dw = {}   # layer -> lgx_gemm_tn argument blocks (filled by _build_gemm_plan)
         self.norm_parts = torch.zeros(256, device=self.dev)
         self._mirrors_valid = False
         self.stats = torch.zeros(3, device=self.dev)
@@ -242,7 +246,8 @@ class FusedPPOUpdate:
         want = [int(x) for x in env.split(",")] if env else []
         self.Sk = []
         for k in range(self.L):
-            sk = want[k] if k < len(want) else self.SPLITS
+            sk = want[k] if k < len(want) else (self._tn_slices(h[k], h[k - 1] if k else self.num_obs, M)
+                                                if self.tn else self.SPLITS)
             self.Sk.append(sk if sk > 0 and M % sk == 0 else 1)
         self.S = self.Sk[0]
         sep = self._separate_critic_obs()
@@ -279,6 +284,18 @@ class FusedPPOUpdate:
             self.col_parts = [torch.empty(int(self.lib.lgx_colsum_partials_floats(M, hk, 2)), device=dev)
                               for hk in h[:-1]]
         self._build_reduce_jobs()
+
+    @staticmethod
+    def _tn_slices(R, Cc, M, cus=256):
+        """Row slices of one lgx_gemm_tn launch: the fewest (>= 8, powers of 2) that give every CU
+        an output tile (R/128 x ceil(Cc/128) tiles per slice and network) with 32-row multiples."""
+        tiles = (R // 128) * (-(-Cc // 128)) * 2
+        s = 8
+        while tiles * s < cus and M % (2 * s * 32) == 0:
+            s *= 2
+        while s > 1 and M % (s * 32):   # small minibatches: fewer slices of 32-row multiples
+            s //= 2
+        return s
 
     def _build_gemm_plan(self):
         """Fixed argument blocks of every lgx_gemm_nt / lgx_copy2d launch of a minibatch (the
@@ -381,6 +398,36 @@ class FusedPPOUpdate:
                           h[k - 1] * h[k], self.D[k - 1], h[k - 1], h[k], 2, abi.GEMM_DELU_COLSUM, Y=self.Y[k - 1],
                           parts=self.col_parts[k - 1], Bs=nlt[k])
         self.gemm_bwd = bwd
+        # weight gradients (lgx_gemm_tn): dW_k = dZ_k^T Y_{k-1} over Sk row slices into P[k]
+        self.gemm_dw = {}
+        if self.tn:
+            def tn(A, lda, sa, B, ldb, sb, Cp, R, Cc, S, batch):
+                t = abi.LgxGemmTnArgs()
+                t.M, t.R, t.Cc, t.slices, t.batch = M, R, Cc, S, batch
+                t.A, t.lda, t.sa = A, lda, sa
+                t.B, t.ldb, t.sb = B, ldb, sb
+                t.C, t.ldc = Cp, Cc
+                return t
+            tn_ok = [M % (self.Sk[k] * 32) == 0 for k in range(L)]   # else the library bmm (rows % 32)
+            for k in range(L - 1, 0, -1):
+                if not tn_ok[k]:
+                    continue
+                dz = self.Y[L - 1] if k == L - 1 else self.D[k]
+                self.gemm_dw[k] = [tn(dz.data_ptr(), h[k], M * h[k], self.Y[k - 1].data_ptr(), h[k - 1], M * h[k - 1],
+                                      self.P[k].data_ptr(), h[k], h[k - 1], self.Sk[k], 2)]
+            # layer 1: B = the minibatch's padded input rows (pointer set per minibatch); the padding
+            # columns up to the next multiple of 128 must exist in the rows
+            if tn_ok[0] and self.Kp >= -(-self.num_obs // 128) * 128 and (
+                    self.Xcp is None or self.Kcp >= -(-self.num_cobs // 128) * 128):
+                d0 = self.D[0]
+                if isinstance(self.P[0], tuple):     # privileged critic inputs: one launch per network
+                    self.gemm_dw[0] = [tn(d0[0].data_ptr(), h[0], 0, 0, self.Kp, 0, self.P[0][0].data_ptr(), h[0],
+                                          self.num_obs, self.Sk[0], 1),
+                                       tn(d0[1].data_ptr(), h[0], 0, 0, self.Kcp, 0, self.P[0][1].data_ptr(), h[0],
+                                          self.num_cobs, self.Sk[0], 1)]
+                else:                                # one input for both networks: batch stride 0
+                    self.gemm_dw[0] = [tn(d0.data_ptr(), h[0], M * h[0], 0, self.Kp, 0, self.P[0].data_ptr(), h[0],
+                                          self.num_obs, self.Sk[0], 2)]
 
     def _separate_critic_obs(self):
         st = self.ppo.storage
@@ -473,7 +520,7 @@ class FusedPPOUpdate:
     def _gather_all(self, indices, obs, cobs, rows, stream):
         # one input for both networks: rows gathered twice per minibatch ([nmb, 2, M, Kp]) so the
         # layer-1 weight gradients of actor and critic are ONE batched split-K GEMM
-        self.dw1_batched = (cobs is None and self.num_obs == self.num_cobs and self.Xcp is None
+        self.dw1_batched = (cobs is None and self.num_obs == self.num_cobs and self.Xcp is None and 0 not in self.gemm_dw
                             and os.environ.get("LGX_PPO_DW1_BATCHED", "1") != "0")
         if self.dw1_batched:
             M = self.M
@@ -657,8 +704,12 @@ class FusedPPOUpdate:
         for k in range(L - 1, 0, -1):
             # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
             Sl = self.Sk[k]
-            torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2), self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]),
-                      out=self.P[k])
+            if k in self.gemm_dw:
+                for t in self.gemm_dw[k]:
+                    chk(lib.lgx_gemm_tn(C.byref(t), stream), "gemm_tn")
+            else:
+                torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2),
+                          self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]), out=self.P[k])
             if fused:
                 self._gemm(self.gemm_bwd[k], stream)
             else:
@@ -666,7 +717,14 @@ class FusedPPOUpdate:
                 chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
                                            _vp(self.col_parts[k - 1]), stream), "elu_bwd")
             dZ = self.D[k - 1]
-        if xs is not None and len(xs) > 2:    # one batched GEMM: 2 networks x S row slices
+        if 0 in self.gemm_dw and fused:     # lgx_gemm_tn over the minibatch's padded input rows
+            t = self.gemm_dw[0]
+            t[0].B = xp.data_ptr()
+            if len(t) > 1:
+                t[1].B = (xcp if xcp is not None else xp).data_ptr()
+            for tk in t:
+                chk(lib.lgx_gemm_tn(C.byref(tk), stream), "gemm_tn")
+        elif xs is not None and len(xs) > 2:    # one batched GEMM: 2 networks x S row slices
             x2 = xs[2].view(2 * S, M // S, self.Kp)[:, :, :self.num_obs]
             torch.bmm(dZ.view(2 * S, M // S, h[0]).transpose(1, 2), x2, out=self.P[0].view(2 * S, h[0], self.num_obs))
         else:

@@ -132,6 +132,12 @@ class LgxGemmArgs(C.Structure):
                 ("partials", C.c_void_p), ("algo", i32), ("reserved", i32), ("Bs", C.c_void_p)]
 
 
+class LgxGemmTnArgs(C.Structure):
+    _fields_ = [("M", i64), ("R", i32), ("Cc", i32), ("slices", i32), ("batch", i32),
+                ("A", C.c_void_p), ("lda", i64), ("sa", i64), ("B", C.c_void_p), ("ldb", i64), ("sb", i64),
+                ("C", C.c_void_p), ("ldc", i64)]
+
+
 class LgxCopy2dJob(C.Structure):
     _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("src_ld", i64), ("src_bs", i64), ("dst_ld", i64),
                 ("dst_bs", i64), ("rows", i32), ("cols", i32), ("batch", i32), ("transpose", i32)]
@@ -189,6 +195,7 @@ def declare(lib, prefix="lgx"):
             "reduce_slices": (C.c_int, [C.POINTER(LgxReduceJob), i32, vp]),
             "gemm_partials_floats": (i64, [i64, i32, i32]),
             "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
+            "gemm_tn": (C.c_int, [C.POINTER(LgxGemmTnArgs), vp]),
             "copy2d": (C.c_int, [C.POINTER(LgxCopy2dJob), i32, vp]),
             "split_bf16_elems": (i64, [i32, i32]),
             "split_bf16": (C.c_int, [C.POINTER(LgxCopy2dJob), i32, vp]),
@@ -214,16 +221,16 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
             "lgx_reduce_slices", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
-            "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16"]
+            "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn"]
 
 
-def check_layout(sizes_fn, n=10):
+def check_layout(sizes_fn, n=11):
     """Compare the library's sizeof() of every ABI struct with these mirrors (the oracle
     reports the first 3)."""
     out = (C.c_int64 * 16)()
     sizes_fn(out)
     mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers), C.sizeof(LgxMlpDesc),
             C.sizeof(LgxPpoLossArgs), C.sizeof(LgxReduceJob), C.sizeof(LgxPpoActArgs),
-            C.sizeof(LgxPpoStoreArgs), C.sizeof(LgxGemmArgs), C.sizeof(LgxCopy2dJob))[:n]
+            C.sizeof(LgxPpoStoreArgs), C.sizeof(LgxGemmArgs), C.sizeof(LgxCopy2dJob), C.sizeof(LgxGemmTnArgs))[:n]
     if tuple(out)[:n] != mine:
         raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)[:n]} vs bindings {mine}")

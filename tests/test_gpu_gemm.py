@@ -224,6 +224,49 @@ def test_split_bf16_is_f32_accurate(gpu, spread):
     assert bool((esp <= K * 2.0 ** -24 * scale).all())
 
 
+def _run_tn(M, S, R, Cc, batch, ldb=None, seed=0):
+    """lgx_gemm_tn against float64: C[z][s] = A[z, slice s]^T B[z, slice s, :Cc]."""
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(seed)
+    ldb = ldb or Cc
+    A = torch.randn(batch, M, R, device=dev, generator=g)
+    B = torch.randn(batch, M, ldb, device=dev, generator=g)
+    Cout = torch.full((batch, S, R, Cc), float("nan"), device=dev)
+    a = abi.LgxGemmTnArgs()
+    a.M, a.R, a.Cc, a.slices, a.batch = M, R, Cc, S, batch
+    a.A, a.lda, a.sa = A.data_ptr(), R, M * R
+    a.B, a.ldb, a.sb = B.data_ptr(), ldb, M * ldb
+    a.C, a.ldc = Cout.data_ptr(), Cc
+    lgxlib.check(_lib().lgx_gemm_tn(C.byref(a), _stream()), "lgx_gemm_tn")
+    torch.cuda.synchronize()
+    Ms = M // S
+    ref = torch.einsum("zsmn,zsmc->zsnc", A.double().view(batch, S, Ms, R), B[..., :Cc].double().view(batch, S, Ms, Cc))
+    tol = 2e-5 * Ms ** 0.5 * ref.abs().max().item() + 1e-6
+    err = (Cout.double() - ref).abs().max().item()
+    assert err <= tol, f"M={M} S={S} R={R} Cc={Cc}: max err {err:.3e} > {tol:.3e}"
+
+
+@pytest.mark.parametrize("M,S,R,Cc,ldb", [(1024, 2, 128, 128, None), (2048, 4, 256, 235, 256), (96, 3, 128, 384, None),
+                                          (24576, 16, 256, 512, None), (24576, 8, 512, 235, 256),
+                                          (24576, 32, 128, 256, None)])
+def test_gemm_tn_weight_gradients(gpu, M, S, R, Cc, ldb):
+    """lgx_gemm_tn (dW = dZ^T Y over row slices, split-bf16 products, transposed LDS reads):
+    small and update-sized shapes, ragged output columns (235 = num_obs, padded input rows),
+    one stage per slice (96 / 3 = 32 rows), several column tiles."""
+    _run_tn(M, S, R, Cc, 2, ldb=ldb, seed=M + S)
+
+
+def test_gemm_tn_rejects_bad_shapes(gpu):
+    a = abi.LgxGemmTnArgs()
+    x = torch.zeros(4096, device="cuda:0")
+    a.M, a.R, a.Cc, a.slices, a.batch = 100, 128, 128, 1, 1      # slice rows % 32 != 0
+    a.A = a.B = a.C = x.data_ptr()
+    a.lda = a.ldb = a.ldc = 128
+    assert _lib().lgx_gemm_tn(C.byref(a), _stream()) != 0
+    a.M, a.R = 128, 100                                            # R % 128 != 0
+    assert _lib().lgx_gemm_tn(C.byref(a), _stream()) != 0
+
+
 def test_gemm_rejects_bad_shapes(gpu):
     a = abi.LgxGemmArgs()
     x = torch.zeros(64, 64, device="cuda:0")

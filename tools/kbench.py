@@ -187,6 +187,32 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
             print(f"  torch bmm (no epilogue) {t2*1e3:.1f} us {f/t2/1e9:.1f} TF/s", flush=True)
 
 
+def tn_bench(M=24576, iters=20):
+    """lgx_gemm_tn (dW GEMMs) at the PPO-update shapes vs torch bmm over row slices."""
+    import ctypes as C
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim import lib as lgxlib
+    dev = "cuda:0"
+    lib = lgxlib.load()
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for (R, Cc, ldb) in ((512, 235, 256), (256, 512, 512), (128, 256, 256)):
+        A = torch.randn(2, M, R, device=dev)
+        B = torch.randn(2, M, ldb, device=dev)
+        f = 2.0 * 2 * M * R * Cc
+        for S in [int(x) for x in os.environ.get("KB_SLICES", "8,16,32").split(",")]:
+            Cout = torch.empty(2, S, R, Cc, device=dev)
+            a = abi.LgxGemmTnArgs()
+            a.M, a.R, a.Cc, a.slices, a.batch = M, R, Cc, S, 2
+            a.A, a.lda, a.sa, a.B, a.ldb, a.sb = A.data_ptr(), R, M * R, B.data_ptr(), ldb, M * ldb
+            a.C, a.ldc = Cout.data_ptr(), Cc
+            t1 = timeit(lambda: lgxlib.check(lib.lgx_gemm_tn(C.byref(a), stream), "tn"), iters=iters)
+            P = torch.empty(2 * S, R, Cc, device=dev)
+            Bv = B[..., :Cc].reshape(2 * S, M // S, Cc) if ldb == Cc else B.view(2 * S, M // S, ldb)[..., :Cc]
+            t2 = timeit(lambda: torch.bmm(A.view(2 * S, M // S, R).transpose(1, 2), Bv, out=P), iters=iters)
+            print(f"gemm_tn R={R} Cc={Cc} S={S}: lgx {t1*1e3:.1f} us {f/t1/1e9:.1f} TF/s; torch bmm {t2*1e3:.1f} us "
+                  f"{f/t2/1e9:.1f} TF/s", flush=True)
+
+
 def phys_run(task="go1_rough", n=4096, steps=10):
     """Short env-step loop for PMC collection (rocprofv3 --pmc): 10 env steps after reset."""
     from oracle_backend import make_env
@@ -217,5 +243,7 @@ if __name__ == "__main__":
             ppo_ab(modes=(m,), gemms=False)
     if "gemm" in what:
         gemm_bench(torch_too="torch" in what)
+    if "tn" in what:
+        tn_bench()
 
 
