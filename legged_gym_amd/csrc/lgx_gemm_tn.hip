@@ -16,11 +16,14 @@
 //     give the 8 m of a 32x32x16 operand.  The XOR makes both the stores and the transposed reads
 //     bank-conflict free;
 //   * 128 x 128 output tile per workgroup, 4 waves (one per SIMD) of 64 x 64; register-staged
-//     prefetch of stage t+2 while stage t computes, two LDS buffers, one barrier per stage;
+//     prefetch of stage t+2 while stage t computes, two LDS buffers, one barrier per stage; the
+//     split / image writes of stage t+1 and the loads of stage t+2 are spread between stage t's
+//     MFMA blocks;
 //     persistent workgroups over XCD-contiguous tile ranges (column tiles of one (n, s, z) adjacent:
 //     the A rows stay in that XCD's L2).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <algorithm>
 
@@ -34,12 +37,26 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef float fx2 __attribute__((ext_vector_type(2)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int TT = 128;                   // output tile (n and c)
+constexpr int TT = 128;                   // output tile columns (c); rows (n): RA = 128 | 256
 constexpr int TK = 32;                    // rows m per stage
-constexpr int TW = 4;                     // waves (2 x 2 of 64 x 64)
-constexpr int IMG = 3 * TK * TT * 2;      // one operand's limb image per stage: 24 KB
-constexpr int STAGE = 2 * IMG;            // A and B
-constexpr int TN_LDS = 2 * STAGE;         // two buffers: 96 KB
+
+// NWV = 4: 128 x 128 tile, 2 x 2 waves (one per SIMD); NWV = 8: 256 x 128 tile, 4 x 2 waves (two
+// per SIMD: one wave's split VALU and LDS traffic overlap the other's MFMAs; half the staged B
+// bytes per MFMA)
+template <int NWV>
+struct TC {
+  static constexpr int RA = NWV == 8 ? 256 : 128;    // A image width (output rows n per tile)
+  static constexpr int PT = 64 * NWV;
+  static constexpr int IMGA = 3 * TK * RA * 2;       // A limb image per stage (24 | 48 KB)
+  static constexpr int IMGB = 3 * TK * TT * 2;       // B limb image (24 KB)
+  static constexpr int STAGE = IMGA + IMGB;
+  static constexpr int LDS = 2 * STAGE;              // two buffers (96 | 144 KB)
+  static constexpr int AQ = RA / 4;                  // A column quads per row
+  static constexpr int AR = TK * AQ / PT;            // staged A rows per thread (4)
+  static constexpr int BR = TK * (TT / 4) / PT;      // staged B rows per thread (4 | 2)
+  static constexpr int AROW = TK / AR;               // thread row groups (8 | 8)
+  static_assert(AR == 4 && (BR == 4 || BR == 2), "staging layout");
+};
 
 struct TnArgs {
   int64_t Ms;            // rows per slice (% 32 == 0)
@@ -62,56 +79,53 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_
   l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
 }
 
-// staged registers of one stage: 4 rows x 4 columns of A and of B per thread
-struct TnStage {
-  float4 a[4], b[4];
-};
-
-// thread t: column quad cq = t % 32 (columns 4cq .. 4cq+3), rows 4 mq .. 4 mq + 3 (mq = t / 32)
-__device__ __forceinline__ void tn_load(TnStage& st, const char* __restrict__ Ab, const char* __restrict__ Bb,
-                                        uint32_t oa, uint32_t ob, uint32_t sta, uint32_t stb) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    st.a[i] = *reinterpret_cast<const float4*>(Ab + oa + i * sta);
-    st.b[i] = *reinterpret_cast<const float4*>(Bb + ob + i * stb);
-  }
-}
-
-__device__ __forceinline__ void tn_store_img(char* img, const float4 (&v)[4], int cq, int mq) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint2 l0, l1, l2;
-    split2(v[i].x, v[i].y, l0.x, l1.x, l2.x);
-    split2(v[i].z, v[i].w, l0.y, l1.y, l2.y);
-    const int m = 4 * mq + i;
-    char* row = img + m * (TT * 2) + ((cq ^ (8 * i)) << 3);   // unit cq at cq ^ 8 (m & 3)
-    *reinterpret_cast<uint2*>(row) = l0;
-    *reinterpret_cast<uint2*>(row + TK * TT * 2) = l1;
-    *reinterpret_cast<uint2*>(row + 2 * TK * TT * 2) = l2;
-  }
+// staged row (m, column quad cq) of one operand into its limb image [limb][32 m][W cols]: split,
+// three 8-byte stores; the 8-byte unit cq of row m sits at cq ^ 8 (m & 3)
+template <int W>
+__device__ __forceinline__ void tn_store_row(char* img, const float4& v, int cq, int m) {
+  uint2 l0, l1, l2;
+#ifndef TN_NO_SPLIT
+  split2(v.x, v.y, l0.x, l1.x, l2.x);
+  split2(v.z, v.w, l0.y, l1.y, l2.y);
+#else   // A/B: raw bits (wrong results; measures the split's VALU cost)
+  l0 = make_uint2(__float_as_uint(v.x), __float_as_uint(v.y));
+  l1 = make_uint2(__float_as_uint(v.z), __float_as_uint(v.w));
+  l2 = l0;
+#endif
+  char* row = img + m * (W * 2) + ((cq ^ (8 * (m & 3))) << 3);
+  *reinterpret_cast<uint2*>(row) = l0;
+  *reinterpret_cast<uint2*>(row + TK * W * 2) = l1;
+  *reinterpret_cast<uint2*>(row + 2 * TK * W * 2) = l2;
 }
 
 __device__ __forceinline__ s16x4 tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
-// fragment of 32 columns (column block a) for 16-k half s: limb l = two transposed reads
-// (m = 16s + 8h + 0..3 and + 4..7)
+// fragment of 32 columns (column block a: offset xa) for 16-k half s of an image W columns wide:
+// limb l = two transposed reads (m = 16s + 8h + 0..3 and + 4..7)
+template <int W>
 __device__ __forceinline__ bf16x8 tn_frag(const char* img, int l, int s, int lane_off, int xa) {
-  const char* p = img + l * (TK * TT * 2) + s * (16 * TT * 2) + lane_off + xa;
-  const s16x4 lo = tr_read(p), hi = tr_read(p + 4 * TT * 2);
+  const char* p = img + l * (TK * W * 2) + s * (16 * W * 2) + lane_off + xa;
+  const s16x4 lo = tr_read(p), hi = tr_read(p + 4 * W * 2);
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-__global__ void __launch_bounds__(64 * TW, 1) gemm_tn_x3_kernel(TnArgs g) {
+template <int NWV>
+__global__ void __launch_bounds__(64 * NWV, 1) gemm_tn_x3_kernel(TnArgs g) {
+  using X = TC<NWV>;
+  constexpr int RA = X::RA;
   extern __shared__ __attribute__((aligned(16))) char tlds[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
   const int wm = wave >> 1, wn = wave & 1;
-  const int cq = tid & 31, mq = tid >> 5;
+  // staging: A thread (column quad aq, rows 4 am .. 4 am + 3); B thread (bq, rows BR bm ..)
+  const int aq = tid % X::AQ, am = tid / X::AQ;
+  const int bq = tid & 31, bm = tid >> 5;
   // transposed-read lane offset: row 8h + q (+ 4 e), 8-byte unit 8 (a ^ q) + 4 gb + p
   const int q = (lane >> 2) & 3, p = lane & 3, gb = (lane >> 4) & 1;
-  const int lane_off = (8 * h + q) * (TT * 2) + (4 * gb + p) * 8;
+  const int lane_a = (8 * h + q) * (RA * 2) + (4 * gb + p) * 8;
+  const int lane_b = (8 * h + q) * (TT * 2) + (4 * gb + p) * 8;
   int xa[2], xb[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -132,9 +146,9 @@ __global__ void __launch_bounds__(64 * TW, 1) gemm_tn_x3_kernel(TnArgs g) {
     const int s = t % g.S;
     const int z = t / g.S;
     const int64_t m0 = (int64_t)s * g.Ms;
-    const char* Ab = reinterpret_cast<const char*>(g.A + z * g.sa + m0 * g.lda + ntile * TT);
+    const char* Ab = reinterpret_cast<const char*>(g.A + z * g.sa + m0 * g.lda + ntile * RA);
     const char* Bb = reinterpret_cast<const char*>(g.B + z * g.sb + m0 * g.ldb + ctile * TT);
-    const uint32_t oa = (4 * mq) * sta + cq * 16, ob = (4 * mq) * stb + cq * 16;
+    const uint32_t oa = (4 * am) * sta + aq * 16, ob = (X::BR * bm) * stb + bq * 16;
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -142,51 +156,99 @@ __global__ void __launch_bounds__(64 * TW, 1) gemm_tn_x3_kernel(TnArgs g) {
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    TnStage st;
-    tn_load(st, Ab, Bb, oa, ob, sta, stb);
-    __syncthreads();   // (previous tile's last reads of buffer 0 are done)
-    tn_store_img(tlds, st.a, cq, mq);
-    tn_store_img(tlds + IMG, st.b, cq, mq);
-    if (nst > 1) tn_load(st, Ab, Bb, oa + TK * sta, ob + TK * stb, sta, stb);
-    __syncthreads();
-    for (int k = 0; k < nst; ++k) {
-      const char* ia = tlds + (k & 1) * STAGE;
-      const char* ib = ia + IMG;
+    float4 sa[4], sb[X::BR];
 #pragma unroll
-      for (int hs = 0; hs < 2; ++hs) {
-        bf16x8 fa[2][3], fb[2][3];
+    for (int i = 0; i < 4; ++i) sa[i] = *reinterpret_cast<const float4*>(Ab + oa + i * sta);
+#pragma unroll
+    for (int i = 0; i < X::BR; ++i) sb[i] = *reinterpret_cast<const float4*>(Bb + ob + i * stb);
+    __syncthreads();   // (previous tile's last reads of buffer 0 are done)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tn_store_row<RA>(tlds, sa[i], aq, 4 * am + i);
+#pragma unroll
+    for (int i = 0; i < X::BR; ++i) tn_store_row<TT>(tlds + X::IMGA, sb[i], bq, X::BR * bm + i);
+    if (nst > 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sa[i] = *reinterpret_cast<const float4*>(Ab + oa + TK * sta + i * sta);
+#pragma unroll
+      for (int i = 0; i < X::BR; ++i) sb[i] = *reinterpret_cast<const float4*>(Bb + ob + TK * stb + i * stb);
+    }
+    __syncthreads();
+#ifdef TN_CLOCK   // A/B instrumentation: per-stage s_memtime stamps of workgroup 0's first tile into g.C
+    uint64_t* clk = (blockIdx.x == 0 && lane == 0 && tile == lo)
+                        ? reinterpret_cast<uint64_t*>(g.C + (int64_t)g.batch * g.S * g.R * g.ldc)   // past the output
+                        : nullptr;
+#define TN_STAMP(e) \
+  if (clk && k < 32 && (wave & 3) == 0) clk[((wave >> 2) * 32 + k) * 4 + (e)] = __builtin_amdgcn_s_memtime()
+#else
+#define TN_STAMP(e)
+#endif
+    for (int k = 0; k < nst; ++k) {
+      TN_STAMP(0);
+      const char* ia = tlds + (k & 1) * X::STAGE;
+      const char* ib = ia + X::IMGA;
+      // stage k+1's split + image writes (into the other buffer, free since the last barrier) and
+      // stage k+2's loads run between the MFMA blocks of stage k: unit u = one staged row of A
+      // (u < 4) or B, its load re-issued right after its write (phase clock: serialised after the
+      // MFMAs they took 1,240 + 350 of 3,710 cycles per stage).  Unconditional (a branch here
+      // makes the compiler wait vmcnt(0) at every unit): the last stage writes the idle buffer,
+      // the last two re-load stage nst-1.
+      char* nb = tlds + ((k + 1) & 1) * X::STAGE;
+      const int kl = min(k + 2, nst - 1);
+      const uint32_t la = oa + kl * TK * sta, lb = ob + kl * TK * stb;
+      auto side = [&](int u) {
+#ifdef TN_NO_SIDE
+        return;
+#endif
+        if (u < 4) {
+          tn_store_row<RA>(nb, sa[u], aq, 4 * am + u);
+          sa[u] = *reinterpret_cast<const float4*>(Ab + la + u * sta);
+        } else if (u - 4 < X::BR) {
+          tn_store_row<TT>(nb + X::IMGA, sb[u - 4], bq, X::BR * bm + u - 4);
+          sb[u - 4] = *reinterpret_cast<const float4*>(Bb + lb + (u - 4) * stb);
+        }
+      };
+      // 4 waves: the fragments of half 1 are read while half 0's MFMAs run (registers to spare at
+      // one wave per SIMD); 8 waves: one half at a time (the other wave covers the read latency)
+      constexpr int FB = NWV == 4 ? 2 : 1;
+      bf16x8 fa[FB][2][3], fb[FB][2][3];
+      auto read_half = [&](int hs) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int l = 0; l < 3; ++l) {
-            fa[i][l] = tn_frag(ia, l, hs, lane_off, xa[i]);
-            fb[i][l] = tn_frag(ib, l, hs, lane_off, xb[i]);
+            fa[hs % FB][i][l] = tn_frag<RA>(ia, l, hs, lane_a, xa[i]);
+            fb[hs % FB][i][l] = tn_frag<TT>(ib, l, hs, lane_b, xb[i]);
           }
+      };
+      read_half(0);
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        if (FB == 2 && hs == 0) read_half(1);
+        if (FB == 1 && hs == 1) read_half(1);
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             f32x16 c = acc[i][j];
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % FB][i][2], fb[hs % FB][j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % FB][i][1], fb[hs % FB][j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % FB][i][0], fb[hs % FB][j][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % FB][i][1], fb[hs % FB][j][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % FB][i][0], fb[hs % FB][j][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs % FB][i][0], fb[hs % FB][j][0], c, 0, 0, 0);
             acc[i][j] = c;
+            side(4 * hs + 2 * i + j);
+            __builtin_amdgcn_sched_barrier(0);   // keep each unit between its MFMA blocks
           }
       }
-      if (k + 1 < nst) {   // buffer (k+1)&1 was last read at stage k-1, before the last barrier
-        char* nb = tlds + ((k + 1) & 1) * STAGE;
-        tn_store_img(nb, st.a, cq, mq);
-        tn_store_img(nb + IMG, st.b, cq, mq);
-        if (k + 2 < nst) tn_load(st, Ab, Bb, oa + (k + 2) * TK * sta, ob + (k + 2) * TK * stb, sta, stb);
-      }
+      TN_STAMP(1);
+      TN_STAMP(2);
+      TN_STAMP(3);
       __syncthreads();
     }
     // acc[i][j][e] = C[n0 + 32i + 8(e >> 2) + 4h + (e & 3)][c0 + 32j + r]: 32 lanes store one
     // 128-byte row segment per element
-    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * TT + wm * 64) * g.ldc;
+    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * RA + wm * 64) * g.ldc;
     const int c0 = ctile * TT + wn * 64 + r;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -230,19 +292,31 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   g.sb = a.sb;
   g.C = a.C;
   g.ldc = a.ldc;
-  g.rt = a.R / TT;
+  // 256-row tiles (8 waves) when R allows; LGX_GEMM_TN_WAVES=4 forces the 128-row tiles
+  static const int force4 = [] {
+    const char* e = getenv("LGX_GEMM_TN_WAVES");
+    return e && atoi(e) == 4;
+  }();
+  const int nwv = (a.R % 256 == 0 && !force4) ? 8 : 4;
+  const int RA = nwv == 8 ? 256 : 128;
+  g.rt = a.R / RA;
   g.ct = (a.Cc + TT - 1) / TT;
   const int64_t tiles = (int64_t)g.rt * g.ct * a.slices * a.batch;
   if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: too many tiles");
   g.tiles = (int32_t)tiles;
   static const bool attrs =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x3_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          TN_LDS) == hipSuccess;
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x3_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TC<4>::LDS) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x3_kernel<8>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TC<8>::LDS) == hipSuccess;
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
-  LGX_LAUNCH(gemm_tn_x3_kernel, dim3((unsigned)wgs), dim3(64 * TW), TN_LDS, reinterpret_cast<hipStream_t>(stream), g);
+  if (nwv == 8)
+    LGX_LAUNCH(gemm_tn_x3_kernel<8>, dim3((unsigned)wgs), dim3(512), TC<8>::LDS, reinterpret_cast<hipStream_t>(stream), g);
+  else
+    LGX_LAUNCH(gemm_tn_x3_kernel<4>, dim3((unsigned)wgs), dim3(256), TC<4>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   return lgx_hip_status("lgx_gemm_tn");
 }

@@ -289,7 +289,7 @@ class FusedPPOUpdate:
     def _tn_slices(R, Cc, M, cus=256):
         """Row slices of one lgx_gemm_tn launch: the fewest (>= 8, powers of 2) that give every CU
         an output tile (R/128 x ceil(Cc/128) tiles per slice and network) with 32-row multiples."""
-        tiles = (R // 128) * (-(-Cc // 128)) * 2
+        tiles = (R // (256 if R % 256 == 0 else 128)) * (-(-Cc // 128)) * 2   # lgx_gemm_tn tile rows
         s = 8
         while tiles * s < cus and M % (2 * s * 32) == 0:
             s *= 2

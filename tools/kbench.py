@@ -200,12 +200,26 @@ def tn_bench(M=24576, iters=20):
         B = torch.randn(2, M, ldb, device=dev)
         f = 2.0 * 2 * M * R * Cc
         for S in [int(x) for x in os.environ.get("KB_SLICES", "8,16,32").split(",")]:
-            Cout = torch.empty(2, S, R, Cc, device=dev)
+            Cbuf = torch.empty(2 * S * R * Cc + 1024, device=dev)   # (+ a tail for TN_CLOCK stamps)
+            Cout = Cbuf[:2 * S * R * Cc].view(2, S, R, Cc)
             a = abi.LgxGemmTnArgs()
             a.M, a.R, a.Cc, a.slices, a.batch = M, R, Cc, S, 2
             a.A, a.lda, a.sa, a.B, a.ldb, a.sb = A.data_ptr(), R, M * R, B.data_ptr(), ldb, M * ldb
             a.C, a.ldc = Cout.data_ptr(), Cc
             t1 = timeit(lambda: lgxlib.check(lib.lgx_gemm_tn(C.byref(a), stream), "tn"), iters=iters)
+            if os.environ.get("KB_CLOCK"):   # TN_CLOCK build: per-stage stamps of workgroup 0's first tile
+                Cbuf.zero_()
+                lgxlib.check(lib.lgx_gemm_tn(C.byref(a), stream), "tn")
+                torch.cuda.synchronize()
+                st = Cbuf[2 * S * R * Cc:].view(torch.int64)[:4 * 32 * 4].view(4, 32, 4).double().cpu()
+                for w in range(4):   # (8-wave kernel: rows 0, 1 = waves 0 and 4)
+                    d = st[w][(st[w, :, 3] > 0) & (st[w, :, 0] > 0)]
+                    if len(d) < 2:
+                        continue
+                    per = (d[1:, 0] - d[:-1, 0]).mean().item()
+                    seg = [(d[:, e + 1] - d[:, e]).mean().item() for e in range(3)]
+                    print(f"  wave {w}: stages {len(d)} per-stage {per:.0f}: compute {seg[0]:.0f} split+write {seg[1]:.0f} "
+                          f"load-issue {seg[2]:.0f} barrier {per - sum(seg):.0f}", flush=True)
             P = torch.empty(2 * S, R, Cc, device=dev)
             Bv = B[..., :Cc].reshape(2 * S, M // S, Cc) if ldb == Cc else B.view(2 * S, M // S, ldb)[..., :Cc]
             t2 = timeit(lambda: torch.bmm(A.view(2 * S, M // S, R).transpose(1, 2), Bv, out=P), iters=iters)
