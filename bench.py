@@ -45,17 +45,21 @@ MI355X_BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PRODUCTS = 6                  # split-bf16: six bf16 limb products per f32 product (lgx_gemm_split.hip)
 
 
-def gemm_kernel_info(epi, split):
-    """(kernel name as rocprof reports it, compute pipe, peak in f32-product TFLOP/s) of the PPO
-    GEMM instantiation with epilogue `epi`."""
-    if split:
-        return (f"gemm_nt_x3p_kernel<{epi}, *, 8>",
-                "bf16 MFMA (v_mfma_f32_32x32x16_bf16), split-bf16: 6 limb products per f32 product",
-                MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS)
-    return f"gemm_nt_kernel<8, {epi}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
+def gemm_kernel_info(key, split):
+    """(kernel name pattern as rocprof reports it, compute pipe, peak in f32-product TFLOP/s) of the
+    PPO GEMM launches timed under `key` (an lgx_gemm_nt epilogue, or "tn" = lgx_gemm_tn)."""
+    pipe = "bf16 MFMA (v_mfma_f32_32x32x16_bf16), split-bf16: 6 limb products per f32 product"
+    if key == "tn":
+        return "gemm_tn_x3_kernel<*>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+    if split:   # bias + ELU: the pipelined kernel; ELU' + column sums: the register-staged one
+        name = f"gemm_nt_x3p_kernel<{key}, *, 8>" if key != 2 else "gemm_nt_x3_kernel<2, true>"
+        return name, pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+    return f"gemm_nt_kernel<8, {key}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
 GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "
                  "to 256, 512->256, 256->128)",
-              2: "lgx_gemm_nt LGX_GEMM_DELU_COLSUM: backward dA of the hidden layers (512x256 and 256x128 weights)"}
+              2: "lgx_gemm_nt LGX_GEMM_DELU_COLSUM: backward dA of the hidden layers (512x256 and 256x128 weights)",
+              "tn": "lgx_gemm_tn: weight gradients dW_k = dZ_k^T Y_{k-1} of the hidden layers over row slices "
+                    "(512x235, 256x512, 128x256 per network)"}
 
 
 def pmc_ppo_traffic_bytes(kernel):
@@ -306,7 +310,7 @@ def main():
     # the PPO-update GEMM instantiations, timed live (events on the launch stream)
     mb_per_iter = runner.alg.num_learning_epochs * runner.alg.num_mini_batches
     gemm_roofs = []
-    for epi, (n, t_ms, flop, mbs) in sorted(gemm_t.items()):
+    for epi, (n, t_ms, flop, mbs) in sorted(gemm_t.items(), key=lambda kv: str(kv[0])):
         if not n or not mbs:
             continue
         kname, pipe, peak = gemm_kernel_info(epi, getattr(fused, "split", False))
@@ -316,7 +320,7 @@ def main():
             "frac": flop / (t_ms * 1e-3) / 1e12 / peak,
             "traffic": pmc_ppo_traffic_bytes(kname), "algorithmic_per_launch": flop / n, "avg_ms": t_ms / n,
             "launches_timed": n, "share_of_iteration": (t_ms / mbs) * mb_per_iter / it_ms,
-            "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K "
+            "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K / Cc "
                     "(f32 products; the split-bf16 peak is the bf16 dense MFMA peak / 6 limb products); HIP events "
                     "around every launch of every k-th minibatch (LGX_BENCH_GEMM_TIMING); traffic = 2 FETCH_SIZE + "
                     f"WRITE_SIZE per launch from {os.path.relpath(PPO_PMC_FILE, ROOT)}"})

@@ -609,6 +609,16 @@ class FusedPPOUpdate:
             k = self.k_alg.get(id(g), g.K)
             self._t_events.append((g.epi, 2.0 * g.M * g.N * k * g.batch, e0, e1))
 
+    def _gemm_tn(self, t, stream):
+        rec = getattr(self, "_t_period", 0) and self._t_count % self._t_period == 0   # (as _gemm)
+        if rec:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        self.check(self.lib.lgx_gemm_tn(C.byref(t), stream), "gemm_tn")
+        if rec:
+            e1.record()
+            self._t_events.append(("tn", 2.0 * t.M * t.R * t.Cc * t.batch, e0, e1))
+
     def gemm_timings(self):
         """{epilogue: (launches, total ms, total algorithmic FLOP, timed minibatches)} of the timed
         launches."""
@@ -706,7 +716,7 @@ class FusedPPOUpdate:
             Sl = self.Sk[k]
             if k in self.gemm_dw:
                 for t in self.gemm_dw[k]:
-                    chk(lib.lgx_gemm_tn(C.byref(t), stream), "gemm_tn")
+                    self._gemm_tn(t, stream)
             else:
                 torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2),
                           self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]), out=self.P[k])
@@ -723,7 +733,7 @@ class FusedPPOUpdate:
             if len(t) > 1:
                 t[1].B = (xcp if xcp is not None else xp).data_ptr()
             for tk in t:
-                chk(lib.lgx_gemm_tn(C.byref(tk), stream), "gemm_tn")
+                self._gemm_tn(tk, stream)
         elif xs is not None and len(xs) > 2:    # one batched GEMM: 2 networks x S row slices
             x2 = xs[2].view(2 * S, M // S, self.Kp)[:, :, :self.num_obs]
             torch.bmm(dZ.view(2 * S, M // S, h[0]).transpose(1, 2), x2, out=self.P[0].view(2 * S, h[0], self.num_obs))
