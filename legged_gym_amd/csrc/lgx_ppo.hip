@@ -444,13 +444,46 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
 // (s = g, g + 256/OT, ...) and combine in LDS in a fixed order.  OT = 64 for short slice loops
 // (split-K partials, 8 slices), 16 for long ones (per-chunk bias / head partials, hundreds of
 // slices): independent loads in flight instead of one serial chain per output.
+// Jobs whose offsets, strides and n are multiples of 4 floats (16-byte aligned: the split-K weight
+// partials) run on float4 lanes (tile_outputs < 0: -4 x 64 outputs per workgroup, 64 lanes x 4
+// slice groups), the rest on scalar lanes.
 __global__ void __launch_bounds__(TPB)
 reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs) {
   __shared__ float red[TPB];
+  __shared__ float4 red4[TPB];
   int b = blockIdx.x, ji = 0;
   while (ji + 1 < njobs && b >= jobs.tile_start[ji + 1]) ++ji;
   const lgx_reduce_job& jb = jobs.job[ji];
   const int ot = jobs.tile_outputs[ji];
+  if (ot < 0) {   // float4 path: 64 lanes x 4 outputs per group, TPB / 64 groups over the slices
+    const int groups = TPB / 64;
+    const int t = threadIdx.x, oi = t % 64, g = t / 64;
+    const int64_t o4 = (int64_t)(b - jobs.tile_start[ji]) * 64 + oi;   // float4 output index
+    const int64_t total4 = (int64_t)jb.count * jb.n / 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    int64_t j = 0, i = 0;
+    if (o4 < total4) {
+      j = (4 * o4) / jb.n;
+      i = 4 * o4 - j * jb.n;
+      const float* s = jb.src + j * jb.job_stride + i;
+#pragma unroll 4
+      for (int k = g; k < jb.slices; k += groups) {
+        const float4 v = *reinterpret_cast<const float4*>(s + (int64_t)k * jb.slice_stride);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    red4[t] = acc;
+    __syncthreads();
+    if (g == 0 && o4 < total4) {
+      float4 sum = red4[oi];
+      for (int q = 1; q < groups; ++q) {
+        const float4 u = red4[q * 64 + oi];
+        sum.x += u.x; sum.y += u.y; sum.z += u.z; sum.w += u.w;
+      }
+      *reinterpret_cast<float4*>(jb.dst + j * jb.dst_stride + i) = sum;
+    }
+    return;
+  }
   const int groups = TPB / ot;
   const int t = threadIdx.x, oi = t % ot, g = t / ot;
   const int64_t o = (int64_t)(b - jobs.tile_start[ji]) * ot + oi;
@@ -725,8 +758,11 @@ extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void
       return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job");
     J.job[i] = j;
     J.tile_start[i] = (int32_t)tiles;
-    J.tile_outputs[i] = j.slices > 32 ? 16 : 64;
-    tiles += ((int64_t)j.count * j.n + J.tile_outputs[i] - 1) / J.tile_outputs[i];
+    const bool vec = j.n % 4 == 0 && j.job_stride % 4 == 0 && j.slice_stride % 4 == 0 && j.dst_stride % 4 == 0 &&
+                     ((uintptr_t)j.src & 15) == 0 && ((uintptr_t)j.dst & 15) == 0 && j.slices <= 128;
+    J.tile_outputs[i] = vec ? -4 : (j.slices > 32 ? 16 : 64);
+    const int64_t per = vec ? 256 : J.tile_outputs[i];
+    tiles += ((int64_t)j.count * j.n + per - 1) / per;
   }
   if (tiles > (1 << 30)) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: too large");
   hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs);

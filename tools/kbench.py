@@ -256,7 +256,7 @@ if __name__ == "__main__":
         if f"ppo_{m}" in what:
             ppo_ab(modes=(m,), gemms=False)
     if "gemm" in what:
-        gemm_bench(torch_too="torch" in what)
+        gemm_bench(M=int(os.environ.get("KB_M", "24576")), torch_too="torch" in what)
     if "tn" in what:
         tn_bench()
 
