@@ -415,6 +415,16 @@ int lgx_head_bwd_finalize(const lgx_ppo_loss_args* loss, const float* d_mu, cons
                           const float* W4c, float* A3, int64_t rows, int32_t num_actions, int32_t hidden,
                           float* partials, void* stream);
 
+/* lgx_ppo_loss (head_in form) and lgx_head_bwd in ONE launch over 32-row chunks: the last hidden
+ * activations are read once; head_in ([2,M,hidden], hidden % 16 == 0) is overwritten by dZ3;
+ * args->partials takes out[0] floats of loss partials, head_partials out[1] floats of
+ * [A*H dW4a | H dW4c | 2H db3] chunk partials (lgx_ppo_loss_bwd_layout; out[2] = dynamic LDS
+ * bytes, <= 96 KB).  d_mu / d_v are not written.  With args->defer_finalize the loss finalize
+ * runs in the following lgx_reduce_slices_finalize call.  Replaces lgx_ppo_loss +
+ * lgx_head_bwd_finalize (rsl_rl ppo.py:154-185 + the output layers' backward). */
+int lgx_ppo_loss_bwd_layout(int64_t rows, int32_t num_actions, int32_t hidden, int64_t out[3]);
+int lgx_ppo_loss_bwd(const lgx_ppo_loss_args* args, float* head_partials, void* stream);
+
 /* dA [nets,M,H] -> dA * elu'(Y) in place (Y = ELU output) + per-chunk column sums */
 int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int32_t nets);
 int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32_t hidden, int32_t nets, float* partials,
@@ -428,6 +438,10 @@ typedef struct lgx_reduce_job {
   int32_t slices, count;
 } lgx_reduce_job;
 int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream);
+/* lgx_reduce_slices plus the deferred loss finalize of a lgx_ppo_loss_bwd call (one extra
+ * workgroup; loss->defer_finalize != 0): d std, head-bias gradients, KL, stats, adaptive LR */
+int lgx_reduce_slices_finalize(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* loss,
+                               void* stream);
 
 /* clip_grad_norm_(max_norm) of (grad_scale * g) fused into torch-Adam (no weight decay) over
  * one flat parameter buffer; *step is advanced on the device; lr is a device double */

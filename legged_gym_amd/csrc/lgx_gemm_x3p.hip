@@ -42,26 +42,31 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float fx2 __attribute__((ext_vector_type(2)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
-constexpr int PM = 256, PN = 128, PK = 32;
-constexpr int A_ST = PM * PK * 4;            // 32 KB: f32 A stage (256 rows x 128 B)
+constexpr int PN = 128, PK = 32;
 constexpr int B_ST = 3 * PN * PK * 2;        // 24 KB: limb B stage ([limb][128 n][64 B])
 constexpr int NSA = 3, NSB = 2;              // ring depths
-constexpr int OFF_B = NSA * A_ST;
-constexpr int OFF_BIAS = OFF_B + NSB * B_ST;   // 3 x 1 KB: bias of the pending / current / next tile
-constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 150,528 B
 constexpr int B_BLK = 3 * 128 * 32;             // bf16 per pre-split (128 n x 32 k) block
 
-template <int NWV>
+// Tile of PM = 256 rows (the default) or 128 rows (half tiles: the layer whose 256-row tile count
+// leaves a fractional last round on the CUs, e.g. 384 tiles on 256 CUs -> 768 half tiles = 3 rounds)
+template <int NWV, int PM>
 struct XC {
+  static constexpr int A_ST = PM * PK * 4;               // f32 A stage (PM rows x 128 B): 32 | 16 KB
+  static constexpr int OFF_B = NSA * A_ST;
+  static constexpr int OFF_BIAS = OFF_B + NSB * B_ST;    // 3 x 1 KB: bias of the pending / current / next tile
+  static constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 150,528 | 101,376 B
   static constexpr int WGN = NWV == 8 ? 2 : 1;          // waves along N
   static constexpr int WGM = NWV / WGN;                  // waves along M (4)
-  static constexpr int WI = PM / WGM / 32;               // 32-row accumulator tiles per wave (2)
+  static constexpr int WI = PM / WGM / 32;               // 32-row accumulator tiles per wave (2 | 1)
   static constexpr int WJ = PN / WGN / 32;               // 32-column accumulator tiles per wave (2 | 4)
   static constexpr int PT = 64 * NWV;
-  static constexpr int A_GL = A_ST / (PT * 16);          // LDS-DMA loads per thread per A stage (4 | 8)
+  static constexpr int A_GL = A_ST / (PT * 16);          // LDS-DMA loads per thread per A stage (4 | 8; 2)
   static constexpr int B_GL = B_ST / (PT * 16);          // per B stage (3 | 6)
-  static constexpr int GROUPS = WI * WJ * 4;             // float4 output runs per lane (16 | 32)
-  static_assert(WGM == 4 && WI == 2, "column-sum pairing and A offsets assume 4 wave rows of 64");
+  static constexpr int GROUPS = WI * WJ * 4;             // float4 output runs per lane (16 | 32; 8)
+  static constexpr int NB = 2 * WI * WJ;                 // MFMA blocks per slot (two 16-k halves)
+  static constexpr int ITEMS = B_GL + 1 + A_GL;          // side items per slot: B loads, bias, A loads
+  static constexpr int IPB = (ITEMS + NB - 1) / NB;      // side items per MFMA block
+  static_assert(WGM == 4 && (WI == 1 || WI == 2), "A offsets assume 4 wave rows of 32 WI");
 };
 
 struct PArgs {
@@ -151,14 +156,14 @@ __device__ __forceinline__ uint32_t lds_addr(const char* p) {
 // Per-lane A source offsets (bytes from the batch entry's base) of one tile's DMA loads: LDS
 // block b = A_GL * wave + i (1 KB) holds tile rows 8b .. 8b + 7; lane l writes row 8b + l / 8 at
 // chunk l % 8, which holds k-chunk (l % 8) ^ ((row >> 1) & 7).
-template <int NWV>
+template <int NWV, int PM>
 struct AOffs {
-  uint32_t o[XC<NWV>::A_GL];
+  uint32_t o[XC<NWV, PM>::A_GL];
 };
 
-template <int NWV>
-__device__ __forceinline__ void a_offs(AOffs<NWV>& a, const PArgs& g, int32_t mt, int tid) {
-  constexpr int AG = XC<NWV>::A_GL;
+template <int NWV, int PM>
+__device__ __forceinline__ void a_offs(AOffs<NWV, PM>& a, const PArgs& g, int32_t mt, int tid) {
+  constexpr int AG = XC<NWV, PM>::A_GL;
   const int w = tid >> 6, lane = tid & 63;
 #pragma unroll
   for (int i = 0; i < AG; ++i) {
@@ -175,27 +180,29 @@ struct DmaPlan {
   uint32_t dst;
 };
 
-template <int NWV>
+template <int NWV, int PM>
 __device__ __forceinline__ DmaPlan plan_a(uint32_t lds0, int buf, const PArgs& g, int z, int ks, int tid) {
-  constexpr int AG = XC<NWV>::A_GL;
+  using X = XC<NWV, PM>;
   return DmaPlan{uniform_ptr(reinterpret_cast<const char*>(g.A + z * g.sa) + ks * (PK * 4)),
-                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + buf * A_ST + (tid >> 6) * (AG * 1024))};
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + buf * X::A_ST + (tid >> 6) * (X::A_GL * 1024))};
 }
 
-template <int NWV>
+template <int NWV, int PM>
 __device__ __forceinline__ DmaPlan plan_b(uint32_t lds0, int buf, const PArgs& g, const PTile& T, int ks, int tid) {
-  constexpr int BG = XC<NWV>::B_GL;
+  using X = XC<NWV, PM>;
+  constexpr int BG = X::B_GL;
   return DmaPlan{uniform_ptr(reinterpret_cast<const char*>(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb + ks) * B_BLK) +
                              (tid >> 6) * (BG * 1024)),
-                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + OFF_B + buf * B_ST + (tid >> 6) * (BG * 1024))};
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + X::OFF_B + buf * B_ST + (tid >> 6) * (BG * 1024))};
 }
 
-template <int NWV>
-__device__ __forceinline__ void issue_a(uint32_t lds0, int buf, const PArgs& g, const AOffs<NWV>& a, int z, int ks,
-                                        int tid) {
-  constexpr int AG = XC<NWV>::A_GL;
+template <int NWV, int PM>
+__device__ __forceinline__ void issue_a(uint32_t lds0, int buf, const PArgs& g, const AOffs<NWV, PM>& a, int z,
+                                        int ks, int tid) {
+  using X = XC<NWV, PM>;
+  constexpr int AG = X::A_GL;
   const char* src = uniform_ptr(reinterpret_cast<const char*>(g.A + z * g.sa) + ks * (PK * 4));
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * A_ST + (tid >> 6) * (AG * 1024));
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + buf * X::A_ST + (tid >> 6) * (AG * 1024));
 #pragma unroll
   for (int i = 0; i < AG; ++i) glds16(src, a.o[i], dst + i * 1024);
 }
@@ -203,18 +210,19 @@ __device__ __forceinline__ void issue_a(uint32_t lds0, int buf, const PArgs& g, 
 // B stage of slot (T, ks); with `bias` (BIAS_ELU, a tile's first stage, wave 0 only) also the
 // tile's 128 bias values into bias buffer `bbuf` (lanes 32-63 duplicate lanes 0-31).  The extra
 // load is issued with the B stage, so every vmcnt count of the pipeline stays the same.
-template <int NWV>
+template <int NWV, int PM>
 __device__ __forceinline__ void issue_b(uint32_t lds0, int buf, const PArgs& g, const PTile& T, int ks, int tid,
                                         bool bias, int bbuf) {
-  constexpr int BG = XC<NWV>::B_GL;
+  using X = XC<NWV, PM>;
+  constexpr int BG = X::B_GL;
   const int w = tid >> 6, lane = tid & 63;
   const char* src = uniform_ptr(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb + ks) * B_BLK);
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + OFF_B + buf * B_ST + w * (BG * 1024));
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + X::OFF_B + buf * B_ST + w * (BG * 1024));
 #pragma unroll
   for (int i = 0; i < BG; ++i) glds16(src, (uint32_t)(w * (BG * 1024) + i * 1024 + lane * 16), dst + i * 1024);
   if (bias)
     glds16(uniform_ptr(g.bias + (int64_t)T.z * g.N + T.nt * PN), (uint32_t)((lane & 31) * 16),
-           __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
+           __builtin_amdgcn_readfirstlane(lds0 + X::OFF_BIAS + bbuf * 1024));
 }
 
 // One 32-k slot of a wave's WI x WJ accumulators: per 16-k half, its A row tiles are read (f32)
@@ -226,10 +234,11 @@ __device__ __forceinline__ void issue_b(uint32_t lds0, int buf, const PArgs& g, 
 // issues and deferred stores are spread between the MFMA blocks, where a DMA issue that waits for
 // the texture unit to accept it costs no MFMA time (issued in one burst before the compute, the 14
 // DMA loads of a 4-wave slot took ~950 cycles of the wave's ~5600).
-template <int NWV, typename Side>
+template <int NWV, int PM, typename Side>
 __device__ __forceinline__ void compute_slot(const char* __restrict__ la, const char* __restrict__ lb, int wm, int wn,
-                                             int r, int h, f32x16v (&acc)[2][XC<NWV>::WJ], Side&& side) {
-  constexpr int WI = XC<NWV>::WI, WJ = XC<NWV>::WJ;
+                                             int r, int h, f32x16v (&acc)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ],
+                                             Side&& side) {
+  constexpr int WI = XC<NWV, PM>::WI, WJ = XC<NWV, PM>::WJ;
   const int sa = (r >> 1) & 7, sb = (r >> 2) & 3;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
@@ -281,12 +290,13 @@ __device__ __forceinline__ float4 q4(const f32x16v& v, int q) {
 }
 
 // Bias + ELU (or plain) output of float4 run gi = (i, j, q), gi = 4 (WJ i + j) + q, of a lane.
-template <int EPI, int NWV>
-__device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pend)[2][XC<NWV>::WJ], const PTile& T,
-                                              int wm, int wn, int r, int h, const float* bias_lds, int gi) {
-  constexpr int WJ = XC<NWV>::WJ;
+template <int EPI, int NWV, int PM>
+__device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pend)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ],
+                                              const PTile& T, int wm, int wn, int r, int h, const float* bias_lds,
+                                              int gi) {
+  constexpr int WI = XC<NWV, PM>::WI, WJ = XC<NWV, PM>::WJ;
   const int q = gi & 3, j = (gi >> 2) % WJ, i = (gi >> 2) / WJ;
-  const int64_t row = (int64_t)T.mt * PM + wm * 64 + 32 * i + r;
+  const int64_t row = (int64_t)T.mt * PM + wm * 32 * WI + 32 * i + r;
   const int cn = wn * 32 * WJ + 32 * j + 8 * q + 4 * h;
   float4 v = q4(pend[i][j], q);
   if (EPI == LGX_GEMM_BIAS_ELU) {
@@ -317,14 +327,17 @@ __device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pe
 // register indices).  KBT == 0: the epilogue runs at the tile's end (after waiting for the next
 // slot's stages, so its stores do not sit in front of them).  (ELU' + column sums: the
 // register-staged gemm_nt_x3_kernel, measured equal or faster for the dA shapes.)
-template <int EPI, int KBT, int NWV>
+template <int EPI, int KBT, int NWV, int PM>
 __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
-  using X = XC<NWV>;
-  constexpr int WJ = X::WJ, AG = X::A_GL;
+  using X = XC<NWV, PM>;
+  constexpr int WI = X::WI, WJ = X::WJ, AG = X::A_GL;
+  constexpr int A_ST = X::A_ST, OFF_B = X::OFF_B, OFF_BIAS = X::OFF_BIAS;
   extern __shared__ __attribute__((aligned(16))) char plds[];
   static_assert(EPI != LGX_GEMM_DELU_COLSUM, "the column-sum epilogue runs on gemm_nt_x3_kernel");
   constexpr bool DEFER = KBT > 0;
-  constexpr int GPS = DEFER ? X::GROUPS / KBT : 0;     // deferred store runs per slot
+  // deferred store runs per slot (slots k with k * GPS < GROUPS store GPS runs each)
+  constexpr int GPS = DEFER ? (X::GROUPS >= KBT ? X::GROUPS / KBT : 1) : 0;
+  static_assert(!DEFER || X::GROUPS % GPS == 0, "every storing slot issues exactly GPS runs (vmcnt counts)");
   constexpr int UNR = KBT > 0 ? KBT : 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -346,13 +359,13 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   int32_t ja = 0, jb = 0;
   PTile Ta = ptile(g, t0), Tb = Ta;
   int ka = 0, kbb = 0;
-  AOffs<NWV> ao;
-  a_offs<NWV>(ao, g, Ta.mt, tid);
+  AOffs<NWV, PM> ao;
+  a_offs<NWV, PM>(ao, g, Ta.mt, tid);
   auto next_a = [&]() {
     if (++ka == kb) {
       ka = 0;
       Ta = ptile(g, t0 + (++ja) * stride);
-      a_offs<NWV>(ao, g, Ta.mt, tid);
+      a_offs<NWV, PM>(ao, g, Ta.mt, tid);
     }
   };
   auto next_b = [&]() {
@@ -364,18 +377,18 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   // prologue: A(0), B(0), A(1)
   constexpr bool BIAS = EPI == LGX_GEMM_BIAS_ELU;
   const bool w0 = __builtin_amdgcn_readfirstlane(wave) == 0;
-  issue_a<NWV>(lds0, 0, g, ao, Ta.z, ka, tid);
+  issue_a<NWV, PM>(lds0, 0, g, ao, Ta.z, ka, tid);
   next_a();
-  issue_b<NWV>(lds0, 0, g, Tb, kbb, tid, BIAS && w0, 0);
+  issue_b<NWV, PM>(lds0, 0, g, Tb, kbb, tid, BIAS && w0, 0);
   next_b();
   if (nslots > 1) {
-    issue_a<NWV>(lds0, 1, g, ao, Ta.z, ka, tid);
+    issue_a<NWV, PM>(lds0, 1, g, ao, Ta.z, ka, tid);
     next_a();
   }
 
-  f32x16v acc[2][WJ], pend[2][WJ];
+  f32x16v acc[WI][WJ], pend[WI][WJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < WI; ++i)
 #pragma unroll
     for (int j = 0; j < WJ; ++j)
 #pragma unroll
@@ -411,14 +424,14 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       const int bbuf = jb % 3;
       DmaPlan pb{nullptr, 0}, pa{nullptr, 0};
       int za = 0;
-      if (do_b) pb = plan_b<NWV>(lds0, (q + 1) % NSB, g, Tb, kbb, tid);
+      if (do_b) pb = plan_b<NWV, PM>(lds0, (q + 1) % NSB, g, Tb, kbb, tid);
       const PTile Tbias = Tb;
       if (do_a) {
-        pa = plan_a<NWV>(lds0, (q + 2) % NSA, g, Ta.z, ka, tid);
+        pa = plan_a<NWV, PM>(lds0, (q + 2) % NSA, g, Ta.z, ka, tid);
         za = Ta.z;
       }
       (void)za;
-      const AOffs<NWV> aoq = ao;
+      const AOffs<NWV, PM> aoq = ao;
       if (do_b) next_b();
       if (do_a) next_a();
       X3P_STAMP(3);
@@ -427,39 +440,44 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       const float* bias_prev = reinterpret_cast<const float*>(plds + OFF_BIAS + ((tj + 2) % 3) * 1024);
       constexpr int BG = X::B_GL;
       auto side = [&](int blk) {
-        // blocks 0 .. BG-1: B loads; BG: bias; BG+1 .. BG+AG: A loads; then the stores
-        if (blk < BG) {
-          if (do_b) glds16(pb.src, (uint32_t)(lane * 16 + blk * 1024), pb.dst + blk * 1024);
-        } else if (blk == BG) {
-          if (do_bias)
-            glds16(uniform_ptr(g.bias + (int64_t)Tbias.z * g.N + Tbias.nt * PN), (uint32_t)((lane & 31) * 16),
-                   __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
-        } else if (blk <= BG + AG) {
-          if (do_a) glds16(pa.src, aoq.o[blk - BG - 1], pa.dst + (blk - BG - 1) * 1024);
+        // side items (IPB per MFMA block, in this order): BG B loads, the bias, AG A loads; then
+        // the stores
+#pragma unroll
+        for (int e = 0; e < X::IPB; ++e) {
+          const int it = blk * X::IPB + e;
+          if (it < BG) {
+            if (do_b) glds16(pb.src, (uint32_t)(lane * 16 + it * 1024), pb.dst + it * 1024);
+          } else if (it == BG) {
+            if (do_bias)
+              glds16(uniform_ptr(g.bias + (int64_t)Tbias.z * g.N + Tbias.nt * PN), (uint32_t)((lane & 31) * 16),
+                     __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
+          } else if (it <= BG + AG) {
+            if (do_a) glds16(pa.src, aoq.o[it - BG - 1], pa.dst + (it - BG - 1) * 1024);
+          }
         }
         if constexpr (DEFER) {
-          constexpr int NB = 2 * X::WI * X::WJ;   // MFMA blocks per slot (2 halves)
-          static_assert(NB >= GPS && NB > BG + AG, "every DMA load and store run gets a block");
+          constexpr int NB = X::NB;
+          static_assert(NB >= GPS, "every store run gets a block");
           // the stores after the last GPS blocks (they may interleave with A(q+2)'s loads: the
           // next wait only needs B(q+1), which precedes both)
           const int u = blk - (NB - GPS);
           if (st_now && u >= 0 && u < GPS)
-            p_store_group<EPI, NWV>(g, pend, Tp, wm, wn, r, h, bias_prev, k * GPS + u);
+            p_store_group<EPI, NWV, PM>(g, pend, Tp, wm, wn, r, h, bias_prev, k * GPS + u);
         }
         __builtin_amdgcn_sched_barrier(0);
       };
       X3P_STAMP(4);
 #ifndef X3P_NO_COMPUTE
-      compute_slot<NWV>(plds + (q % NSA) * A_ST, plds + OFF_B + (q % NSB) * B_ST, wm, wn, r, h, acc, side);
+      compute_slot<NWV, PM>(plds + (q % NSA) * A_ST, plds + OFF_B + (q % NSB) * B_ST, wm, wn, r, h, acc, side);
 #else
-      for (int blk = 0; blk < 2 * X::WI * X::WJ; ++blk) side(blk);
+      for (int blk = 0; blk < X::NB; ++blk) side(blk);
 #endif
       X3P_STAMP(5);
     }
     // ---- tile end
     if constexpr (DEFER) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
         for (int j = 0; j < WJ; ++j) pend[i][j] = acc[i][j];
       Tp = T;
@@ -472,14 +490,14 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 #ifndef X3P_NO_EPI
 #pragma unroll
       for (int gi = 0; gi < X::GROUPS; ++gi)
-        p_store_group<EPI, NWV>(g, acc, T, wm, wn, r, h,
-                                reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
+        p_store_group<EPI, NWV, PM>(g, acc, T, wm, wn, r, h,
+                                    reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
 #else
-      if (acc[0][0][0] == 1234.5f) g.C[tid] = acc[1][1][3] + acc[0][1][2] + acc[1][0][1];
+      if (acc[0][0][0] == 1234.5f) g.C[tid] = acc[WI - 1][1][3] + acc[0][1][2] + acc[WI - 1][0][1];
 #endif
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
       for (int j = 0; j < WJ; ++j)
 #pragma unroll
@@ -489,10 +507,10 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 #ifndef X3P_NO_EPI
 #pragma unroll
     for (int gi = 0; gi < X::GROUPS; ++gi)
-      p_store_group<EPI, NWV>(g, pend, Tp, wm, wn, r, h,
-                              reinterpret_cast<const float*>(plds + OFF_BIAS + ((ntiles - 1) % 3) * 1024), gi);
+      p_store_group<EPI, NWV, PM>(g, pend, Tp, wm, wn, r, h,
+                                  reinterpret_cast<const float*>(plds + OFF_BIAS + ((ntiles - 1) % 3) * 1024), gi);
 #else
-    if (pend[0][0][0] == 1234.5f) g.C[tid] = pend[1][1][3] + pend[0][1][2] + pend[1][0][1];
+    if (pend[0][0][0] == 1234.5f) g.C[tid] = pend[WI - 1][1][3] + pend[0][1][2] + pend[WI - 1][0][1];
 #endif
   }
 }
@@ -500,24 +518,38 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 typedef void (*x3p_fn)(PArgs);
 
 // [epilogue (PLAIN, BIAS_ELU)][KBT index: 0 (runtime K), 4, 8, 16]
-template <int NWV>
+template <int NWV, int PM>
 struct X3PTable {
   static constexpr x3p_fn k[2][4] = {
-      {&gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 0, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 4, NWV>,
-       &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 16, NWV>},
-      {&gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 0, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 4, NWV>,
-       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV>}};
+      {&gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 4, NWV, PM>,
+       &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 16, NWV, PM>},
+      {&gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 4, NWV, PM>,
+       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV, PM>}};
 };
 
-template <int NWV>
+template <int NWV, int PM>
 bool x3p_attrs() {
   bool ok = true;
-  for (const auto& row : X3PTable<NWV>::k)
+  for (const auto& row : X3PTable<NWV, PM>::k)
     for (x3p_fn f : row)
       if (f)
         ok &= hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  P_LDS) == hipSuccess;
+                                  XC<NWV, PM>::P_LDS) == hipSuccess;
   return ok;
+}
+
+// Tile height: 256 rows, or 128 (8 waves) when that fills the CUs' rounds better: cost = rounds of
+// persistent tiles x tile time, a half tile measured 0.55-0.62 of a full one (e.g. the 512 -> 256 layer
+// at M = 24576: 384 full tiles = 2 rounds on 256 CUs, 768 half tiles = 3 rounds of 0.6: 100 -> 93 us).
+// LGX_GEMM_X3P_PM=128 / 256 forces one (A/B switch).
+int pick_pm(int64_t M, int ntn, int batch, int cus, int nwv) {
+  const char* e = getenv("LGX_GEMM_X3P_PM");   // (read per call: tests switch it)
+  const int forced = e ? atoi(e) : 0;
+  if (nwv != 8) return 256;
+  if (forced == 128 || forced == 256) return forced;
+  const int64_t t256 = (M + 255) / 256 * ntn * batch, t128 = (M + 127) / 128 * ntn * batch;
+  const double c256 = (double)((t256 + cus - 1) / cus), c128 = 0.6 * (double)((t128 + cus - 1) / cus);
+  return c128 < c256 ? 128 : 256;
 }
 
 }  // namespace
@@ -543,9 +575,6 @@ int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
   g.Y = a.Y;
   g.partials = a.partials;
   g.ntn = a.N / PN;
-  const int64_t tiles = ((a.M + PM - 1) / PM) * g.ntn * a.batch;
-  if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too many tiles");
-  g.tiles = (int32_t)tiles;
   if (((uintptr_t)a.Bs & 15) || a.M * a.lda * 4 >= (1ll << 32))
     return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: pre-split B must be 16-byte aligned; A < 4 GB per batch entry");
   // K = 128 / 256 / 512 (the PPO-update layers): the k loop unrolled, BIAS_ELU / PLAIN epilogue
@@ -559,15 +588,21 @@ int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
     const char* e = getenv("LGX_GEMM_X3P_WAVES");
     return e && atoi(e) == 4 ? 4 : 8;
   }();
-  static const bool attrs = x3p_attrs<4>() && x3p_attrs<8>();
+  static const bool attrs = x3p_attrs<4, 256>() && x3p_attrs<8, 256>() && x3p_attrs<8, 128>();
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_nt: hipFuncSetAttribute (dynamic LDS) failed");
   if (a.epi == LGX_GEMM_DELU_COLSUM) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt_x3p: no column-sum epilogue");
+  const int pm = pick_pm(a.M, g.ntn, a.batch, cus, nwv);
+  const int64_t tiles = ((a.M + pm - 1) / pm) * g.ntn * a.batch;
+  if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too many tiles");
+  g.tiles = (int32_t)tiles;
   const int kbt = (defer && (g.kb == 4 || g.kb == 8 || g.kb == 16)) ? g.kb : 0;
   const int ki = kbt == 0 ? 0 : kbt == 4 ? 1 : kbt == 8 ? 2 : 3;
-  const x3p_fn f = nwv == 8 ? X3PTable<8>::k[a.epi][ki] : X3PTable<4>::k[a.epi][ki];
+  const x3p_fn f = nwv == 4 ? X3PTable<4, 256>::k[a.epi][ki]
+                 : pm == 128 ? X3PTable<8, 128>::k[a.epi][ki] : X3PTable<8, 256>::k[a.epi][ki];
+  const int lds = nwv == 8 && pm == 128 ? XC<8, 128>::P_LDS : XC<8, 256>::P_LDS;
   // persistent: one workgroup per CU, a multiple of 8 (XCD tile ranges)
   const int64_t per_xcd = (g.tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
-  LGX_LAUNCH(f, dim3((unsigned)wgs), dim3(64 * nwv), P_LDS, stream, g);
+  LGX_LAUNCH(f, dim3((unsigned)wgs), dim3(64 * nwv), lds, stream, g);
   return lgx_hip_status("lgx_gemm_nt");
 }

@@ -390,6 +390,213 @@ head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, c
   }
 }
 
+// ---------------------------------------------------------------------------------------- loss + head bwd
+// lgx_ppo_loss_bwd: ppo_loss_kernel<true> and head_bwd_kernel of LB_ROWS rows per workgroup in
+// ONE launch.  The rows' last hidden activations of both networks are read from HBM once into LDS
+// (row stride H + 4 floats), then
+//   1. output layers: LB_LPR lanes per row dot interleaved float4 columns against the head
+//      weights (LDS broadcasts), combined across the row's lanes by xor shuffles;
+//   2. loss and its gradient per row: the row's lanes take actions j = q, q + LB_LPR, ...
+//      (log-prob / KL partials combined by shuffles), dMU / dV into LDS, loss partials per
+//      workgroup (fixed-order row sums, same layout as ppo_loss_kernel's);
+//   3. output-layer backward (thread = (net, column)): dZ3 = (dMU W4a | dV w4c) * elu'(A3) over
+//      head_in in place, dW4 and db3 partials per workgroup (head_bwd_kernel's layout).
+// The loss finalize (d std, head-bias gradients, KL, stats, adaptive LR) runs later on one extra
+// workgroup of lgx_reduce_slices_finalize (it needs every workgroup's partials).
+constexpr int LB_ROWS = 32;
+constexpr int LB_LPR = TPB / LB_ROWS;   // lanes per row in phases 1-2 (8)
+
+__device__ __forceinline__ float lb_rowsum(float v) {   // sum over the LB_LPR lanes of a row
+#pragma unroll
+  for (int m = 1; m < LB_LPR; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+template <int MAXA>
+__global__ void __launch_bounds__(TPB)
+ppo_loss_bwd_kernel(lgx_ppo_loss_args a, float* __restrict__ hparts) {
+  constexpr int JQ = (MAXA + LB_LPR - 1) / LB_LPR;   // actions per lane
+  constexpr int DS = ((MAXA + 1 + 3) / 4) * 4;      // dMU row (+ dV), 16-byte LDS reads
+  const int A = a.num_actions, H = a.hidden, H4 = H >> 2, HS = H + 4;
+  const int NP = 2 * A + 4;
+  extern __shared__ float4 lb_dyn[];
+  float* ylds = reinterpret_cast<float*>(lb_dyn);            // [2][LB_ROWS][HS]
+  float* wlds = ylds + 2 * LB_ROWS * HS;                      // [A + 1][H]: W4a rows, then w4c
+  __shared__ __align__(16) float dmu[LB_ROWS][DS];
+  __shared__ float red[LB_ROWS][2 * MAXA + 4 + 1];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * LB_ROWS;
+  const int nr = (int)min((int64_t)LB_ROWS, a.rows - r0);
+  float* A3 = const_cast<float*>(a.head_in);
+  // ---- stage the rows (rows past M as zeros) and the head weights
+  for (int i = t; i < 2 * LB_ROWS * H4; i += TPB) {
+    const int nrow = i / H4, c4 = i - nrow * H4;              // nrow = net * LB_ROWS + row
+    const int net = nrow >= LB_ROWS, rr = nrow - net * LB_ROWS;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (rr < nr) v = reinterpret_cast<const float4*>(A3 + ((int64_t)net * a.rows + r0 + rr) * H)[c4];
+    *reinterpret_cast<float4*>(ylds + nrow * HS + 4 * c4) = v;
+  }
+  for (int i = t; i < (A + 1) * H4; i += TPB)
+    reinterpret_cast<float4*>(wlds)[i] = i < A * H4 ? reinterpret_cast<const float4*>(a.W4a)[i]
+                                                    : reinterpret_cast<const float4*>(a.W4c)[i - A * H4];
+  __syncthreads();
+  // ---- 1. output layers
+  const int rr = t / LB_LPR, q = t % LB_LPR;
+  float hv[MAXA + 1];
+#pragma unroll
+  for (int j = 0; j <= MAXA; ++j) hv[j] = 0.f;
+  {
+    const float* ya = ylds + rr * HS;
+    const float* yc = ylds + (LB_ROWS + rr) * HS;
+    const float4* w4 = reinterpret_cast<const float4*>(wlds);
+    for (int c4 = q; c4 < H4; c4 += LB_LPR) {
+      const float4 x = *reinterpret_cast<const float4*>(ya + 4 * c4);
+      const float4 y = *reinterpret_cast<const float4*>(yc + 4 * c4);
+#pragma unroll
+      for (int j = 0; j < MAXA; ++j)
+        if (j < A) {
+          const float4 w = w4[j * H4 + c4];
+          hv[j] += x.x * w.x + x.y * w.y + x.z * w.z + x.w * w.w;
+        }
+      const float4 w = w4[A * H4 + c4];
+      hv[MAXA] += y.x * w.x + y.y * w.y + y.z * w.z + y.w * w.w;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j <= MAXA; ++j) hv[j] = lb_rowsum(hv[j]);
+  // ---- 2. loss per row (lane q: actions q + LB_LPR m)
+  float* my = red[rr];
+  const bool valid = rr < nr;
+  {
+    const int64_t r = r0 + rr;
+    const int64_t g = valid ? (a.idx ? a.idx[r] : r) : 0;
+    const float invM = 1.0f / (float)a.rows;
+    const float half_log_2pi = 0.91893853320467274178f;
+    float mu[JQ], sd[JQ], act[JQ];
+    float logp = 0.f, kl = 0.f;
+#pragma unroll
+    for (int m = 0; m < JQ; ++m) {
+      const int j = q + LB_LPR * m;
+      float h = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < MAXA; ++jj) h = jj == j ? hv[jj] : h;
+      mu[m] = sd[m] = 1.f;
+      act[m] = 0.f;
+      if (valid && j < A) {
+        mu[m] = h + a.b4a[j];
+        sd[m] = a.std[j];
+        act[m] = a.actions[g * A + j];
+        const float var = sd[m] * sd[m];
+        const float d = act[m] - mu[m];
+        logp += -(d * d) / (2.f * var) - logf(sd[m]) - half_log_2pi;
+        const float so = a.old_sigma[g * A + j], mo = a.old_mu[g * A + j];
+        kl += logf(sd[m] / so + 1.e-5f) + (so * so + (mo - mu[m]) * (mo - mu[m])) / (2.f * var) - 0.5f;
+      }
+    }
+    logp = lb_rowsum(logp);
+    kl = lb_rowsum(kl);
+    float dlogp = 0.f, surr = 0.f, vl = 0.f, dv = 0.f;
+    if (valid) {
+      const float adv = a.advantages[g];
+      const float ratio = expf(logp - a.old_logp[g]);
+      const float lo = 1.f - a.clip_param, hi = 1.f + a.clip_param;
+      const float rc = fminf(fmaxf(ratio, lo), hi);
+      const float s1 = -adv * ratio, s2 = -adv * rc;
+      const bool inside = ratio >= lo && ratio <= hi;
+      float dsdr;   // torch.maximum backward: ties split the gradient; clamp passes it inside [lo, hi]
+      if (s1 > s2) dsdr = -adv;
+      else if (s1 < s2) dsdr = inside ? -adv : 0.f;
+      else dsdr = 0.5f * (-adv) + 0.5f * (inside ? -adv : 0.f);
+      surr = fmaxf(s1, s2);
+      dlogp = dsdr * invM * ratio;
+      const float v = hv[MAXA] + a.b4c[0];
+      const float tv = a.target_values[g], ret = a.returns[g];
+      if (a.use_clipped_value_loss) {
+        const float dvt = v - tv;
+        const float vc = tv + fminf(fmaxf(dvt, -a.clip_param), a.clip_param);
+        const bool vin = dvt >= -a.clip_param && dvt <= a.clip_param;
+        const float u1 = (v - ret) * (v - ret), u2 = (vc - ret) * (vc - ret);
+        vl = fmaxf(u1, u2);
+        const float g1 = 2.f * (v - ret), g2 = vin ? 2.f * (vc - ret) : 0.f;
+        dv = u1 > u2 ? g1 : (u1 < u2 ? g2 : 0.5f * g1 + 0.5f * g2);
+      } else {
+        vl = (ret - v) * (ret - v);
+        dv = 2.f * (v - ret);
+      }
+      dv *= a.value_loss_coef * invM;
+    }
+#pragma unroll
+    for (int m = 0; m < JQ; ++m) {
+      const int j = q + LB_LPR * m;
+      if (j < A) {
+        const float var = sd[m] * sd[m];
+        const float d = act[m] - mu[m];
+        const float dm = valid ? dlogp * d / var : 0.f;
+        dmu[rr][j] = dm;
+        my[A + j] = dm;
+        my[j] = valid ? dlogp * (d * d / (var * sd[m]) - 1.f / sd[m]) : 0.f;
+      }
+    }
+    if (q == 0) {
+      dmu[rr][A] = dv;
+      my[2 * A] = dv;
+      my[2 * A + 1] = valid ? kl : 0.f;
+      my[2 * A + 2] = surr;
+      my[2 * A + 3] = vl;
+    }
+  }
+  __syncthreads();
+  if (t < NP) {   // loss partials of this workgroup (rows in order)
+    float s = 0.f;
+    for (int i = 0; i < LB_ROWS; ++i) s += red[i][t];
+    a.partials[(int64_t)blockIdx.x * NP + t] = s;
+  }
+  // ---- 3. output-layer backward (as head_bwd_kernel; A3 rows from LDS)
+  float* P = hparts + (int64_t)blockIdx.x * ((A + 1) * H + 2 * H);
+  for (int o = t; o < 2 * H; o += TPB) {
+    const int net = o >= H, c = o - net * H;
+    const int nj = net == 0 ? A : 1;
+    float w[MAXA], acc[MAXA];
+#pragma unroll
+    for (int j = 0; j < MAXA; ++j) {
+      w[j] = j < nj ? wlds[(net == 0 ? j : A) * H + c] : 0.f;
+      acc[j] = 0.f;
+    }
+    const float* ycol = ylds + net * LB_ROWS * HS + c;
+    float* col = A3 + ((int64_t)net * a.rows + r0) * H + c;
+    float cs = 0.f;
+    for (int i = 0; i < nr; ++i) {
+      const float y = ycol[i * HS];
+      float drow[DS];
+#pragma unroll
+      for (int u = 0; u < DS / 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(&dmu[i][4 * u]);
+        drow[4 * u] = v.x; drow[4 * u + 1] = v.y; drow[4 * u + 2] = v.z; drow[4 * u + 3] = v.w;
+      }
+      float dA = 0.f;
+      if (net == 0) {
+#pragma unroll
+        for (int j = 0; j < MAXA; ++j)
+          if (j < nj) { acc[j] += drow[j] * y; dA += drow[j] * w[j]; }
+      } else {
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j <= MAXA; ++j) d = (j == A) ? drow[j] : d;   // dV column
+        acc[0] += d * y;
+        dA = d * w[0];
+      }
+      const float dz = dA * elu_grad_from_out(y);
+      col[(int64_t)i * H] = dz;
+      cs += dz;
+    }
+    const int jo = net == 0 ? 0 : A;
+#pragma unroll
+    for (int j = 0; j < MAXA; ++j)
+      if (j < nj) P[(jo + j) * H + c] = acc[j];
+    P[(A + 1) * H + o] = cs;
+  }
+}
+
 // ---------------------------------------------------------------------------------------- elu bwd
 // dA [nets, rows, H] -> dZ = dA * elu'(Y) in place; partial column sums per 64-row chunk:
 // partials[chunk][net*H + c].  Thread = 4 consecutive columns (16-B loads and stores).
@@ -448,10 +655,16 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
 // partials) run on float4 lanes (tile_outputs < 0: -4 x 64 outputs per workgroup, 64 lanes x 4
 // slice groups), the rest on scalar lanes.
 __global__ void __launch_bounds__(TPB)
-reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs) {
+reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin, int32_t fin_blocks) {
+  // workgroup 0: the deferred loss finalize of lgx_ppo_loss_bwd (first, so its serial partial
+  // sums overlap the reduction tiles instead of trailing them)
+  if (fin_blocks > 0 && blockIdx.x == 0) {
+    loss_finalize(fin, fin_blocks);
+    return;
+  }
   __shared__ float red[TPB];
   __shared__ float4 red4[TPB];
-  int b = blockIdx.x, ji = 0;
+  int b = blockIdx.x - (fin_blocks > 0 ? 1 : 0), ji = 0;
   while (ji + 1 < njobs && b >= jobs.tile_start[ji + 1]) ++ji;
   const lgx_reduce_job& jb = jobs.job[ji];
   const int ot = jobs.tile_outputs[ji];
@@ -734,6 +947,47 @@ extern "C" int lgx_head_bwd_finalize(const lgx_ppo_loss_args* loss, const float*
   return head_bwd_launch(loss, d_mu, d_v, W4a, W4c, A3, rows, num_actions, hidden, partials, stream);
 }
 
+extern "C" int lgx_ppo_loss_bwd_layout(int64_t rows, int32_t num_actions, int32_t hidden, int64_t* out) {
+  if (!out || rows <= 0 || num_actions <= 0 || num_actions > LGX_PPO_MAX_ACTIONS || hidden <= 0)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_loss_bwd_layout: bad args");
+  const int64_t blocks = (rows + LB_ROWS - 1) / LB_ROWS;
+  out[0] = blocks * (2 * (int64_t)num_actions + 4);
+  out[1] = blocks * ((int64_t)(num_actions + 1) * hidden + 2 * (int64_t)hidden);
+  out[2] = (int64_t)(2 * LB_ROWS * (hidden + 4) + (num_actions + 1) * hidden) * (int64_t)sizeof(float);
+  return LGX_OK;
+}
+
+extern "C" int lgx_ppo_loss_bwd(const lgx_ppo_loss_args* args, float* head_partials, void* stream) {
+  if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_loss_bwd: null args");
+  const lgx_ppo_loss_args& a = *args;
+  if (a.rows <= 0 || a.num_actions <= 0 || a.num_actions > LGX_PPO_MAX_ACTIONS || !a.b4a || !a.b4c || !a.std ||
+      !a.actions || !a.old_logp || !a.old_mu || !a.old_sigma || !a.advantages || !a.target_values || !a.returns ||
+      !a.partials || !a.g_std || !a.g_b4a || !a.g_b4c || !a.stats || !head_partials)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_loss_bwd: bad args");
+  if (!a.head_in || !a.W4a || !a.W4c || a.hidden <= 0 || a.hidden % 16)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_loss_bwd: head_in / W4a / W4c required, hidden % 16 == 0");
+  int64_t lay[3];
+  lgx_ppo_loss_bwd_layout(a.rows, a.num_actions, a.hidden, lay);
+  if (lay[2] > 96 * 1024) return lgx_fail(LGX_EINVAL, "lgx_ppo_loss_bwd: hidden too wide for the LDS row stage");
+  static const bool attr_ok = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_loss_bwd_kernel<12>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
+           hipFuncSetAttribute(reinterpret_cast<const void*>(&ppo_loss_bwd_kernel<LGX_PPO_MAX_ACTIONS>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
+  }();
+  if (!attr_ok) return lgx_fail(LGX_EHIP, "lgx_ppo_loss_bwd: hipFuncSetAttribute failed");
+  const int blocks = (int)((a.rows + LB_ROWS - 1) / LB_ROWS);
+  if (a.num_actions <= 12)
+    hipLaunchKernelGGL(ppo_loss_bwd_kernel<12>, dim3(blocks), dim3(TPB), (size_t)lay[2], LGX_STREAM(stream), a,
+                       head_partials);
+  else
+    hipLaunchKernelGGL(ppo_loss_bwd_kernel<LGX_PPO_MAX_ACTIONS>, dim3(blocks), dim3(TPB), (size_t)lay[2],
+                       LGX_STREAM(stream), a, head_partials);
+  if (!a.defer_finalize)
+    hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
+  return lgx_hip_status("lgx_ppo_loss_bwd");
+}
+
 extern "C" int64_t lgx_colsum_partials_floats(int64_t rows, int32_t hidden, int32_t nets) {
   return ((rows + CHUNK - 1) / CHUNK) * (int64_t)hidden * nets;
 }
@@ -748,7 +1002,8 @@ extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32
   return lgx_hip_status("lgx_elu_bwd_colsum");
 }
 
-extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream) {
+static int reduce_slices_launch(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* fin,
+                                void* stream) {
   if (!jobs || njobs <= 0 || njobs > LGX_MAX_REDUCE_JOBS) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job count");
   lgx_reduce_jobs J;
   int64_t tiles = 0;
@@ -765,8 +1020,27 @@ extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void
     tiles += ((int64_t)j.count * j.n + per - 1) / per;
   }
   if (tiles > (1 << 30)) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: too large");
-  hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs);
+  lgx_ppo_loss_args f{};
+  int32_t fin_blocks = 0;
+  if (fin) {
+    f = *fin;
+    fin_blocks = (int32_t)((f.rows + LB_ROWS - 1) / LB_ROWS);
+    tiles += 1;
+  }
+  hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs, f,
+                     fin_blocks);
   return lgx_hip_status("lgx_reduce_slices");
+}
+
+extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream) {
+  return reduce_slices_launch(jobs, njobs, nullptr, stream);
+}
+
+extern "C" int lgx_reduce_slices_finalize(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* loss,
+                                          void* stream) {
+  if (!loss || !loss->defer_finalize || loss->rows <= 0)
+    return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_finalize: loss args must be a deferred-finalize lgx_ppo_loss_bwd call's");
+  return reduce_slices_launch(jobs, njobs, loss, stream);
 }
 
 extern "C" int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,

@@ -274,8 +274,21 @@ class FusedPPOUpdate:
               (torch.empty(Sk[0], h[0], self.num_obs, device=dev), torch.empty(Sk[0], h[0], self.num_cobs, device=dev)))
         self.P = [p0] + \
                  [torch.empty(2 * Sk[k], h[k], h[k - 1], device=dev) for k in range(1, self.L)]
-        self.loss_parts = torch.empty(int(self.lib.lgx_ppo_loss_partials_floats(M, A)), device=dev)
-        self.head_parts = torch.empty(int(self.lib.lgx_head_bwd_partials_floats(M, A, h[-1])), device=dev)
+        # output layers evaluated inside the loss call (no head GEMM launches) when they fit its LDS;
+        # with them, loss + output-layer backward in one launch (lgx_ppo_loss_bwd, its loss finalize
+        # in the reduction launch) unless LGX_PPO_LOSS_BWD=0
+        H = h[-1]
+        self.head_in_loss = (os.environ.get("LGX_PPO_HEAD_IN_LOSS", "1") != "0" and H % 16 == 0
+                             and (A + 1) * H * 4 <= 65536)
+        lay = (C.c_int64 * 3)()
+        self.check(self.lib.lgx_ppo_loss_bwd_layout(M, A, H, lay), "loss_bwd_layout")
+        self.loss_bwd = self.head_in_loss and lay[2] <= 96 * 1024 and os.environ.get("LGX_PPO_LOSS_BWD", "1") != "0"
+        if self.loss_bwd:
+            self.loss_parts = torch.empty(int(lay[0]), device=dev)
+            self.head_parts = torch.empty(int(lay[1]), device=dev)
+        else:
+            self.loss_parts = torch.empty(int(self.lib.lgx_ppo_loss_partials_floats(M, A)), device=dev)
+            self.head_parts = torch.empty(int(self.lib.lgx_head_bwd_partials_floats(M, A, H)), device=dev)
         if self.lgx_gemm:
             self.col_parts = [torch.empty(int(self.lib.lgx_gemm_partials_floats(M, hk, 2)), device=dev)
                               for hk in h[:-1]]
@@ -556,16 +569,13 @@ class FusedPPOUpdate:
         a.g_b4c = a.g_b4a + 4 * self.A
         a.g_std = self.flat_g.data_ptr() + 4 * self.std_off
         a.stats = self.stats.data_ptr()
-        # output layers evaluated inside the loss call (no head GEMM launches) when they fit its LDS
         H = self.hidden[-1]
-        self.head_in_loss = (os.environ.get("LGX_PPO_HEAD_IN_LOSS", "1") != "0" and H % 16 == 0
-                             and (self.A + 1) * H * 4 <= 65536)
-        if self.head_in_loss:
+        if self.head_in_loss:   # (decided in _alloc)
             a.head_in, a.hidden = self.Y[self.L - 1].data_ptr(), H
             a.W4a, a.W4c = self.W[self.L][0].data_ptr(), self.W[self.L][1].data_ptr()
         else:
             a.head_in, a.W4a, a.W4c, a.hidden = None, None, None, 0
-        a.defer_finalize = 1     # run by lgx_head_bwd_finalize
+        a.defer_finalize = 1     # run by lgx_head_bwd_finalize / lgx_reduce_slices_finalize
         # single process with the adaptive schedule: the loss finalize adapts the learning rate
         # (data-parallel: lgx_ppo_adapt_lr after the all-reduce the KL rides in)
         if p.desired_kl is not None and p.schedule == "adaptive" and p.dist is None:
@@ -704,12 +714,15 @@ class FusedPPOUpdate:
             torch.mm(self.Y[L - 1][1], whc.t(), out=self.V)
         # ---- loss, gradient at the heads, KL -> adaptive learning rate
         args.idx = idx.data_ptr()
-        chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
-        adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"   # (single process: in the loss call)
-        # ---- backward
-        # (+ the loss finalize on one extra workgroup of the same launch)
-        chk(lib.lgx_head_bwd_finalize(C.byref(args), _vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc),
-                                      _vp(self.Y[L - 1]), M, A, h[-1], _vp(self.head_parts), stream), "head_bwd")
+        adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"   # (single process: in the loss finalize)
+        if self.loss_bwd:
+            # loss + output-layer backward in one launch (dZ3 over Y[L-1]); finalize in the reduction
+            chk(lib.lgx_ppo_loss_bwd(C.byref(args), _vp(self.head_parts), stream), "lgx_ppo_loss_bwd")
+        else:
+            chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
+            # ---- backward (+ the loss finalize on one extra workgroup of the same launch)
+            chk(lib.lgx_head_bwd_finalize(C.byref(args), _vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc),
+                                          _vp(self.Y[L - 1]), M, A, h[-1], _vp(self.head_parts), stream), "head_bwd")
         dZ = self.Y[L - 1]                           # dZ of the last hidden layer (in place)
         for k in range(L - 1, 0, -1):
             # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
@@ -740,7 +753,10 @@ class FusedPPOUpdate:
         else:
             torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
             torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
-        chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
+        if self.loss_bwd:
+            chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
+        else:
+            chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
         if not apply:
             return
         grad_scale = 1.0

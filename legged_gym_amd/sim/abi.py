@@ -193,6 +193,9 @@ def declare(lib, prefix="lgx"):
             "colsum_partials_floats": (i64, [i64, i32, i32]),
             "elu_bwd_colsum": (C.c_int, [vp, vp, i64, i32, i32, vp, vp]),
             "reduce_slices": (C.c_int, [C.POINTER(LgxReduceJob), i32, vp]),
+            "reduce_slices_finalize": (C.c_int, [C.POINTER(LgxReduceJob), i32, C.POINTER(LgxPpoLossArgs), vp]),
+            "ppo_loss_bwd_layout": (C.c_int, [i64, i32, i32, C.POINTER(i64)]),
+            "ppo_loss_bwd": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp, vp]),
             "gemm_partials_floats": (i64, [i64, i32, i32]),
             "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
             "gemm_tn": (C.c_int, [C.POINTER(LgxGemmTnArgs), vp]),
@@ -219,7 +222,7 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
-            "lgx_reduce_slices", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
+            "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn"]
 

@@ -135,6 +135,18 @@ def test_gemm_presplit_update_shape(gpu, epi):
          presplit=True)
 
 
+@pytest.mark.parametrize("pm", [128, 256])
+@pytest.mark.parametrize("M,N,K", [(24576, 256, 512), (4096, 512, 256), (300, 128, 256), (513, 256, 128),
+                                   (1000, 128, 96), (1, 128, 32)])
+def test_gemm_presplit_tile_heights(gpu, monkeypatch, pm, M, N, K):
+    """The pipelined kernel with 256-row tiles and with 128-row half tiles (chosen when they fill the
+    CUs' rounds better, forced here with LGX_GEMM_X3P_PM): unrolled K 512 / 256 / 128 with the
+    deferred epilogue, runtime K 96, ragged M, one row."""
+    monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
+    for epi in (abi.GEMM_PLAIN, abi.GEMM_BIAS_ELU):
+        _run(M, N, K, 2, epi, seed=M + K + pm, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+
+
 @pytest.mark.parametrize("transpose", [False, True])
 def test_split_bf16_limbs(gpu, transpose):
     """lgx_split_bf16: limbs are RNE bf16 (x0 = bf16(x), |x1| <= 2^-8|x0|, |x2| <= 2^-8|x1|),

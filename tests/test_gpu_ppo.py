@@ -85,10 +85,44 @@ def test_fused_minibatch_gradient_matches_autograd(gpu):
     idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
     gref = autograd_grads(ref, idx)
     fus._fused.gradients(idx)
+    assert fus._fused.loss_bwd      # loss + output-layer backward in one launch (lgx_ppo_loss_bwd)
     for n, p in fus.actor_critic.named_parameters():
         a, b = p.grad, gref[n]
         tol = 1e-5 + 2e-3 * b.abs()
         assert ((a - b).abs() <= tol).all(), (n, (a - b).abs().max().item(), b.abs().max().item())
+
+
+@pytest.mark.parametrize("rows", [1000, 37])
+def test_fused_minibatch_gradient_ragged_rows(gpu, rows):
+    """Minibatches whose row count is not a multiple of the 32-row loss / head-backward chunk."""
+    ref, fus = make_pair()
+    idx = torch.randperm(T * N, device="cuda:0")[:rows]
+    gref = autograd_grads(ref, idx)
+    fus._fused.gradients(idx)
+    for n, p in fus.actor_critic.named_parameters():
+        a, b = p.grad, gref[n]
+        assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), (rows, n, (a - b).abs().max().item())
+
+
+def test_fused_minibatch_gradient_separate_loss_and_head(gpu, monkeypatch):
+    """lgx_ppo_loss + lgx_head_bwd_finalize as two launches (LGX_PPO_LOSS_BWD=0) instead of
+    lgx_ppo_loss_bwd: minibatch gradient and a full update against autograd."""
+    monkeypatch.setenv("LGX_PPO_LOSS_BWD", "0")
+    ref, fus = make_pair()
+    idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
+    gref = autograd_grads(ref, idx)
+    fus._fused.gradients(idx)
+    assert not fus._fused.loss_bwd
+    for n, p in fus.actor_critic.named_parameters():
+        a, b = p.grad, gref[n]
+        assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), n
+    ref, fus = make_pair()
+    torch.manual_seed(11)
+    vl_r, sl_r = ref.update()
+    torch.manual_seed(11)
+    vl_f, sl_f = fus.update()
+    assert fus.learning_rate == ref.learning_rate
+    assert abs(vl_f - vl_r) <= 1e-4 * abs(vl_r) + 1e-6 and abs(sl_f - sl_r) <= 1e-4 * abs(sl_r) + 1e-6
 
 
 @pytest.mark.parametrize("mode", ["auto", "lib", "f32"])
