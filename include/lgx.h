@@ -201,8 +201,8 @@ int lgx_version(void);
 /* sizeof(lgx_model), sizeof(lgx_env_params), sizeof(lgx_buffers), sizeof(lgx_mlp_desc),
  * sizeof(lgx_ppo_loss_args), sizeof(lgx_reduce_job), sizeof(lgx_ppo_act_args),
  * sizeof(lgx_ppo_store_args), sizeof(lgx_gemm_args), sizeof(lgx_copy2d_job),
- * sizeof(lgx_gemm_tn_args): lets bindings verify layout */
-void lgx_struct_sizes(int64_t out[11]);
+ * sizeof(lgx_gemm_tn_args), sizeof(lgx_mlp_x3_desc): lets bindings verify layout */
+void lgx_struct_sizes(int64_t out[12]);
 
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
@@ -289,6 +289,27 @@ typedef struct lgx_mlp_desc {
   const float* biases[6];
 } lgx_mlp_desc;
 int lgx_mlp_forward_batch(const lgx_mlp_desc* descs, int32_t count, void* stream);
+
+/* The same MLP forward (rows-in-LDS fusion of every layer, one or two networks per launch) on
+ * split-bf16 MFMA products (f32-accurate, as lgx_gemm_nt's split-bf16 path): the rollout's
+ * actor / critic inference (rsl_rl ActorCritic.act / evaluate).  weights[l] = lgx_mlp_x3_split
+ * image of layer l's nn.Linear weight [dims[l+1]][dims[l]] (lgx_mlp_x3_weight_elems bf16,
+ * 16-byte aligned); dims <= 512; the activations of 32 rows must fit the LDS
+ * (lgx_mlp_x3_lds_bytes >= 0). */
+typedef struct lgx_mlp_x3_desc {
+  const float* x;
+  float* y;
+  int64_t rows;
+  int32_t nl;
+  int32_t act;                  /* 1 ELU, 2 tanh (hidden layers; the last layer is linear) */
+  int32_t dims[7];
+  const uint16_t* weights[6];
+  const float* biases[6];
+} lgx_mlp_x3_desc;
+int64_t lgx_mlp_x3_weight_elems(int32_t n_out, int32_t k_in);
+int lgx_mlp_x3_split(const float* W, int32_t n_out, int32_t k_in, uint16_t* dst, void* stream);
+int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* descs, int32_t count);   /* -1: unsupported */
+int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* descs, int32_t count, void* stream);
 
 /* In-library kernel timing for the measurement harness (bench.py): with `period` = k > 0, every
  * k-th lgx_step dispatches its kernels through hipExtLaunchKernelGGL with a (start, stop)

@@ -77,7 +77,7 @@ extern "C" {
 const char* lgx_last_error(void) { return g_err.c_str(); }
 int lgx_version(void) { return 1; }
 
-void lgx_struct_sizes(int64_t out[11]) {
+void lgx_struct_sizes(int64_t out[12]) {
   out[0] = (int64_t)sizeof(lgx_model);
   out[1] = (int64_t)sizeof(lgx_env_params);
   out[2] = (int64_t)sizeof(lgx_buffers);
@@ -89,6 +89,7 @@ void lgx_struct_sizes(int64_t out[11]) {
   out[8] = (int64_t)sizeof(lgx_gemm_args);
   out[9] = (int64_t)sizeof(lgx_copy2d_job);
   out[10] = (int64_t)sizeof(lgx_gemm_tn_args);
+  out[11] = (int64_t)sizeof(lgx_mlp_x3_desc);
 }
 
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms) {

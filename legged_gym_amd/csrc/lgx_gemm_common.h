@@ -37,7 +37,7 @@ struct GemmArgs {
   const uint16_t* Bs;   // split-bf16 path: B pre-split into bf16 limbs (or null)
 };
 
-__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : __expf(x) - 1.f; }  // v_exp_f32
+__device__ __forceinline__ float elu_f(float x) { return lgx_elu(x); }
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }

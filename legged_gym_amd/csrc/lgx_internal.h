@@ -88,3 +88,12 @@ struct lgx_reduce_jobs {
 #define LGX_ENV_BLOCK 16  // envs per post-physics workgroup (16 lanes each)
 #endif
 #define LGX_PARTIAL_STRIDE (LGX_MAX_TERMS + 2)
+
+#ifdef __HIPCC__
+// ELU (alpha 1) of the policy networks: exp(x) - 1 on v_exp_f32 for x <= 0.  Absolute error
+// <= ~1.2e-7 against torch's expm1 (a few ulp of 1; relative error grows only where the output
+// is tiny, |x| < 2^-8); libm's expm1f costs ~10x more VALU, which in the GEMM epilogues competes
+// with the operand splits for the MFMA issue gaps (measured: layer-1 forward 54 -> 61 us with
+// an expm1-accurate polynomial form).
+__device__ __forceinline__ float lgx_elu(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+#endif

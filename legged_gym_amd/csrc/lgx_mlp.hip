@@ -54,7 +54,7 @@ struct MlpBatch {
 };
 
 LGX_DEV float activate(float x, int act) {
-  if (act == 1) return x > 0.f ? x : expm1f(x);
+  if (act == 1) return lgx_elu(x);
   if (act == 2) return tanhf(x);
   return x;
 }

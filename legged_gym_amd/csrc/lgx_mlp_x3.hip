@@ -1,0 +1,332 @@
+// Fused MLP forward on split-bf16 MFMA for the rollout's actor and critic (rsl_rl
+// ActorCritic.act / evaluate, obs-512-256-128-{12,1} with ELU: the per-env-step policy
+// inference of OnPolicyRunner.learn's rollout loop), both networks in ONE launch (blockIdx.y).
+// Same arithmetic as the PPO-update GEMMs (lgx_gemm_split.hip): every f32 operand as three RNE
+// bf16 limbs, the six limb products of order <= 2 on v_mfma_f32_32x32x16_bf16 with f32
+// accumulation (f32-accurate); 2.67x the product rate of lgx_mlp_forward_kernel's f32 MFMA.
+//
+//   * 32 rows per workgroup, 8 waves.  The rows' activations stay in LDS across all layers as
+//     bf16 limb images [limb][32 rows][Kp] (Kp = width rounded up to 64, 16-byte row pad), split
+//     once by their producer (the input staging or the previous layer's epilogue), so the MFMA
+//     operand reads are plain ds_read_b128 with no per-fragment split;
+//   * weights pre-split (lgx_mlp_x3_split, once per parameter version) into the fragment image
+//     [n / 32][k / 16][limb][32 n][16 k]: each wave-load of a fragment limb is 1 KB contiguous,
+//     streamed from L2 (a network's limbs are 1.7 MB) with a double-buffered group of k blocks in
+//     flight ahead of the MFMAs;
+//   * wave w owns output column blocks w, w + 8, ...; the weights are the MFMA's first operand,
+//     which leaves each lane four runs of 4 consecutive output columns of one row: bias + ELU +
+//     split into 8-byte stores of the next layer's limb image (last layer: f32 rows to HBM).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "lgx_device.h"
+#include "lgx_internal.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float fx2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int XM_BM = 32;           // rows per workgroup
+constexpr int XM_NW = 8;            // waves per workgroup
+constexpr int XM_NT = 64 * XM_NW;
+constexpr int XM_MAXL = 6;
+constexpr int XM_MAXW = 512;
+constexpr int XM_LDS_MAX = 160 * 1024;
+
+__host__ __device__ inline int xm_kp(int k) { return (k + 63) & ~63; }         // padded width (image / weight K)
+__host__ __device__ inline int xm_rs(int k) { return xm_kp(k) * 2 + 16; }       // image row stride, bytes
+__host__ __device__ inline int xm_img(int k) { return 3 * XM_BM * xm_rs(k); }   // limb image bytes
+
+struct XmNet {
+  const float* x;
+  float* y;
+  int64_t rows;
+  int32_t nl, act;
+  int32_t dims[XM_MAXL + 1];
+  const uint16_t* w[XM_MAXL];
+  const float* b[XM_MAXL];
+};
+struct XmBatch {
+  XmNet m[2];
+  int32_t region;   // byte offset of the second image region (the first at 0)
+};
+
+// three RNE bf16 limbs of two floats, packed (low half = first element); both subtractions exact
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
+  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){x0, x1}, bf16x2));
+  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
+  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+  r0 -= __uint_as_float(l1 << 16);
+  r1 -= __uint_as_float(l1 & 0xffff0000u);
+  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+}
+
+__device__ __forceinline__ float xm_act(float v, int act) {
+  if (act == 1) return lgx_elu(v);
+  if (act == 2) return tanhf(v);
+  return v;
+}
+
+// One layer's products for the TPW column blocks of this wave: acc[t] (+)= W[cb_t] . X over KB
+// k blocks of 16 (KB % 4 == 0).  G k blocks per load group, two groups of B fragments in flight.
+template <int TPW>
+__device__ __forceinline__ void xm_layer(const char* __restrict__ img, int rs, const char* __restrict__ W, int KB,
+                                         int wave, int lane, f32x16 (&acc)[2]) {
+  constexpr int G = 4 / TPW;
+  const int lo = (lane & 31) * 32 + (lane >> 5) * 16;     // B fragment lane offset in a 1 KB limb block
+  const int ao = (lane & 31) * rs + (lane >> 5) * 16;     // A fragment lane offset in an image limb
+  const int limb_bytes = XM_BM * rs;
+  bf16x8 bA[G][TPW][3], bB[G][TPW][3];
+  auto load = [&](bf16x8 (&b)[G][TPW][3], int kb0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int t = 0; t < TPW; ++t)
+#pragma unroll
+        for (int l = 0; l < 3; ++l)
+          b[g][t][l] = *reinterpret_cast<const bf16x8*>(
+              W + ((int64_t)((wave + XM_NW * t) * KB + kb0 + g) * 3 + l) * 1024 + lo);
+  };
+  auto compute = [&](const bf16x8 (&b)[G][TPW][3], int kb0) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const char* pa = img + ao + (kb0 + g) * 32;
+      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(pa);
+      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(pa + limb_bytes);
+      const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(pa + 2 * limb_bytes);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        f32x16 c = acc[t];   // small limb products first
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][2], a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][1], a1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][0], a2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][1], a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][0], a1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][0], a0, c, 0, 0, 0);
+        acc[t] = c;
+      }
+    }
+  };
+  load(bA, 0);
+  for (int kb0 = 0; kb0 < KB; kb0 += 2 * G) {
+    if (kb0 + G < KB) load(bB, kb0 + G);
+    compute(bA, kb0);
+    if (kb0 + G >= KB) break;
+    if (kb0 + 2 * G < KB) load(bA, kb0 + 2 * G);
+    compute(bB, kb0 + G);
+  }
+}
+
+__global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_t count) {
+  extern __shared__ __attribute__((aligned(16))) char xm_lds[];
+  // two networks: XCDs 0-3 (workgroup id % 8) run the first, 4-7 the second, so each XCD's L2
+  // holds one network's weight limbs (1.7 MB) instead of both
+  const int b = blockIdx.x;
+  const int net = count == 2 ? (b & 7) >> 2 : 0;
+  const int64_t tile = count == 2 ? (int64_t)(b >> 3) * 4 + (b & 3) : b;
+  const XmNet& a = batch.m[net];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t r0 = tile * XM_BM;
+  if (r0 >= a.rows) return;   // (the other network of the launch may have more rows)
+  char* const img0 = xm_lds;
+  char* const img1 = xm_lds + batch.region;
+  LGX_CLK_DECL(8)
+  // ---- input rows -> limb image 0 (zero rows past M, zero columns past K0)
+  {
+    const int K0 = a.dims[0], rs = xm_rs(K0), pairs = xm_kp(K0) / 2;
+    for (int i = tid; i < XM_BM * pairs; i += XM_NT) {
+      const int row = i / pairs, k = 2 * (i - row * pairs);
+      const int64_t gr = r0 + row;
+      float v0 = 0.f, v1 = 0.f;
+      if (gr < a.rows) {
+        if (k < K0) v0 = a.x[gr * K0 + k];
+        if (k + 1 < K0) v1 = a.x[gr * K0 + k + 1];
+      }
+      uint32_t l0, l1, l2;
+      split2(v0, v1, l0, l1, l2);
+      char* p = img0 + row * rs + 2 * k;
+      *reinterpret_cast<uint32_t*>(p) = l0;
+      *reinterpret_cast<uint32_t*>(p + XM_BM * rs) = l1;
+      *reinterpret_cast<uint32_t*>(p + 2 * XM_BM * rs) = l2;
+    }
+  }
+  LGX_CLK(0);
+  __syncthreads();
+  LGX_CLK(1);
+  const int row = lane & 31, h = lane >> 5;
+  for (int l = 0; l < a.nl; ++l) {
+    const int K = a.dims[l], N = a.dims[l + 1];
+    const bool last = l == a.nl - 1;
+    const char* in = (l & 1) ? img1 : img0;
+    char* out = (l & 1) ? img0 : img1;
+    const int ncb = (N + 31) / 32;
+    const int tpw = wave < ncb ? (ncb - wave + XM_NW - 1) / XM_NW : 0;   // column blocks of this wave
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
+    const char* W = reinterpret_cast<const char*>(a.w[l]);
+    // this lane's bias values, loaded before the products so their latency hides under them
+    // (clamped index + mask: no branch, no wait inside the epilogue)
+    const float* bias = a.b[l];
+    float bv[2][4][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = (wave + XM_NW * t) * 32 + 8 * q + 4 * h + i;
+          bv[t][q][i] = bias[min(c, N - 1)];
+        }
+    if (tpw == 2) xm_layer<2>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc);
+    else if (tpw == 1) xm_layer<1>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc);
+    LGX_CLK(2 + (l < 3 ? l : 2));
+    // epilogue: lane holds row `row`, columns cb*32 + 8q + 4h + (0..3) in acc[t][4q .. 4q+3]
+    const int rs_out = xm_rs(N);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (t >= tpw) break;
+      const int cb = wave + XM_NW * t;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c0 = cb * 32 + 8 * q + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[t][4 * q + i] + (c0 + i < N ? bv[t][q][i] : 0.f);
+        if (!last) {   // padding columns: zero weights and bias -> act(0) = 0
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = xm_act(v[i], a.act);
+          uint32_t a0, a1, a2, b0, b1, b2;
+          split2(v[0], v[1], a0, a1, a2);
+          split2(v[2], v[3], b0, b1, b2);
+          char* p = out + row * rs_out + 2 * c0;
+          *reinterpret_cast<uint2*>(p) = make_uint2(a0, b0);
+          *reinterpret_cast<uint2*>(p + XM_BM * rs_out) = make_uint2(a1, b1);
+          *reinterpret_cast<uint2*>(p + 2 * XM_BM * rs_out) = make_uint2(a2, b2);
+        } else {
+          const int64_t gr = r0 + row;
+          if (gr < a.rows) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (c0 + i < N) a.y[gr * N + c0 + i] = v[i];
+          }
+        }
+      }
+    }
+    if (!last) {   // image columns past the column blocks (up to the 64-padded width) are zero
+      const int c_lo = ncb * 32, kpo = xm_kp(N);
+      const int wpairs = (kpo - c_lo) / 2;
+      for (int i = tid; i < 3 * XM_BM * wpairs; i += XM_NT) {
+        const int lr = i / wpairs, k = c_lo + 2 * (i - lr * wpairs);   // lr = limb * 32 + row
+        *reinterpret_cast<uint32_t*>(out + lr * rs_out + 2 * k) = 0u;
+      }
+    }
+    LGX_CLK(5);
+    __syncthreads();   // the output image is complete; the input region is free for the next layer
+    LGX_CLK(6);
+  }
+  LGX_CLK_PRINT("mlp_x3", 7)
+}
+
+// weights W [n_out][k_in] (nn.Linear layout) -> fragment image [n/32][k/16][limb][32 n][16 k],
+// zero-padded to 32 n and 64 k; one thread per (n, k pair)
+__global__ void __launch_bounds__(256) xm_split_kernel(const float* __restrict__ W, int N, int K,
+                                                       uint16_t* __restrict__ dst) {
+  const int KP = xm_kp(K), KB = KP / 16, pairs = KP / 2;
+  const int64_t total = (int64_t)((N + 31) / 32) * 32 * pairs;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int n = (int)(i / pairs), k = 2 * (int)(i - (int64_t)n * pairs);
+  const float v0 = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.f;
+  const float v1 = (n < N && k + 1 < K) ? W[(int64_t)n * K + k + 1] : 0.f;
+  uint32_t l0, l1, l2;
+  split2(v0, v1, l0, l1, l2);
+  const int64_t base = ((int64_t)((n >> 5) * KB + (k >> 4)) * 3) * 512 + (n & 31) * 16 + (k & 15);
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst + base);
+  d[0] = l0;
+  d[256] = l1;   // + 512 bf16 per limb
+  d[512] = l2;
+}
+
+int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region) {
+  int64_t r0 = 0, r1 = 0;
+  for (int i = 0; i < count; ++i) {
+    const lgx_mlp_x3_desc& m = d[i];
+    if (m.nl < 1 || m.nl > XM_MAXL || m.rows < 0 || m.act < 0 || m.act > 2) return -1;
+    for (int l = 0; l <= m.nl; ++l)
+      if (m.dims[l] <= 0 || m.dims[l] > XM_MAXW) return -1;
+    for (int l = 0; l < m.nl; ++l) {   // the image of width dims[l] lives in region l & 1
+      const int64_t b = xm_img(m.dims[l]);
+      if (l & 1) r1 = std::max(r1, b);
+      else r0 = std::max(r0, b);
+    }
+  }
+  if (region) *region = (int32_t)r0;
+  return r0 + r1 <= XM_LDS_MAX ? r0 + r1 : -1;
+}
+
+}  // namespace
+
+extern "C" int64_t lgx_mlp_x3_weight_elems(int32_t n_out, int32_t k_in) {
+  if (n_out <= 0 || k_in <= 0) return -1;
+  return (int64_t)((n_out + 31) / 32) * (xm_kp(k_in) / 16) * 3 * 512;
+}
+
+extern "C" int lgx_mlp_x3_split(const float* W, int32_t n_out, int32_t k_in, uint16_t* dst, void* stream) {
+  if (!W || !dst || n_out <= 0 || k_in <= 0 || n_out > XM_MAXW || k_in > XM_MAXW || ((uintptr_t)dst & 3))
+    return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_split: bad args");
+  const int64_t total = (int64_t)((n_out + 31) / 32) * 32 * (xm_kp(k_in) / 2);
+  hipLaunchKernelGGL(xm_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), W, n_out, k_in, dst);
+  return lgx_hip_status("lgx_mlp_x3_split");
+}
+
+extern "C" int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* d, int32_t count) {
+  if (!d || count < 1 || count > 2) return -1;
+  return lds_bytes(d, count, nullptr);
+}
+
+extern "C" int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* d, int32_t count, void* stream) {
+  if (!d || count < 1 || count > 2) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: count must be 1 or 2");
+  XmBatch b{};
+  const int64_t lds = lds_bytes(d, count, &b.region);
+  if (lds < 0) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: bad dims or activations exceed the LDS (160 KB)");
+  int64_t rows = 0;
+  for (int i = 0; i < count; ++i) {
+    const lgx_mlp_x3_desc& m = d[i];
+    if (!m.x || !m.y) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: null rows");
+    for (int l = 0; l < m.nl; ++l)
+      if (!m.weights[l] || !m.biases[l] || ((uintptr_t)m.weights[l] & 15))
+        return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: weight images must be 16-byte aligned (lgx_mlp_x3_split)");
+    XmNet& n = b.m[i];
+    n.x = m.x;
+    n.y = m.y;
+    n.rows = m.rows;
+    n.nl = m.nl;
+    n.act = m.act;
+    for (int l = 0; l <= m.nl; ++l) n.dims[l] = m.dims[l];
+    for (int l = 0; l < m.nl; ++l) {
+      n.w[l] = m.weights[l];
+      n.b[l] = m.biases[l];
+    }
+    rows = std::max(rows, m.rows);
+  }
+  if (rows == 0) return LGX_OK;
+  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&lgx_mlp_x3_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, XM_LDS_MAX) == hipSuccess;
+  if (!attr) return lgx_fail(LGX_EHIP, "lgx_mlp_x3_forward: hipFuncSetAttribute (dynamic LDS) failed");
+  const int64_t tiles = (rows + XM_BM - 1) / XM_BM;
+  const int64_t grid = count == 2 ? 8 * ((tiles + 3) / 4) : tiles;
+  if (grid >= (1ll << 31)) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: too many rows");
+  LGX_LAUNCH(lgx_mlp_x3_kernel, dim3((unsigned)grid), dim3(XM_NT), (size_t)lds, reinterpret_cast<hipStream_t>(stream), b,
+             count);
+  return lgx_hip_status("lgx_mlp_x3_forward");
+}

@@ -28,7 +28,7 @@ constexpr int CHUNK = 64;  // rows per workgroup in the backward epilogues
 constexpr int HEAD_CHUNK = 32;  // rows per workgroup in the output-layer backward
 constexpr int LOSS_TPB = 64;    // rows per loss workgroup (384 workgroups per 24576-row minibatch)
 
-__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+__device__ __forceinline__ float elu_f(float x) { return lgx_elu(x); }
 __device__ __forceinline__ float elu_grad_from_out(float y) { return y > 0.f ? 1.f : y + 1.f; }
 
 // rsl_rl adaptive schedule (PPO.update): lr /= 1.5 if KL > 2 kl*, *= 1.5 if 0 < KL < kl*/2,

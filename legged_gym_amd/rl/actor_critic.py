@@ -68,34 +68,63 @@ def _mlp(n_in, hidden, n_out, act):
 
 
 class _FusedMLP:
-    """Inference-only view of an nn.Sequential(Linear, act, ..., Linear) on lgx_mlp_forward."""
+    """Inference-only view of an nn.Sequential(Linear, act, ..., Linear) on the fused MLP kernels:
+    lgx_mlp_x3_forward (split-bf16 MFMA products, weights pre-split once per parameter version)
+    by default, lgx_mlp_forward_batch (f32 MFMA) with LGX_MLP_X3=0 or when the activations of
+    32 rows do not fit the LDS."""
 
     ACT = {nn.ELU: 1, nn.Tanh: 2}
 
     def __init__(self, seq):
+        import os
         self.linears = [m for m in seq if isinstance(m, nn.Linear)]
         acts = {type(m) for m in seq if not isinstance(m, nn.Linear)}
         self.act = self.ACT.get(next(iter(acts)), 0) if len(acts) == 1 else 0
         self.dims = [self.linears[0].in_features] + [l.out_features for l in self.linears]
         self.ok = self.act != 0 and max(self.dims) <= 512 and len(self.linears) <= 6
+        self.x3 = self.ok and os.environ.get("LGX_MLP_X3", "1") != "0"
         self._ver = None
-        self._wt = self._b = None
+        self._wt = self._b = self._wl = None
 
     def _refresh(self):
         ver = tuple(l.weight._version for l in self.linears) + tuple(l.bias._version for l in self.linears)
-        if ver != self._ver or self._wt is None or self._wt[0].device != self.linears[0].weight.device:
+        if ver != self._ver or self._b is None or self._b[0].device != self.linears[0].weight.device:
             with torch.no_grad():
-                self._wt = [l.weight.detach().t().contiguous() for l in self.linears]
                 self._b = [l.bias.detach().contiguous() for l in self.linears]
+                if self.x3:
+                    from legged_gym_amd.sim import lib as lgxlib
+                    lib = lgxlib.load()
+                    dev = self.linears[0].weight.device
+                    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                    if self._wl is None or self._wl[0].device != dev:
+                        self._wl = [torch.empty(int(lib.lgx_mlp_x3_weight_elems(l.out_features, l.in_features)),
+                                                dtype=torch.int16, device=dev) for l in self.linears]
+                    for l, wl in zip(self.linears, self._wl):
+                        w = l.weight.detach().contiguous()
+                        lgxlib.check(lib.lgx_mlp_x3_split(C.c_void_p(w.data_ptr()), l.out_features, l.in_features,
+                                                          C.c_void_p(wl.data_ptr()), stream), "lgx_mlp_x3_split")
+                    self._wt = None
+                else:
+                    self._wt = [l.weight.detach().t().contiguous() for l in self.linears]
             self._ver = ver
             n = len(self.linears)
             self._dims_c = (C.c_int32 * (n + 1))(*self.dims)
-            self._wp = (C.c_void_p * n)(*[t.data_ptr() for t in self._wt])
+            if self._wt is not None:
+                self._wp = (C.c_void_p * n)(*[t.data_ptr() for t in self._wt])
             self._bp = (C.c_void_p * n)(*[t.data_ptr() for t in self._b])
 
     def desc(self, x, y):
         from legged_gym_amd.sim import abi
         self._refresh()
+        if self.x3:
+            d = abi.LgxMlpX3Desc()
+            d.x, d.y, d.rows, d.nl, d.act = x.data_ptr(), y.data_ptr(), x.shape[0], len(self.linears), self.act
+            for i, v in enumerate(self.dims):
+                d.dims[i] = v
+            for i in range(len(self.linears)):
+                d.weights[i] = self._wl[i].data_ptr()
+                d.biases[i] = self._b[i].data_ptr()
+            return d
         d = abi.LgxMlpDesc()
         d.x, d.y, d.rows, d.nl, d.act = x.data_ptr(), y.data_ptr(), x.shape[0], len(self.linears), self.act
         for i, v in enumerate(self.dims):
@@ -113,22 +142,62 @@ class _FusedMLP:
 
 
 def launch_forward(descs, count, stream):
-    """`count` (1 or 2) MLP descriptors in one lgx_mlp_forward_batch launch on `stream`."""
+    """`count` (1 or 2) MLP descriptors in one lgx_mlp_forward_batch / lgx_mlp_x3_forward launch
+    on `stream` (by descriptor type)."""
+    from legged_gym_amd.sim import abi
     from legged_gym_amd.sim import lib as lgxlib
-    lgxlib.check(lgxlib.load().lgx_mlp_forward_batch(descs, count, stream), "lgx_mlp_forward_batch")
+    lib = lgxlib.load()
+    if isinstance(descs[0], abi.LgxMlpX3Desc):
+        lgxlib.check(lib.lgx_mlp_x3_forward(descs, count, stream), "lgx_mlp_x3_forward")
+    else:
+        lgxlib.check(lib.lgx_mlp_forward_batch(descs, count, stream), "lgx_mlp_forward_batch")
+
+
+def _x3_fits(mlps):
+    """One lgx_mlp_x3_forward launch holds these networks' activations in LDS (decided once per
+    combination, from dims alone)."""
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim import lib as lgxlib
+    key = tuple(tuple(m.dims) for m in mlps) + tuple(m.act for m in mlps)
+    fit = _X3_FIT.get(key)
+    if fit is None:
+        ds = (abi.LgxMlpX3Desc * len(mlps))()
+        for d, m in zip(ds, mlps):
+            d.nl, d.act, d.rows = len(m.linears), m.act, 1
+            for i, v in enumerate(m.dims):
+                d.dims[i] = v
+        fit = _X3_FIT[key] = lgxlib.load().lgx_mlp_x3_lds_bytes(ds, len(mlps)) >= 0
+    return fit
+
+
+_X3_FIT = {}
+
+
+def make_descs(triples):
+    """Descriptor array of one fused launch over up to two (fused_mlp, input, output) triples:
+    split-bf16 (lgx_mlp_x3_forward) when every network takes it and their activations fit the LDS
+    together, else f32 MFMA (lgx_mlp_forward_batch) for all of them."""
+    from legged_gym_amd.sim import abi
+    mlps = [m for m, _, _ in triples]
+    if any(m.x3 for m in mlps) and not (all(m.x3 for m in mlps) and _x3_fits(mlps)):
+        for m in mlps:
+            if m.x3:
+                m.x3, m._ver = False, None
+    descs = ((abi.LgxMlpX3Desc if mlps[0].x3 else abi.LgxMlpDesc) * len(triples))()
+    for i, (m, x, y) in enumerate(triples):
+        descs[i] = m.desc(x, y)
+    return descs
 
 
 def run_fused(pairs):
     """Forward of up to two (fused_mlp, input) pairs in one launch."""
-    from legged_gym_amd.sim import abi
-    outs, descs = [], (abi.LgxMlpDesc * len(pairs))()
-    for i, (m, x) in enumerate(pairs):
+    triples = []
+    for m, x in pairs:
         x = x.contiguous()
-        y = torch.empty(x.shape[0], m.dims[-1], device=x.device, dtype=torch.float)
-        descs[i] = m.desc(x, y)
-        outs.append((x, y))
-    launch_forward(descs, len(pairs), C.c_void_p(torch.cuda.current_stream(pairs[0][1].device).cuda_stream))
-    return [y for _, y in outs]
+        triples.append((m, x, torch.empty(x.shape[0], m.dims[-1], device=x.device, dtype=torch.float)))
+    launch_forward(make_descs(triples), len(triples),
+                   C.c_void_p(torch.cuda.current_stream(pairs[0][1].device).cuda_stream))
+    return [y for _, _, y in triples]
 
 
 class ActorCritic(nn.Module):

@@ -18,7 +18,7 @@ import torch.optim as optim
 
 from legged_gym_amd.sim import abi
 
-from .actor_critic import ActorCritic, launch_forward
+from .actor_critic import ActorCritic, launch_forward, make_descs
 from .fused_ppo import FusedPPOUpdate
 from .storage import RolloutStorage
 
@@ -96,8 +96,7 @@ class PPO:
         if getattr(self, "_mean_buf", None) is None or self._mean_buf.shape != (obs.shape[0], A):
             self._mean_buf = torch.empty(obs.shape[0], A, device=obs.device)
         mean = self._mean_buf
-        descs = (abi.LgxMlpDesc * 2)(ac._fused_actor.desc(obs, mean),
-                                     ac._fused_critic.desc(critic_obs, st.values[s]))
+        descs = make_descs([(ac._fused_actor, obs, mean), (ac._fused_critic, critic_obs, st.values[s])])
         launch_forward(descs, 2, C.c_void_p(main.cuda_stream))   # actor and critic in one launch
         if getattr(self, "_act_out", None) is None or self._act_out.shape != mean.shape:
             self._act_out = torch.empty_like(mean)

@@ -100,6 +100,11 @@ class LgxMlpDesc(C.Structure):
                 ("weights", C.c_void_p * 6), ("biases", C.c_void_p * 6)]
 
 
+class LgxMlpX3Desc(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("y", C.c_void_p), ("rows", i64), ("nl", i32), ("act", i32), ("dims", i32 * 7),
+                ("weights", C.c_void_p * 6), ("biases", C.c_void_p * 6)]
+
+
 class LgxPpoLossArgs(C.Structure):
     _fields_ = [("rows", i64), ("num_actions", i32), ("use_clipped_value_loss", i32), ("clip_param", C.c_float),
                 ("value_loss_coef", C.c_float), ("entropy_coef", C.c_float)] + [
@@ -196,6 +201,10 @@ def declare(lib, prefix="lgx"):
             "reduce_slices_finalize": (C.c_int, [C.POINTER(LgxReduceJob), i32, C.POINTER(LgxPpoLossArgs), vp]),
             "ppo_loss_bwd_layout": (C.c_int, [i64, i32, i32, C.POINTER(i64)]),
             "ppo_loss_bwd": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp, vp]),
+            "mlp_x3_weight_elems": (i64, [i32, i32]),
+            "mlp_x3_split": (C.c_int, [vp, i32, i32, vp, vp]),
+            "mlp_x3_lds_bytes": (i64, [C.POINTER(LgxMlpX3Desc), i32]),
+            "mlp_x3_forward": (C.c_int, [C.POINTER(LgxMlpX3Desc), i32, vp]),
             "gemm_partials_floats": (i64, [i64, i32, i32]),
             "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
             "gemm_tn": (C.c_int, [C.POINTER(LgxGemmTnArgs), vp]),
@@ -224,16 +233,18 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_fl
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
             "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
-            "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn"]
+            "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
+            "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward"]
 
 
-def check_layout(sizes_fn, n=11):
+def check_layout(sizes_fn, n=12):
     """Compare the library's sizeof() of every ABI struct with these mirrors (the oracle
     reports the first 3)."""
     out = (C.c_int64 * 16)()
     sizes_fn(out)
     mine = (C.sizeof(LgxModel), C.sizeof(LgxEnvParams), C.sizeof(LgxBuffers), C.sizeof(LgxMlpDesc),
             C.sizeof(LgxPpoLossArgs), C.sizeof(LgxReduceJob), C.sizeof(LgxPpoActArgs),
-            C.sizeof(LgxPpoStoreArgs), C.sizeof(LgxGemmArgs), C.sizeof(LgxCopy2dJob), C.sizeof(LgxGemmTnArgs))[:n]
+            C.sizeof(LgxPpoStoreArgs), C.sizeof(LgxGemmArgs), C.sizeof(LgxCopy2dJob), C.sizeof(LgxGemmTnArgs),
+            C.sizeof(LgxMlpX3Desc))[:n]
     if tuple(out)[:n] != mine:
         raise RuntimeError(f"lgx ABI layout mismatch: library {tuple(out)[:n]} vs bindings {mine}")

@@ -202,6 +202,65 @@ def test_mlp_forward_matches_torch(gpu, dims):
     assert ok, f"mlp forward max err {e}"
 
 
+@pytest.mark.parametrize("dims,act,rows", [((235, 512, 256, 128, 12), 1, 4096), ((235, 512, 256, 128, 1), 1, 37),
+                                           ((48, 512, 256, 128, 12), 1, 1000), ((7, 33, 5), 1, 1000),
+                                           ((30, 128, 128, 128, 3), 2, 777)])
+def test_mlp_x3_forward_matches_torch(gpu, dims, act, rows):
+    """lgx_mlp_x3_forward (split-bf16 products, weights from lgx_mlp_x3_split) against a float64
+    torch forward: f32-level agreement, ragged row tiles, widths off the 32 / 64 paddings."""
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim import lib as lgxlib
+    lib = lgxlib.load()
+    gen = torch.Generator().manual_seed(sum(dims) + rows)
+    x = torch.randn(rows, dims[0], generator=gen)
+    ws = [torch.randn(dims[i + 1], dims[i], generator=gen) / dims[i] ** 0.5 for i in range(len(dims) - 1)]
+    bs = [torch.randn(dims[i + 1], generator=gen) * 0.1 for i in range(len(dims) - 1)]
+    h = x.double()
+    for i, (w, b) in enumerate(zip(ws, bs)):
+        h = h @ w.double().T + b.double()
+        if i < len(ws) - 1:
+            h = torch.nn.functional.elu(h) if act == 1 else torch.tanh(h)
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wls = []
+    for w in ws:
+        wd = w.to(gpu)
+        wl = torch.empty(int(lib.lgx_mlp_x3_weight_elems(w.shape[0], w.shape[1])), dtype=torch.int16, device=gpu)
+        lgxlib.check(lib.lgx_mlp_x3_split(C.c_void_p(wd.data_ptr()), w.shape[0], w.shape[1], C.c_void_p(wl.data_ptr()),
+                                          stream), "split")
+        wls.append((wd, wl))
+    bds = [b.to(gpu) for b in bs]
+    xd = x.to(gpu)
+    y = torch.full((rows, dims[-1]), float("nan"), device=gpu)
+    d = (abi.LgxMlpX3Desc * 1)()
+    d[0].x, d[0].y, d[0].rows, d[0].nl, d[0].act = xd.data_ptr(), y.data_ptr(), rows, len(ws), act
+    for i, v in enumerate(dims):
+        d[0].dims[i] = v
+    for i in range(len(ws)):
+        d[0].weights[i], d[0].biases[i] = wls[i][1].data_ptr(), bds[i].data_ptr()
+    assert lib.lgx_mlp_x3_lds_bytes(d, 1) > 0
+    lgxlib.check(lib.lgx_mlp_x3_forward(d, 1, stream), "mlp_x3_forward")
+    torch.cuda.synchronize()
+    err = (y.cpu().double() - h).abs().max().item()
+    assert err <= 2e-5 * max(1.0, h.abs().max().item()), f"mlp x3 max err {err:.3e}"
+
+
+def test_mlp_x3_falls_back_when_lds_is_short(gpu):
+    """Three 512-wide hidden layers: 32 rows of two 512-wide limb images exceed the LDS, so the
+    rollout forward runs on the f32 MFMA kernel (lgx_mlp_forward_batch) and still matches torch."""
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    torch.manual_seed(1)
+    ac = ActorCritic(48, 48, 12, [512, 512, 512], [512, 512, 512]).to(gpu)
+    obs = torch.randn(300, 48, device=gpu)
+    with torch.inference_mode():
+        mean, value = ac.rollout_forward(obs, obs)
+        ref_mean, ref_v = ac.actor(obs), ac.critic(obs)
+    assert not ac._fused_actor.x3 and not ac._fused_critic.x3
+    ok, e = close(mean, ref_mean, 2e-4, 2e-4)
+    assert ok, f"actor mean max err {e}"
+    ok, e = close(value, ref_v, 2e-4, 2e-4)
+    assert ok, f"critic value max err {e}"
+
+
 def test_lstm_matches_oracle(gpu):
     import os
     import legged_gym_amd
@@ -281,6 +340,7 @@ def test_mlp_forward_batch_actor_critic(gpu):
     assert ok, f"actor mean max err {e}"
     ok, e = close(v, ref_v, 2e-4, 2e-4)
     assert ok, f"critic value max err {e}"
+    assert ac._fused_actor.x3 and ac._fused_critic.x3   # the split-bf16 kernel ran
 
 
 def test_gae_kernel_matches_torch_loop(gpu):
