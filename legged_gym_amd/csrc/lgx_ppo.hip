@@ -679,7 +679,7 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin,
       j = (4 * o4) / jb.n;
       i = 4 * o4 - j * jb.n;
       const float* s = jb.src + j * jb.job_stride + i;
-#pragma unroll 4
+#pragma unroll 8
       for (int k = g; k < jb.slices; k += groups) {
         const float4 v = *reinterpret_cast<const float4*>(s + (int64_t)k * jb.slice_stride);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
@@ -766,13 +766,33 @@ struct Mirrors {
   int32_t n;
 };
 
+// one mirror element: updated parameter value pi at (batch b, row rr, col cc) of block J
+__device__ __forceinline__ void mirror_store(const Mirror& J, int32_t b, int32_t rr, int32_t cc, float pi) {
+  if (J.transpose & 2) {   // bf16 limb layout of lgx_split_bf16 (split-bf16 GEMM operand)
+    const int32_t nn = (J.transpose & 1) ? cc : rr, kk = (J.transpose & 1) ? rr : cc;
+    const int32_t kout = (J.transpose & 1) ? J.rows : J.cols;
+    uint16_t* d = reinterpret_cast<uint16_t*>(J.dst) + b * J.dst_bs + x3_limb_off(nn, kk, 0, (kout + 31) >> 5);
+    const uint16_t l0 = bf16_rne(pi);
+    const float r1 = pi - __uint_as_float((uint32_t)l0 << 16);
+    const uint16_t l1 = bf16_rne(r1);
+    d[0] = l0;                   // limb l at + l * 128 * 32
+    d[4096] = l1;
+    d[8192] = bf16_rne(r1 - __uint_as_float((uint32_t)l1 << 16));
+  } else {
+    J.dst[b * J.dst_bs + (J.transpose ? (int64_t)cc * J.dst_ld + rr : (int64_t)rr * J.dst_ld + cc)] = pi;
+  }
+}
+
+// One parameter per thread (consecutive lanes: consecutive elements, so a non-transposed limb
+// mirror's 2-byte stores coalesce); the clip coefficient and the bias corrections (double pow)
+// computed once per workgroup.
 __global__ void __launch_bounds__(TPB)
 adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v, int64_t n,
                  const float* __restrict__ partials, int32_t nparts, float grad_scale, float max_norm,
                  const double* __restrict__ lr, const int64_t* __restrict__ step, float beta1, float beta2, float eps,
                  Mirrors mir) {
   __shared__ float red[TPB];
-  __shared__ float coef_s;
+  __shared__ float coef_s, step_size_s, bc2_sqrt_s;
   float s = 0.f;
   for (int i = threadIdx.x; i < nparts; i += TPB) s += partials[i];
   red[threadIdx.x] = s;
@@ -782,25 +802,25 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    float norm = sqrtf(red[0]);
-    float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
+    const float norm = sqrtf(red[0]);
+    const float c = max_norm > 0.f ? max_norm / (norm + 1e-6f) : 1.f;
     coef_s = fminf(c, 1.f) * grad_scale;
+    const double t = (double)step[0];
+    const float bc1 = (float)(1.0 - pow((double)beta1, t));
+    const float bc2 = (float)(1.0 - pow((double)beta2, t));
+    step_size_s = (float)(lr[0] / (double)bc1);
+    bc2_sqrt_s = sqrtf(bc2);
   }
   __syncthreads();
-  const float coef = coef_s;
-  const double t = (double)step[0];
-  const float bc1 = (float)(1.0 - pow((double)beta1, t));
-  const float bc2 = (float)(1.0 - pow((double)beta2, t));
-  const float step_size = (float)(lr[0] / (double)bc1);
-  const float bc2_sqrt = sqrtf(bc2);
+  const float coef = coef_s, step_size = step_size_s, bc2_sqrt = bc2_sqrt_s;
   for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
-    float gi = g[i] * coef;
+    const float gi = g[i] * coef;
     g[i] = gi;
-    float mi = beta1 * m[i] + (1.f - beta1) * gi;
-    float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
+    const float mi = beta1 * m[i] + (1.f - beta1) * gi;
+    const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
     const float pi = p[i] - step_size * mi / denom;
     p[i] = pi;
     for (int q = 0; q < mir.n; ++q) {
@@ -809,19 +829,7 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
       if (li < (uint64_t)J.count) {
         const int32_t l = (int32_t)li, rc = J.rows * J.cols;
         const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
-        if (J.transpose & 2) {   // bf16 limb layout of lgx_split_bf16 (split-bf16 GEMM operand)
-          const int32_t nn = (J.transpose & 1) ? cc : rr, kk = (J.transpose & 1) ? rr : cc;
-          const int32_t kout = (J.transpose & 1) ? J.rows : J.cols;
-          uint16_t* d = reinterpret_cast<uint16_t*>(J.dst) + b * J.dst_bs + x3_limb_off(nn, kk, 0, (kout + 31) >> 5);
-          const uint16_t l0 = bf16_rne(pi);
-          const float r1 = pi - __uint_as_float((uint32_t)l0 << 16);
-          const uint16_t l1 = bf16_rne(r1);
-          d[0] = l0;                   // limb l at + l * 128 * 32
-          d[4096] = l1;
-          d[8192] = bf16_rne(r1 - __uint_as_float((uint32_t)l1 << 16));
-        } else {
-          J.dst[b * J.dst_bs + (J.transpose ? (int64_t)cc * J.dst_ld + rr : (int64_t)rr * J.dst_ld + cc)] = pi;
-        }
+        mirror_store(J, b, rr, cc, pi);
       }
     }
   }
