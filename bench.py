@@ -52,7 +52,7 @@ def gemm_kernel_info(key, split):
     if key == "tn":
         return "gemm_tn_x3_kernel<*>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     if split:   # bias + ELU: the pipelined kernel; ELU' + column sums: the register-staged one
-        name = f"gemm_nt_x3p_kernel<{key}, *, 8>" if key != 2 else "gemm_nt_x3_kernel<2, true>"
+        name = f"gemm_nt_x3p_kernel<{key}, *>" if key != 2 else "gemm_nt_x3_kernel<2, true>"
         return name, pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     return f"gemm_nt_kernel<8, {key}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
 GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "

@@ -43,6 +43,26 @@ def mlp_bench():
     ms = timeit(fn)
     flop = rows * 2 * (30 * 128 + 128 * 128 * 2 + 128 * 3)
     print(f"actuator mlp rows={rows}: {ms*1e3:.1f} us  {flop/ms/1e9:.1f} TFLOP/s")
+    # the same net on lgx_mlp_x3_forward (split-bf16, weights streamed from L2)
+    from legged_gym_amd.sim import abi
+    dims = (30, 128, 128, 128, 3)
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    wl, bl = [], []
+    for i in range(4):
+        wi = torch.randn(dims[i + 1], dims[i], device=dev) / dims[i] ** 0.5
+        t = torch.empty(int(lib.lgx_mlp_x3_weight_elems(dims[i + 1], dims[i])), dtype=torch.int16, device=dev)
+        lgxlib.check(lib.lgx_mlp_x3_split(C.c_void_p(wi.data_ptr()), dims[i + 1], dims[i], C.c_void_p(t.data_ptr()),
+                                          stream), "split")
+        wl.append(t)
+        bl.append(torch.randn(dims[i + 1], device=dev))
+    d = (abi.LgxMlpX3Desc * 1)()
+    d[0].x, d[0].y, d[0].rows, d[0].nl, d[0].act = x.data_ptr(), y.data_ptr(), rows, 4, 2
+    for i, v in enumerate(dims):
+        d[0].dims[i] = v
+    for i in range(4):
+        d[0].weights[i], d[0].biases[i] = wl[i].data_ptr(), bl[i].data_ptr()
+    ms = timeit(lambda: lib.lgx_mlp_x3_forward(d, 1, stream))
+    print(f"actuator-shaped mlp_x3 rows={rows}: {ms*1e3:.1f} us  {flop/ms/1e9:.1f} TFLOP/s")
     ac = ActorCritic(235, 235, 12, [512, 256, 128], [512, 256, 128]).to(dev)
     obs = torch.randn(4096, 235, device=dev)
     with torch.inference_mode():
