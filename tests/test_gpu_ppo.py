@@ -104,6 +104,20 @@ def test_fused_minibatch_gradient_ragged_rows(gpu, rows):
         assert ((a - b).abs() <= 1e-5 + 2e-3 * b.abs()).all(), (rows, n, (a - b).abs().max().item())
 
 
+def test_fused_update_single_stream(gpu, monkeypatch):
+    """Every backward launch on one stream (LGX_PPO_DW_SIDE=0; default: the weight-gradient GEMMs
+    on a second stream next to the dA GEMMs): a full update against autograd."""
+    monkeypatch.setenv("LGX_PPO_DW_SIDE", "0")
+    ref, fus = make_pair()
+    torch.manual_seed(11)
+    vl_r, sl_r = ref.update()
+    torch.manual_seed(11)
+    vl_f, sl_f = fus.update()
+    assert fus.learning_rate == ref.learning_rate
+    assert abs(vl_f - vl_r) <= 1e-4 * abs(vl_r) + 1e-6 and abs(sl_f - sl_r) <= 1e-4 * abs(sl_r) + 1e-6
+    assert getattr(fus._fused, "_side", None) is None
+
+
 def test_fused_minibatch_gradient_separate_loss_and_head(gpu, monkeypatch):
     """lgx_ppo_loss + lgx_head_bwd_finalize as two launches (LGX_PPO_LOSS_BWD=0) instead of
     lgx_ppo_loss_bwd: minibatch gradient and a full update against autograd."""
