@@ -466,6 +466,7 @@ class FusedPPOUpdate:
             job(self.P[0][1], self.Wg[0] + n1, n1c, 1, 0, Sk[0], n1c, 0)
         else:
             job(self.P[0], self.Wg[0], n1, 2, Sk[0] * n1, Sk[0], n1, n1)            # dW1 (actor, critic)
+        n_dw1 = len(jobs)   # (the layer-1 jobs come first: the rest can be reduced before dW1 is done)
         for k in range(1, self.L):
             nk = h[k] * h[k - 1]
             job(self.P[k], self.Wg[k], nk, 2, Sk[k] * nk, Sk[k], nk, nk)            # dW_k stacked
@@ -481,6 +482,8 @@ class FusedPPOUpdate:
             raise RuntimeError("too many reduction jobs for one launch")
         self.jobs = (abi.LgxReduceJob * len(jobs))(*jobs)
         self.njobs = len(jobs)
+        self.jobs_dw1 = (abi.LgxReduceJob * n_dw1)(*jobs[:n_dw1])
+        self.jobs_rest = (abi.LgxReduceJob * (len(jobs) - n_dw1))(*jobs[n_dw1:])
 
     # ------------------------------------------------------------------ update
     @torch.no_grad()
@@ -757,6 +760,16 @@ class FusedPPOUpdate:
                 chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
                                            _vp(self.col_parts[k - 1]), stream), "elu_bwd")
             dZ = self.D[k - 1]
+        early = (side_used and self.loss_bwd and len(self.jobs_rest) > 0
+                 and os.environ.get("LGX_PPO_EARLY_REDUCE", "1") != "0")
+        if early:
+            # every gradient block but dW1's is complete once dA_1 (this stream) and the side
+            # stream's dW GEMMs are: reduce them (+ the loss finalize) on the side stream while dW1
+            # runs here - the memory-bound reduction next to the MFMA-bound GEMM
+            self._ev_in[0].record(torch.cuda.current_stream(self.dev))
+            self._side.wait_event(self._ev_in[0])
+            chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
+                                               C.c_void_p(self._side.cuda_stream)), "reduce")
         if 0 in self.gemm_dw and fused:     # lgx_gemm_tn over the minibatch's padded input rows
             t = self.gemm_dw[0]
             t[0].B = xp.data_ptr()
@@ -773,7 +786,9 @@ class FusedPPOUpdate:
         if side_used:   # the weight gradients are complete before the reduction reads them
             self._ev_out.record(self._side)
             torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
-        if self.loss_bwd:
+        if early:
+            chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
+        elif self.loss_bwd:
             chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
         else:
             chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
