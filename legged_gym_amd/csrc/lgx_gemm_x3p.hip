@@ -11,9 +11,9 @@
 //     XCD-contiguous tile ranges (consecutive tiles share A rows: L2 reuse on one XCD).  Wave
 //     layouts (template NWV): 4 waves = one per SIMD, 64 x 128 each (2 x 4 transposed 32x32
 //     accumulators) - no second wave competes for the SIMD's issue, so the barrier that closes
-//     every 32-k slot does not wait on a starved wave; 8 waves = two per SIMD, 64 x 64 each
-//     (measured with s_memtime stamps: the younger wave of each SIMD loses issue arbitration
-//     and the older one idles ~35 % of every slot at the barrier);
+//     every 32-k slot does not wait on a starved wave; 8 waves = two per SIMD, 32 x 128 each
+//     (X3P_WGN; measured with s_memtime stamps: the younger wave of each SIMD loses issue
+//     arbitration and the older one idles ~35 % of every slot at the barrier);
 //   * every global -> LDS copy is an LDS-DMA load (global_load_lds_dwordx4): no staging
 //     registers, no LDS write pass.  A (f32 activations) goes through a 3-deep ring of 32 KB
 //     stages, its 16-byte chunks placed at chunk ^ ((row >> 1) & 7) by the per-lane SOURCE
@@ -47,6 +47,12 @@ constexpr int B_ST = 3 * PN * PK * 2;        // 24 KB: limb B stage ([limb][128 
 constexpr int NSA = 3, NSB = 2;              // ring depths
 constexpr int B_BLK = 3 * 128 * 32;             // bf16 per pre-split (128 n x 32 k) block
 
+// X3P_WGN: waves along N of the 8-wave 256-row tile.  1 (default): 8 x 1 waves of 32 x 128, each
+// wave splits only its own 32 A rows (the 4 x 2 layout of 64 x 64 waves split every A row in
+// two waves) for twice the B fragment reads (LDS has the slack): layer-1 forward 81.8 -> 75-77 us
+#ifndef X3P_WGN
+#define X3P_WGN 1
+#endif
 // Tile of PM = 256 rows (the default) or 128 rows (half tiles: the layer whose 256-row tile count
 // leaves a fractional last round on the CUs, e.g. 384 tiles on 256 CUs -> 768 half tiles = 3 rounds)
 template <int NWV, int PM>
@@ -55,8 +61,8 @@ struct XC {
   static constexpr int OFF_B = NSA * A_ST;
   static constexpr int OFF_BIAS = OFF_B + NSB * B_ST;    // 3 x 1 KB: bias of the pending / current / next tile
   static constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 150,528 | 101,376 B
-  static constexpr int WGN = NWV == 8 ? 2 : 1;          // waves along N
-  static constexpr int WGM = NWV / WGN;                  // waves along M (4)
+  static constexpr int WGN = NWV == 8 && (PM == 128 || X3P_WGN == 2) ? 2 : 1;   // waves along N
+  static constexpr int WGM = NWV / WGN;                  // waves along M (4 | 8)
   static constexpr int WI = PM / WGM / 32;               // 32-row accumulator tiles per wave (2 | 1)
   static constexpr int WJ = PN / WGN / 32;               // 32-column accumulator tiles per wave (2 | 4)
   static constexpr int PT = 64 * NWV;
@@ -66,7 +72,7 @@ struct XC {
   static constexpr int NB = 2 * WI * WJ;                 // MFMA blocks per slot (two 16-k halves)
   static constexpr int ITEMS = B_GL + 1 + A_GL;          // side items per slot: B loads, bias, A loads
   static constexpr int IPB = (ITEMS + NB - 1) / NB;      // side items per MFMA block
-  static_assert(WGM == 4 && (WI == 1 || WI == 2), "A offsets assume 4 wave rows of 32 WI");
+  static_assert((WGM == 4 || WGM == 8) && (WI == 1 || WI == 2), "wave rows of 32 WI rows");
 };
 
 struct PArgs {
