@@ -51,8 +51,9 @@ def gemm_kernel_info(key, split):
     pipe = "bf16 MFMA (v_mfma_f32_32x32x16_bf16), split-bf16: 6 limb products per f32 product"
     if key == "tn":
         return "gemm_tn_x3_kernel<*>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
-    if split:   # bias + ELU: the pipelined kernel; ELU' + column sums: the register-staged one
-        name = f"gemm_nt_x3p_kernel<{key}, *>" if key != 2 else "gemm_nt_x3_kernel<2, true>"
+    if split:   # the pipelined kernel (ELU' + column sums on the register-staged one with LGX_GEMM_X3P_DELU=0)
+        staged = key == 2 and os.environ.get("LGX_GEMM_X3P_DELU", "1") == "0"
+        name = "gemm_nt_x3_kernel<2, true>" if staged else f"gemm_nt_x3p_kernel<{key}, *>"
         return name, pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     return f"gemm_nt_kernel<8, {key}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
 GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "

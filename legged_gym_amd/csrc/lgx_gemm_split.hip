@@ -405,6 +405,9 @@ __global__ void __launch_bounds__(256) split_rows_kernel(SplitJobs J) {
 
 }  // namespace
 
+#ifndef X3P_DELU_DEFAULT
+#define X3P_DELU_DEFAULT 1
+#endif
 // lgx_gemm_nt's split-bf16 path (lgx_gemm.hip checks the common arguments first)
 int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream_) {
   static const bool pipelined = [] {   // A/B switch: LGX_GEMM_X3P=0 keeps the register-staged kernel
@@ -412,9 +415,12 @@ int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream_) {
     return !(e && e[0] == '0');
   }();
 
-  // the pipelined kernel for the bias + ELU / plain epilogues; the column-sum epilogue runs here
-  // (its x3p form, without deferral, measured equal or slower: dA3 48 vs 43 us)
-  if (a.Bs && a.K % BK == 0 && pipelined && a.epi != LGX_GEMM_DELU_COLSUM) return lgx_gemm_nt_x3p(a, cus, stream_);
+  // the pipelined kernel for the bias + ELU / plain epilogues and (LGX_GEMM_X3P_DELU, read per
+  // call) the ELU' + column-sum epilogue at its tiles' ends
+  const char* ed = getenv("LGX_GEMM_X3P_DELU");
+  const bool x3p_delu = ed ? ed[0] != '0' : X3P_DELU_DEFAULT;
+  if (a.Bs && a.K % BK == 0 && pipelined && (a.epi != LGX_GEMM_DELU_COLSUM || x3p_delu))
+    return lgx_gemm_nt_x3p(a, cus, stream_);
   const hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
              a.partials, 0, a.Bs};

@@ -26,7 +26,10 @@
 //   * A is split into its limbs after the fragment read (8 floats per lane per 16 k: 12
 //     v_cvt_pk_bf16_f32 + exact f32 subtractions);
 //   * epilogues: bias + ELU / plain deferred into the next tile's slots (16-byte row stores of the
-//     transposed accumulators, a few per slot, under the MFMAs).
+//     transposed accumulators, a few per slot, under the MFMAs); ELU' + bias-gradient column sums
+//     (the backward dA) at each tile's end from non-transposed accumulators (lane = column: the
+//     column sums stay in registers), Y read there (dA2 101-103 -> 89-93 us vs the
+//     register-staged gemm_nt_x3_kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -60,7 +63,7 @@ struct XC {
   static constexpr int A_ST = PM * PK * 4;               // f32 A stage (PM rows x 128 B): 32 | 16 KB
   static constexpr int OFF_B = NSA * A_ST;
   static constexpr int OFF_BIAS = OFF_B + NSB * B_ST;    // 3 x 1 KB: bias of the pending / current / next tile
-  static constexpr int P_LDS = OFF_BIAS + 3 * 1024;      // 150,528 | 101,376 B
+  static constexpr int P_LDS = OFF_BIAS + 4 * 1024;      // 151,552 | 102,400 B (DELU: 4 KB column-sum scratch)
   static constexpr int WGN = NWV == 8 && (PM == 128 || X3P_WGN == 2) ? 2 : 1;   // waves along N
   static constexpr int WGM = NWV / WGN;                  // waves along M (4 | 8)
   static constexpr int WI = PM / WGM / 32;               // 32-row accumulator tiles per wave (2 | 1)
@@ -240,7 +243,7 @@ __device__ __forceinline__ void issue_b(uint32_t lds0, int buf, const PArgs& g, 
 // issues and deferred stores are spread between the MFMA blocks, where a DMA issue that waits for
 // the texture unit to accept it costs no MFMA time (issued in one burst before the compute, the 14
 // DMA loads of a 4-wave slot took ~950 cycles of the wave's ~5600).
-template <int NWV, int PM, typename Side>
+template <int NWV, int PM, bool TRANS, typename Side>
 __device__ __forceinline__ void compute_slot(const char* __restrict__ la, const char* __restrict__ lb, int wm, int wn,
                                              int r, int h, f32x16v (&acc)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ],
                                              Side&& side) {
@@ -279,12 +282,21 @@ __device__ __forceinline__ void compute_slot(const char* __restrict__ la, const 
         continue;
 #endif
         f32x16v c = acc[i][j];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][2], a[i][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][1], a[i][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][1], a[i][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][0], c, 0, 0, 0);
+        if constexpr (TRANS) {   // weights first: lane = output row, 4 runs of 4 columns
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][2], a[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][1], a[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][1], a[i][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[j][0], a[i][0], c, 0, 0, 0);
+        } else {                 // rows first: lane = output column (column sums in registers)
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], c, 0, 0, 0);
+        }
         acc[i][j] = c;
         side((s * WI + i) * WJ + j);
       }
@@ -315,6 +327,74 @@ __device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pe
   if (row < g.M) *reinterpret_cast<float4*>(g.C + T.z * g.sc + row * g.ldc + T.nt * PN + cn) = v;
 }
 
+// ELU' + bias-gradient column sums at a tile's end (non-transposed accumulators: lane = column
+// 32 j + r of the wave's 32 WI rows, acc[i][j][e] = row 32 i + 8 (e >> 2) + 4 h + (e & 3)):
+// D = acc * elu'(Y) with 128-byte row segments per load / store, column sums in registers, then
+// across the lane halves and, in a fixed order, across the waves of each 128-row partial block
+// (partials[m / 128][z][n], the layout of gemm_nt_x3_kernel's).  scratch: [NWV][128] floats.
+template <int NWV, int PM>
+__device__ __forceinline__ void delu_epilogue(const PArgs& g, const f32x16v (&acc)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ],
+                                              const PTile& T, int wave, int wm, int wn, int r, int h,
+                                              float* scratch) {
+  using X = XC<NWV, PM>;
+  constexpr int WI = X::WI, WJ = X::WJ;
+  const int64_t m0 = (int64_t)T.mt * PM + wm * 32 * WI;
+  const int cl = wn * 32 * WJ;                         // the wave's first column in the tile
+  const int64_t n0 = (int64_t)T.nt * PN + cl;
+  const float* Y = g.Y + T.z * g.sc;
+  float* C = g.C + T.z * g.sc;
+  float cs[WJ];
+#pragma unroll
+  for (int j = 0; j < WJ; ++j) cs[j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < WI; ++i)
+#pragma unroll
+    for (int e0 = 0; e0 < 16; e0 += 4) {   // 4 WJ loads of Y in flight, then the stores
+      float y[4][WJ];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+          const int64_t row = min(m0 + 32 * i + 8 * ((e0 + e) >> 2) + 4 * h + ((e0 + e) & 3), g.M - 1);
+          y[e][j] = Y[row * g.ldc + n0 + 32 * j + r];
+        }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) {
+          const int64_t row = m0 + 32 * i + 8 * ((e0 + e) >> 2) + 4 * h + ((e0 + e) & 3);
+          const float d = acc[i][j][e0 + e] * elu_grad_from_out(y[e][j]);
+          if (row < g.M) {
+            C[row * g.ldc + n0 + 32 * j + r] = d;
+            cs[j] += d;
+          }
+        }
+    }
+#pragma unroll
+  for (int j = 0; j < WJ; ++j) cs[j] += __shfl_xor(cs[j], 32);
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) scratch[wave * 128 + cl + 32 * j + r] = cs[j];
+  }
+  __syncthreads();
+  // wave w of the first X::WGN * (128 / (32 WI)) waves... : one 128-row block = 128 / (32 WI)
+  // wave rows; the waves of wave row 0 of each block write its partial row
+  constexpr int BLOCK_WM = 128 / (32 * WI);            // wave rows per 128-row partial block
+  if (wm % BLOCK_WM == 0 && h == 0) {
+    const int64_t mb = ((int64_t)T.mt * PM + wm * 32 * WI) / 128;
+    if (mb * 128 < g.M) {
+      float* P = g.partials + mb * ((int64_t)g.batch * g.N) + (int64_t)T.z * g.N;
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) {
+        float v = 0.f;
+#pragma unroll
+        for (int w = 0; w < BLOCK_WM; ++w) v += scratch[((wm + w) * X::WGN + wn) * 128 + cl + 32 * j + r];   // fixed order
+        P[n0 + 32 * j + r] = v;
+      }
+    }
+  }
+}
+
 #ifdef X3P_CLOCK   // A/B instrumentation: per-slot s_memtime stamps of workgroup 0 into g.partials
 #define X3P_STAMP(e) \
   if (clk && q < 32) clk[(wave * 32 + q) * 8 + (e)] = __builtin_amdgcn_s_memtime()
@@ -339,8 +419,8 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   constexpr int WI = X::WI, WJ = X::WJ, AG = X::A_GL;
   constexpr int A_ST = X::A_ST, OFF_B = X::OFF_B, OFF_BIAS = X::OFF_BIAS;
   extern __shared__ __attribute__((aligned(16))) char plds[];
-  static_assert(EPI != LGX_GEMM_DELU_COLSUM, "the column-sum epilogue runs on gemm_nt_x3_kernel");
-  constexpr bool DEFER = KBT > 0;
+  constexpr bool DELU = EPI == LGX_GEMM_DELU_COLSUM;
+  constexpr bool DEFER = KBT > 0 && !DELU;             // (ELU' + column sums: at the tile's end)
   // deferred store runs per slot (slots k with k * GPS < GROUPS store GPS runs each)
   constexpr int GPS = DEFER ? (X::GROUPS >= KBT ? X::GROUPS / KBT : 1) : 0;
   static_assert(!DEFER || X::GROUPS % GPS == 0, "every storing slot issues exactly GPS runs (vmcnt counts)");
@@ -474,7 +554,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       };
       X3P_STAMP(4);
 #ifndef X3P_NO_COMPUTE
-      compute_slot<NWV, PM>(plds + (q % NSA) * A_ST, plds + OFF_B + (q % NSB) * B_ST, wm, wn, r, h, acc, side);
+      compute_slot<NWV, PM, !DELU>(plds + (q % NSA) * A_ST, plds + OFF_B + (q % NSB) * B_ST, wm, wn, r, h, acc, side);
 #else
       for (int blk = 0; blk < X::NB; ++blk) side(blk);
 #endif
@@ -494,10 +574,14 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       else wait_vm<0>();
       waited = true;
 #ifndef X3P_NO_EPI
+      if constexpr (DELU) {
+        delu_epilogue<NWV, PM>(g, acc, T, wave, wm, wn, r, h, reinterpret_cast<float*>(plds + OFF_BIAS));
+      } else {
 #pragma unroll
-      for (int gi = 0; gi < X::GROUPS; ++gi)
-        p_store_group<EPI, NWV, PM>(g, acc, T, wm, wn, r, h,
-                                    reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
+        for (int gi = 0; gi < X::GROUPS; ++gi)
+          p_store_group<EPI, NWV, PM>(g, acc, T, wm, wn, r, h,
+                                      reinterpret_cast<const float*>(plds + OFF_BIAS + (tj % 3) * 1024), gi);
+      }
 #else
       if (acc[0][0][0] == 1234.5f) g.C[tid] = acc[WI - 1][1][3] + acc[0][1][2] + acc[WI - 1][0][1];
 #endif
@@ -523,14 +607,16 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 
 typedef void (*x3p_fn)(PArgs);
 
-// [epilogue (PLAIN, BIAS_ELU)][KBT index: 0 (runtime K), 4, 8, 16]
+// [epilogue (PLAIN, BIAS_ELU, DELU_COLSUM)][KBT index: 0 (runtime K), 4, 8, 16]
 template <int NWV, int PM>
 struct X3PTable {
-  static constexpr x3p_fn k[2][4] = {
+  static constexpr x3p_fn k[3][4] = {
       {&gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 4, NWV, PM>,
        &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 16, NWV, PM>},
       {&gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 4, NWV, PM>,
-       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV, PM>}};
+       &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV, PM>},
+      {&gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 4, NWV, PM>,
+       &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 16, NWV, PM>}};
 };
 
 template <int NWV, int PM>
@@ -596,7 +682,6 @@ int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
   }();
   static const bool attrs = x3p_attrs<4, 256>() && x3p_attrs<8, 256>() && x3p_attrs<8, 128>();
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_nt: hipFuncSetAttribute (dynamic LDS) failed");
-  if (a.epi == LGX_GEMM_DELU_COLSUM) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt_x3p: no column-sum epilogue");
   const int pm = pick_pm(a.M, g.ntn, a.batch, cus, nwv);
   const int64_t tiles = ((a.M + pm - 1) / pm) * g.ntn * a.batch;
   if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too many tiles");

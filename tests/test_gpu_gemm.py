@@ -147,6 +147,18 @@ def test_gemm_presplit_tile_heights(gpu, monkeypatch, pm, M, N, K):
         _run(M, N, K, 2, epi, seed=M + K + pm, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
 
 
+@pytest.mark.parametrize("pm", [128, 256])
+@pytest.mark.parametrize("M,N,K", [(24576, 256, 128), (24576, 512, 256), (300, 128, 256), (513, 256, 128),
+                                   (1000, 128, 96), (1, 128, 32)])
+def test_gemm_presplit_delu_pipelined(gpu, monkeypatch, pm, M, N, K):
+    """ELU' + bias-gradient column sums on the pipelined kernel (LGX_GEMM_X3P_DELU=1): the epilogue
+    at each tile's end with non-transposed accumulators, partial rows per 128 output rows from
+    the waves of both tile heights; ragged M, one row, runtime K."""
+    monkeypatch.setenv("LGX_GEMM_X3P_DELU", "1")
+    monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
+    _run(M, N, K, 2, abi.GEMM_DELU_COLSUM, seed=M + K + pm + 1, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+
+
 @pytest.mark.parametrize("transpose", [False, True])
 def test_split_bf16_limbs(gpu, transpose):
     """lgx_split_bf16: limbs are RNE bf16 (x0 = bf16(x), |x1| <= 2^-8|x0|, |x2| <= 2^-8|x1|),
