@@ -249,9 +249,13 @@ LGX_DEV void extras_finalize_body(const lgx_env_params* __restrict__ P, const lg
 // finalize, so the reduction needs no second launch.  Release: every thread's partial /
 // time_out / level writes are fenced at device scope before the ticket; acquire: the last
 // workgroup fences again before reading them (the L2s of the 8 XCDs are not coherent).
+// The release fence (an L2 write-back at agent scope) is taken by wave 0 only: the block's
+// partial row was written by threads < T + 2 <= 64 (block_partials), and every other wave skips
+// the write-back (measured: all four waves fencing took ~15 us of each workgroup's timeline).
 LGX_DEV bool take_last_ticket(const lgx_buffers& B, int nblocks) {
   __shared__ int last;
-  __threadfence();
+  static_assert(LGX_PARTIAL_STRIDE <= 64, "the partial-row writers are wave 0");
+  if (threadIdx.x < 64) __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned int* ctr = reinterpret_cast<unsigned int*>(B.scratch + (int64_t)nblocks * LGX_PARTIAL_STRIDE);
@@ -393,6 +397,18 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
       }
     }
   }
+  // the env lane's pre-step root state, commands and episode length, staged with the rows above
+  // (their global loads would otherwise be phase B's first exposed round trip)
+  __shared__ float sroot[LGX_ENV_BLOCK][13];
+  __shared__ float scmd[LGX_ENV_BLOCK][4];
+  __shared__ int64_t sep[LGX_ENV_BLOCK];
+  for (int idx = tid; idx < LGX_ENV_BLOCK * 17; idx += ENV_THREADS) {
+    const int le = idx / 17, c = idx - le * 17;
+    const int64_t e = min(e0 + le, N - 1);
+    if (c < 13) sroot[le][c] = B.root_states[e * 13 + c];
+    else scmd[le][c - 13] = B.commands[e * 4 + c - 13];
+  }
+  if (tid < LGX_ENV_BLOCK) sep[tid] = B.episode_length[min(e0 + tid, N - 1)];
   // episode sums [T, N] and feet_air_time [N, 4] are read-modify-written by the env lane: stage
   // them too (coalesced over envs), so phase B has no dependent global round trips
   __shared__ float ssum[LGX_MAX_TERMS][LGX_ENV_BLOCK];
@@ -413,16 +429,17 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
     const int e = e0 + tid;
     for (int t = 0; t < LGX_PARTIAL_STRIDE; ++t) part[tid][t] = 0.f;
     if (e < N) {
-      int64_t ep = B.episode_length[e] + 1;  // :118
+      int64_t ep = sep[tid] + 1;  // :118
       B.episode_length[e] = ep;
-      float* rs = B.root_states + (int64_t)e * 13;
-      const float qx = rs[3], qy = rs[4], qz = rs[5], qw = rs[6];
+      float* rs = B.root_states + (int64_t)e * 13;   // (written: pushes, resets)
+      const float* rs0 = sroot[tid];                 // pre-step values, staged
+      const float qx = rs0[3], qy = rs0[4], qz = rs0[5], qw = rs0[6];
       EnvView v;
-      v.blv = quat_rotate_inverse(qx, qy, qz, qw, mk3(rs[7], rs[8], rs[9]));     // :122-125
-      v.bav = quat_rotate_inverse(qx, qy, qz, qw, mk3(rs[10], rs[11], rs[12]));
+      v.blv = quat_rotate_inverse(qx, qy, qz, qw, mk3(rs0[7], rs0[8], rs0[9]));     // :122-125
+      v.bav = quat_rotate_inverse(qx, qy, qz, qw, mk3(rs0[10], rs0[11], rs0[12]));
       v.pg = quat_rotate_inverse(qx, qy, qz, qw, mk3(0.f, 0.f, -1.f));
       float* cmd_g = B.commands + (int64_t)e * 4;
-      for (int k = 0; k < 4; ++k) v.cmd[k] = cmd_g[k];
+      for (int k = 0; k < 4; ++k) v.cmd[k] = scmd[tid][k];
       if (ep % P->resample_interval == 0) resample_cmd(P, D, e, LGX_DRAW_CMD, step, 0u, v.cmd);  // :342-343
       if (P->heading_command) {  // :344-347
         f3 f = quat_apply(qx, qy, qz, qw, mk3(1.f, 0.f, 0.f));
@@ -441,8 +458,8 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
       v.la = srow[tid] + 48 + LGX_MAX_BODIES * 3;
       v.ldv = srow[tid] + 60 + LGX_MAX_BODIES * 3;
       v.fat = sfat[tid];
-      v.rootz = rs[2];
-      v.mh = B.measured_heights ? B.measured_heights + (int64_t)e * P->num_height_points : nullptr;
+      v.rootz = rs0[2];
+      v.mh = P->measure_heights ? sheight[tid] : nullptr;   // this step's scan (phase A), from LDS
       // check_termination :143-148
       bool r = false;
       for (int i = 0; i < P->num_termination_bodies; ++i) r |= norm3p(v.cf + 3 * P->termination_indices[i]) > 1.f;
@@ -480,7 +497,7 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
       sbase[tid][6] = v.pg.x; sbase[tid][7] = v.pg.y; sbase[tid][8] = v.pg.z;
 #pragma unroll
       for (int k = 0; k < 4; ++k) sbase[tid][9 + k] = v.cmd[k];
-      sbase[tid][13] = rs[2];
+      sbase[tid][13] = v.reset ? rs[2] : rs0[2];   // post-reset root z
       for (int k = 0; k < 4; ++k) cmd_g[k] = v.cmd[k];
       if (P->curriculum) part[tid][T + 1] = (float)B.terrain_levels[e];
       float* o3 = B.base_lin_vel + (int64_t)e * 3;
