@@ -521,30 +521,54 @@ LGX_DEV void post_physics_body(const lgx_env_params* __restrict__ P, const lgx_b
   LGX_CLK(3);
   // ---- phase C: observations (:214-231) + noise + clip (:103-104); a lane owns 4 consecutive
   // entries of a row, whose noise is one Philox block (LGX_DRAW_NOISE is a multiple of 4)
+  // Two branch-free loops (the index ranges of one wave's lanes used to diverge over the five
+  // source cases): entries 0..47 read their source through a per-index LDS offset into the
+  // env's staged rows, the height entries 48.. (quads 12..) come from the scan.
   const int nq = (nobs + 3) >> 2;
-  const int total = LGX_ENV_BLOCK * nq;
-#pragma unroll 2
-  for (int idx = tid; idx < total; idx += ENV_THREADS) {
-    const int le = idx / nq, q = idx - le * nq;
+  const int nq0 = min(nq, 12);
+  __shared__ int16_t src_off[48];   // entry i < 48 -> float offset: sbase row (< 16) or srow row (+ 16)
+  if (tid < 48) {
+    const int i = tid;
+    src_off[i] = (int16_t)(i < 12 ? i : i < 24 ? 16 + 2 * (i - 12) : i < 36 ? 16 + 2 * (i - 24) + 1
+                                                                           : 16 + 36 + LGX_MAX_BODIES * 3 + i - 36);
+  }
+  __syncthreads();
+  const bool noise = P->add_noise != 0;
+  const float clip = P->clip_obs;
+  for (int idx = tid; idx < LGX_ENV_BLOCK * nq0; idx += ENV_THREADS) {
+    const int le = idx / nq0, q = idx - le * nq0;
     const int e = e0 + le;
     if (e >= N) continue;
     float nz[4] = {0.5f, 0.5f, 0.5f, 0.5f};
-    if (P->add_noise) D.quad(e, (LGX_DRAW_NOISE >> 2) + q, step, 0u, nz);
+    if (noise) D.quad(e, (LGX_DRAW_NOISE >> 2) + q, step, 0u, nz);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int i = 4 * q + u;
       if (i >= nobs) break;
-      const float* sb = sbase[le];
-      const float* sr = srow[le];
-      float v;   // source value (reference order, legged_robot.py:216-226)
-      if (i < 12) v = sb[i];
-      else if (i < 24) v = sr[2 * (i - 12)];
-      else if (i < 36) v = sr[2 * (i - 24) + 1];
-      else if (i < 48) v = sr[36 + LGX_MAX_BODIES * 3 + i - 36];
-      else v = clampf(sb[13] - 0.5f - sheight[le][i - 48], -1.f, 1.f);
+      const int so = src_off[i];
+      const float v = so < 16 ? sbase[le][so] : srow[le][so - 16];   // (reference order, :216-226)
       float o = (v - obs_sub[i]) * obs_mul[i];
-      if (P->add_noise) o += (2.f * nz[u] - 1.f) * obs_nsc[i];
-      B.obs[(int64_t)e * nobs + i] = clampf(o, -P->clip_obs, P->clip_obs);
+      if (noise) o += (2.f * nz[u] - 1.f) * obs_nsc[i];
+      B.obs[(int64_t)e * nobs + i] = clampf(o, -clip, clip);
+    }
+  }
+  const int nqh = nq - nq0;   // height quads
+#pragma unroll 2
+  for (int idx = tid; idx < LGX_ENV_BLOCK * nqh; idx += ENV_THREADS) {
+    const int le = idx / nqh, q = nq0 + (idx - le * nqh);
+    const int e = e0 + le;
+    if (e >= N) continue;
+    float nz[4] = {0.5f, 0.5f, 0.5f, 0.5f};
+    if (noise) D.quad(e, (LGX_DRAW_NOISE >> 2) + q, step, 0u, nz);
+    const float z = sbase[le][13] - 0.5f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = 4 * q + u;
+      if (i >= nobs) break;
+      const float v = clampf(z - sheight[le][i - 48], -1.f, 1.f);
+      float o = (v - obs_sub[i]) * obs_mul[i];
+      if (noise) o += (2.f * nz[u] - 1.f) * obs_nsc[i];
+      B.obs[(int64_t)e * nobs + i] = clampf(o, -clip, clip);
     }
   }
   LGX_CLK(4);
