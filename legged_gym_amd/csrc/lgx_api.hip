@@ -223,8 +223,9 @@ static int join_aux(lgx_sim* s, hipStream_t st) {
 }
 
 // Where the Go1 actuator net runs (A/B switch LGX_ACT_OVERLAP): 2 (default) = on workgroups of
-// its own inside the post-physics launch, 1 = its own launch on an auxiliary stream, 0 = its own
-// launch on the caller's stream.
+// its own inside the post-physics launch (f32 MFMA body), 3 = the same with the split-bf16 body,
+// 1 = its own launch on an auxiliary stream, 0 = its own launch on the caller's stream (own
+// launches: the split-bf16 kernel unless LGX_ACT_X3=0).
 static int act_mode() {
   const char* e = getenv("LGX_ACT_OVERLAP");
   return e ? atoi(e) : 2;
@@ -269,14 +270,14 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
   if (rc) return rc;
   const bool act_net = p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel;
   const int mode = act_mode();
-  if (act_net && mode == 2) {
+  if (act_net && (mode == 2 || mode == 3)) {
     // UniNet on every (substep, env, leg) row of this step's model_ins, inside the post-physics
     // launch (the next physics launch, stream-ordered after it, rewrites model_ins)
     arm(s, 2, sample);
     rc = launch_check(lgx_launch_post_physics_act(s->d_params, s->bufs, p.num_envs, step, s->draws, s->extras_snapshot,
                                                   s->bufs.model_ins, s->bufs.act_dvel,
                                                   (int64_t)p.decimation * p.num_envs * 4, s->bufs.act_net_w,
-                                                  s->bufs.act_net_scale, st),
+                                                  s->bufs.act_net_scale, st, mode == 3),
                       "lgx_step: post-physics + actuator launch");
     lgx_timing = lgx_timing_slot{};
     return rc;

@@ -24,7 +24,7 @@ int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int3
 // post-physics + the Go1 actuator net (act_rows rows of act_in -> act_out) in one launch
 int lgx_launch_post_physics_act(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int64_t step,
                                 const float* draws, float* extras_snapshot, const float* act_in, float* act_out,
-                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream);
+                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream, int x3 = 0);
 int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
                          const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
                          float* extras_snapshot, hipStream_t stream);

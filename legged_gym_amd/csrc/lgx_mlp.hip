@@ -292,9 +292,16 @@ int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t st
 #include "lgx_actuator_ws.h"
 
 __global__ void __launch_bounds__(256, 2) lgx_actuator_ws_kernel(WsArgs a) { actuator_ws_body(a, blockIdx.x, gridDim.x); }
+// split-bf16 body: one workgroup (one wave per SIMD) per CU, 216 weight registers per lane
+__global__ void __launch_bounds__(256, 1) lgx_actuator_x3_kernel(WsArgs a) { actuator_x3_body(a, blockIdx.x, gridDim.x); }
 
 static int actuator_ws_enabled() {
   const char* e = getenv("LGX_ACT_WS");  // A/B switch: 0 = generic fused MLP kernel
+  return e ? atoi(e) : 1;
+}
+
+int lgx_actuator_x3_enabled() {   // A/B switch: LGX_ACT_X3=0 keeps the f32 MFMA kernel for own launches
+  const char* e = getenv("LGX_ACT_X3");
   return e ? atoi(e) : 1;
 }
 
@@ -302,6 +309,15 @@ static int actuator_ws_enabled() {
 int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
                             hipStream_t stream, int wg_per_cu) {
   if (rows <= 0) return 0;
+  if (actuator_ws_enabled() && lgx_actuator_x3_enabled()) {
+    WsArgs wa{in, out, rows, w, out_scale};
+    const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int grid = (int)std::min<int64_t>(tiles, cus);
+    LGX_LAUNCH(lgx_actuator_x3_kernel, dim3(grid), dim3(256), 0, stream, wa);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+  }
   if (actuator_ws_enabled()) {
     WsArgs wa{in, out, rows, w, out_scale};
     const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
