@@ -198,6 +198,8 @@ class FusedPPOUpdate:
                 p.grad = self.flat_g[off:off + k].view_as(p)
                 off += k
         self.n = n
+        self.nW1 = self.off[id(la[1].weight)]   # end of the {actor, critic} layer-1 weight blocks
+        self.bucketed = False                     # (last minibatch: two all-reduce buckets)
         self.la, self.lc = la, lc
         self.W = []    # per layer k < L: stacked [2, out, in] weight view (k >= 1) or per-net views (k == 0)
         for k in range(self.L + 1):
@@ -770,6 +772,16 @@ class FusedPPOUpdate:
             self._side.wait_event(self._ev_in[0])
             chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
                                                C.c_void_p(self._side.cuda_stream)), "reduce")
+        bucketed = early and apply and ppo.dist is not None
+        self.bucketed = bucketed
+        if bucketed:
+            # data-parallel: the first gradient bucket (every block after dW1's in the layer-major
+            # flat layout + the KL slot) is all-reduced from the side stream as soon as it is
+            # reduced, concurrent with dW1's GEMM here; dW1's bucket follows below (one
+            # communicator: the collectives run in issue order on every rank)
+            with torch.cuda.stream(self._side):
+                self.g_comm[self.n:].copy_(self.stats[0:1])
+                ppo.dist.all_reduce(self.g_comm[self.nW1:])
         if 0 in self.gemm_dw and fused:     # lgx_gemm_tn over the minibatch's padded input rows
             t = self.gemm_dw[0]
             t[0].B = xp.data_ptr()
@@ -783,11 +795,15 @@ class FusedPPOUpdate:
         else:
             torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
             torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
-        if side_used:   # the weight gradients are complete before the reduction reads them
+        if side_used and not early:   # the weight gradients are complete before the reduction reads them
             self._ev_out.record(self._side)
             torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
-        if early:
+        if early:   # (dW1's partials come from this stream; the side stream's blocks are joined below)
             chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
+            if bucketed:
+                ppo.dist.all_reduce(self.g_comm[:self.nW1])
+            self._ev_out.record(self._side)
+            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
         elif self.loss_bwd:
             chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
         else:
@@ -796,10 +812,12 @@ class FusedPPOUpdate:
             return
         grad_scale = 1.0
         if ppo.dist is not None:
-            # one collective: summed gradient + summed KL (rsl_rl adapts the LR before the step,
-            # only the optimizer step reads it, so adapting after the backward is equivalent)
-            self.g_comm[self.n:].copy_(self.stats[0:1])
-            ppo.dist.all_reduce(self.g_comm)
+            # summed gradient + summed KL (rsl_rl adapts the LR before the step, only the optimizer
+            # step reads it, so adapting after the backward is equivalent): two buckets issued
+            # above, or one collective here
+            if not bucketed:
+                self.g_comm[self.n:].copy_(self.stats[0:1])
+                ppo.dist.all_reduce(self.g_comm)
             grad_scale = 1.0 / ppo.dist.get_world_size()
             if adaptive:
                 chk(lib.lgx_ppo_adapt_lr(C.c_void_p(self.g_comm.data_ptr() + 4 * self.n), grad_scale,

@@ -46,14 +46,18 @@ def _make(n_envs, sl):
     return ppo
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, early):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      LGX_PPO_EARLY_REDUCE=early)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ppo = _make(B, slice(rank * B, (rank + 1) * B))
         vl, sl = ppo.update()
+        # early reduction on: two gradient buckets, the first all-reduced from the side stream
+        # while dW1 runs; off: one collective after the whole backward
+        assert ppo._fused.bucketed == (early == "1")
         if rank == 0:
             q.put([p.detach().cpu().numpy() for p in ppo.actor_critic.parameters()] + [ppo.learning_rate])
         dist.barrier()
@@ -69,13 +73,14 @@ def _free_port():
     return p
 
 
-def test_fused_update_two_ranks_equal_one_process(gpu):
+@pytest.mark.parametrize("early", ["1", "0"])
+def test_fused_update_two_ranks_equal_one_process(gpu, early):
     ref = _make(2 * B, slice(0, 2 * B))
     ref.update()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, early)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=300)
