@@ -27,8 +27,8 @@ MI355X_F32_PEAK_TFLOPS = 157.3      # vector FP32 == f32 MFMA peak (MI355X_MICRO
 MI355X_HBM_PEAK_GBS = 8000.0
 # HBM bytes per launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts
 # half of wide reads), from the rocprofv3 --pmc passes of the same build (tools/pmc_round.sh ->
-# profiles/r01_pmc_env_kernels.json); the actuator net from the passes that launch it on its own
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_env_kernels.json")
+# profiles/r02_pmc_env_kernels.json); the actuator net from the passes that launch it on its own
+PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_env_kernels.json")
 
 
 def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
@@ -283,7 +283,16 @@ def main():
     if fused_act:
         # the actuator net shares the post-physics launch in the rollout; its own roofline is
         # measured on the same rows with the standalone launch (after the timed region)
+        # (the f32 body is the one the fused launch runs: LGX_ACT_X3=0 selects its standalone kernel)
+        prev = os.environ.get("LGX_ACT_X3")
+        os.environ["LGX_ACT_X3"] = "0"
         avg[1], launches = standalone_actuator_ms(lib, env, torch)
+        os.environ["LGX_ACT_X3"] = "1"
+        act_x3_ms, _ = standalone_actuator_ms(lib, env, torch)
+        if prev is None:
+            os.environ.pop("LGX_ACT_X3")
+        else:
+            os.environ["LGX_ACT_X3"] = prev
         act_note = (f"standalone lgx_actuator_ws_kernel on this step's model_ins rows, {launches} launches after the "
                     "timed region (in the rollout it runs on workgroups of lgx_post_physics_act_kernel)")
     decim = env.cfg.control.decimation
@@ -296,7 +305,7 @@ def main():
             "algorithmic_per_launch": phys_flop,
             "note": ("compute roof = FP32 peak (vector FP32 = f32 MFMA = 157.3 TF on gfx950); algorithmic FLOP "
                      "from legged_gym_amd/sim/flops.py x envs x substeps; traffic = FETCH_SIZE*2 + WRITE_SIZE "
-                     "per launch from profiles/r01_pmc_env_kernels.json (tools/pmc_round.sh); latency-bound, see DESIGN.md 4.1")}
+                     "per launch from profiles/r02_pmc_env_kernels.json (tools/pmc_round.sh); latency-bound, see DESIGN.md 4.1")}
     act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
     roof2 = {"kernel": "lgx_actuator_ws_kernel", "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
              "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None,
@@ -304,6 +313,11 @@ def main():
              "algorithmic_per_launch": act_flop}
     if act_note:
         roof2["note"] = act_note
+        # the split-bf16 actuator kernel of the serial / aux-stream modes, same rows
+        roof2["split_bf16_kernel"] = {
+            "kernel": "lgx_actuator_x3_kernel", "avg_ms": act_x3_ms, "peak": MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS,
+            "achieved": act_flop / (act_x3_ms * 1e-3) / 1e12 if act_x3_ms else None,
+            "frac": (act_flop / (act_x3_ms * 1e-3) / 1e12 / (MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS)) if act_x3_ms else None}
     for r in (roof, roof2):
         if r["achieved"] is not None:
             r["frac"] = r["achieved"] / r["peak"]

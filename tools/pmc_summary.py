@@ -1,5 +1,5 @@
 """Summarise rocprofv3 --pmc passes (gpurun_out/pmc/<pass>/run_counter_collection.csv) into the
-per-dispatch means JSON that bench.py reads (profiles/r01_pmc_env_kernels.json)."""
+per-dispatch means JSON that bench.py reads (profiles/r02_pmc_env_kernels.json)."""
 import csv
 import glob
 import json
@@ -9,7 +9,7 @@ import sys
 from collections import defaultdict
 
 src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_pmc_env_kernels.json"
+dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/r02_pmc_env_kernels.json"
 what = sys.argv[3] if len(sys.argv) > 3 else None
 out = {"what": what or "rocprofv3 --kernel-trace --pmc, per-dispatch means over tools/kbench.py physrun (go1_rough, "
                "4096 envs, 10 env steps); FETCH_SIZE/WRITE_SIZE in KB (gfx950: FETCH_SIZE reads half of wide "
