@@ -258,9 +258,10 @@ int lgx_reset_idx(lgx_sim* sim, const int32_t* env_ids, int32_t n, int64_t commo
 int lgx_set_draws(lgx_sim* sim, const float* draws);
 
 /* Go1 actuator MLP (UniNet, go1.py:22-35,100-105): rows of 30 inputs -> 3 outputs,
- * 30-128-128-128-3 tanh MLP on f32 MFMA.  w: packed [W0t b0 W1t b1 W2t b2 W3t b3] with
- * W_lt = transposed torch Linear weight ([in x out]).  out = net(in) * out_scale[col]
- * (dVel *= vel_std). */
+ * 30-128-128-128-3 tanh MLP, f32-accurate: split-bf16 MFMA (three bf16 limbs per operand, six
+ * limb products; LGX_ACT_X3=0 selects the f32-MFMA kernel).  w: packed [W0t b0 W1t b1 W2t b2
+ * W3t b3] with W_lt = transposed torch Linear weight ([in x out]).  out = net(in) *
+ * out_scale[col] (dVel *= vel_std). */
 int lgx_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
                      void* stream);
 
