@@ -1,6 +1,6 @@
-"""GPU: the fused PPO update (lgx PPO kernels + library GEMMs over flat buffers) against the
+"""GPU: the fused PPO update (lgx PPO kernels + hand-written GEMMs over flat buffers) against the
 autograd formulation of rsl_rl v1.0.x PPO.update (legged_gym_amd/rl/ppo.py, pinned on CPU by
-tests/test_ppo.py).
+tests/test_ppo.py) and against oracle/ppo_oracle.py (numpy float64, hand-derived gradients).
 
 Tolerances (float32; different reduction orders): minibatch gradient |d| <= 1e-5 + 2e-3 |g|;
 after a full update (2 epochs x 4 minibatches of Adam) identical learning-rate sequence, losses
@@ -300,3 +300,34 @@ def test_fused_rollout_act_and_store(gpu, monkeypatch, batched):
     ref_r = rew + fus.gamma * st.values[0, :, 0] * time_outs.float()
     assert torch.allclose(st.rewards[0, :, 0], ref_r, atol=1e-6, rtol=1e-6)
     assert torch.equal(st.dones[0, :, 0], dones.byte())
+
+
+def test_fused_minibatch_gradient_matches_numpy_oracle(gpu):
+    """The fused minibatch gradient (HIP kernels) against oracle/ppo_oracle.py's hand-derived
+    float64 gradient of rsl_rl's PPO loss (independent of torch autograd and of rl/ppo.py):
+    |d| <= 1e-5 + 2e-3 |g|, losses to 1e-4."""
+    from ppo_oracle_io import oracle_minibatch_grads, grad_deviation
+    _, fus = make_pair()
+    idx = torch.randperm(T * N, device="cuda:0", generator=torch.Generator(device="cuda:0").manual_seed(8))[: T * N // 4]
+    fus._fused.gradients(idx)
+    want = oracle_minibatch_grads(fus, idx)
+    worst, name = grad_deviation(fus.actor_critic, want[3], rtol=2e-3)
+    assert worst <= 1.0, (worst, name)
+
+
+@pytest.mark.parametrize("schedule", ["adaptive", "fixed"])
+def test_fused_update_matches_numpy_oracle(gpu, schedule):
+    """A full fused update (2 epochs x 4 minibatches, Adam, adaptive or fixed learning rate)
+    against the oracle's float64 update from the same parameters, storage and permutation:
+    same learning-rate sequence, losses to 1e-4, parameters within the rule of the
+    fused-vs-autograd test."""
+    from ppo_oracle_io import oracle_update, param_deviation
+    _, fus = make_pair(schedule)
+    want = oracle_update(fus, seed=13)
+    torch.manual_seed(13)
+    vl, sl = fus.update()
+    assert fus.learning_rate == pytest.approx(want[3], rel=1e-9)
+    assert abs(vl - want[4]) <= 1e-4 * abs(want[4]) + 1e-6 and abs(sl - want[5]) <= 1e-4 * abs(want[5]) + 1e-6
+    dmax, big, total = param_deviation(fus.actor_critic, want)
+    assert dmax <= 2 * 8 * 1e-3, dmax
+    assert big <= 1e-3 * total, (big, total)

@@ -93,6 +93,91 @@ def test_update_runs_and_adapts_lr():
     assert any(not torch.equal(a, b) for a, b in zip(p0, alg.actor_critic.parameters()))
 
 
+@pytest.mark.parametrize("schedule,sigma,clipped_v,mbs", [("adaptive", 1.0, True, 2), ("adaptive", 0.1, True, 2),
+                                                          ("fixed", 1.0, False, 3)])
+def test_update_matches_numpy_oracle(schedule, sigma, clipped_v, mbs):
+    """PPO.update (autograd, CPU float32) against oracle/ppo_oracle.py, the hand-differentiated
+    numpy float64 restatement of rsl_rl's PPO.update (minibatch order, clipped surrogate /
+    value loss, entropy, adaptive KL learning rate, clip_grad_norm_, Adam).  sigma 0.1: the
+    rollout's std far from the policy's -> the learning rate falls at every minibatch."""
+    from ppo_oracle_io import oracle_update, param_deviation
+    alg = make_alg(2 * B, epochs=2, mbs=mbs)
+    alg.schedule = schedule
+    alg.use_clipped_value_loss = clipped_v
+    fill(alg.storage, None, 2 * B)
+    alg.storage.sigma.fill_(sigma)
+    alg.storage.compute_returns(torch.randn(2 * B, 1, generator=torch.Generator().manual_seed(5)), 0.99, 0.95)
+    want = oracle_update(alg, seed=21)
+    torch.manual_seed(21)
+    vl, sl = alg.update()
+    assert alg.learning_rate == pytest.approx(want[3], rel=1e-12)
+    assert vl == pytest.approx(want[4], rel=1e-5, abs=1e-7) and sl == pytest.approx(want[5], rel=1e-5, abs=1e-7)
+    dmax, big, total = param_deviation(alg.actor_critic, want)
+    n_steps = 2 * mbs
+    assert dmax <= 2 * n_steps * 1e-3, dmax
+    assert big <= max(2, 1e-3 * total), (big, total)
+
+
+def test_update_matches_numpy_oracle_policy_widths():
+    """The same at the go1_rough policy widths (235 -> 512 -> 256 -> 128 -> 12 / 1), 2 epochs x 4
+    minibatches: at this size the value-clipping branches include in-range rows where rounding
+    makes tv + (v - tv) != v (torch routes the whole gradient through the larger branch)."""
+    from ppo_oracle_io import oracle_update, param_deviation
+    Tn, Nn, obs_n, act_n = 4, 96, 235, 12
+    torch.manual_seed(0)
+    ac = ActorCritic(obs_n, obs_n, act_n, [512, 256, 128], [512, 256, 128])
+    alg = PPO(ac, num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95, value_loss_coef=1.0,
+              entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0, schedule="adaptive", desired_kl=0.01,
+              device="cpu")
+    alg.init_storage(Nn, Tn, [obs_n], [None], [act_n])
+    g = torch.Generator().manual_seed(3)
+    st = alg.storage
+    st.observations.copy_(torch.randn(Tn, Nn, obs_n, generator=g))
+    st.actions.copy_(torch.randn(Tn, Nn, act_n, generator=g))
+    st.rewards.copy_(torch.randn(Tn, Nn, 1, generator=g))
+    st.dones.copy_((torch.rand(Tn, Nn, 1, generator=g) < 0.1).byte())
+    st.values.copy_(torch.randn(Tn, Nn, 1, generator=g))
+    st.actions_log_prob.copy_(torch.randn(Tn, Nn, 1, generator=g) * 0.3 - 17)
+    st.mu.copy_(torch.randn(Tn, Nn, act_n, generator=g) * 0.1)
+    st.sigma.copy_(torch.rand(Tn, Nn, act_n, generator=g) * 0.5 + 0.75)
+    st.step = Tn
+    st.compute_returns(torch.randn(Nn, 1, generator=g), 0.99, 0.95)
+    want = oracle_update(alg, seed=13)
+    torch.manual_seed(13)
+    vl, sl = alg.update()
+    assert alg.learning_rate == pytest.approx(want[3], rel=1e-12)
+    assert vl == pytest.approx(want[4], rel=1e-5) and sl == pytest.approx(want[5], rel=1e-5)
+    dmax, big, total = param_deviation(alg.actor_critic, want)
+    assert dmax <= 2 * 8 * 1e-3, dmax
+    assert big <= 1e-3 * total, (big, total)
+
+
+def test_minibatch_gradient_matches_numpy_oracle():
+    """d loss / d parameters of one minibatch (autograd, CPU float32) against the oracle's
+    hand-derived float64 gradient: |d| <= 1e-5 + 1e-4 |g|."""
+    from ppo_oracle_io import oracle_minibatch_grads, grad_deviation
+    alg = make_alg(2 * B, epochs=1, mbs=2)
+    fill(alg.storage, None, 2 * B)
+    alg.storage.compute_returns(torch.randn(2 * B, 1, generator=torch.Generator().manual_seed(5)), 0.99, 0.95)
+    idx = torch.randperm(T * 2 * B, generator=torch.Generator().manual_seed(4))[: T * B]
+    st, ac = alg.storage, alg.actor_critic
+    Bf = T * 2 * B
+    ac.act(st.observations.view(Bf, -1)[idx])
+    logp = ac.get_actions_log_prob(st.actions.view(Bf, -1)[idx])
+    value = ac.evaluate(st.observations.view(Bf, -1)[idx])
+    ratio = torch.exp(logp - st.actions_log_prob.view(Bf)[idx])
+    adv = st.advantages.view(Bf)[idx]
+    s_loss = torch.max(-adv * ratio, -adv * torch.clamp(ratio, 0.8, 1.2)).mean()
+    tv, ret = st.values.view(Bf, 1)[idx], st.returns.view(Bf, 1)[idx]
+    vc = tv + (value - tv).clamp(-0.2, 0.2)
+    v_loss = torch.max((value - ret).pow(2), (vc - ret).pow(2)).mean()
+    (s_loss + v_loss - 0.01 * ac.entropy.mean()).backward()
+    want = oracle_minibatch_grads(alg, idx)
+    assert float(v_loss) == pytest.approx(want[0], rel=1e-5) and float(s_loss) == pytest.approx(want[1], rel=1e-5)
+    worst, name = grad_deviation(ac, want[3], rtol=1e-4)
+    assert worst <= 1.0, (worst, name)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
