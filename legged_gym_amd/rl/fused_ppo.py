@@ -24,6 +24,7 @@ state_dict has torch.optim.Adam's format (checkpoints stay loadable by upstream 
 """
 import ctypes as C
 import os
+import time
 
 import torch
 import torch.nn as nn
@@ -494,6 +495,7 @@ class FusedPPOUpdate:
     # ------------------------------------------------------------------ update
     @torch.no_grad()
     def update(self):
+        t_issue = time.perf_counter()
         ppo = self.ppo
         st = ppo.storage
         T, N = st.num_transitions_per_env, st.num_envs
@@ -532,6 +534,7 @@ class FusedPPOUpdate:
                     mx = tuple(x[i * M:(i + 1) * M] if x is not None else None for x in xs)
                 self._minibatch(idx, obs, cobs, args, stream, xs=mx)
         n = ppo.num_learning_epochs * nmb
+        self.host_issue_s = time.perf_counter() - t_issue   # host time to issue every launch (tools/host_overhead.py)
         s = self.stats.tolist()   # the one host synchronisation of the update
         lr = float(self.optimizer.lr_dev.item())
         if ppo.desired_kl is not None and ppo.schedule == "adaptive":

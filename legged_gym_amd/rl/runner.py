@@ -66,10 +66,16 @@ class OnPolicyRunner:
         lenbuffer = deque(maxlen=100)
         cur_reward_sum = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
         cur_episode_length = torch.zeros(self.env.num_envs, dtype=torch.float, device=self.device)
-        sync = torch.cuda.synchronize if str(self.device).startswith("cuda") else (lambda: None)
+        # Phase times on CUDA come from stream events read after update(), whose statistics readback
+        # already waits for the stream: no extra host synchronisation between the rollout and the
+        # update (upstream rsl_rl likewise times with time.time() and no sync).
+        cuda = str(self.device).startswith("cuda")
         tot_iter = self.current_learning_iteration + num_learning_iterations
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
+            if cuda:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                ev[0].record()
             with torch.inference_mode():
                 for _ in range(self.num_steps_per_env):
                     actions = self.alg.act(obs, critic_obs)
@@ -88,15 +94,20 @@ class OnPolicyRunner:
                         lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
                         cur_reward_sum[new_ids] = 0
                         cur_episode_length[new_ids] = 0
-                sync()
+                if cuda:
+                    ev[1].record()
                 stop = time.time()
                 collection_time = stop - start
                 start = stop
                 self.alg.compute_returns(critic_obs)
             mean_value_loss, mean_surrogate_loss = self.alg.update()
-            sync()
             stop = time.time()
             learn_time = stop - start
+            if cuda:
+                ev[2].record()
+                ev[2].synchronize()
+                collection_time = ev[0].elapsed_time(ev[1]) * 1e-3
+                learn_time = ev[1].elapsed_time(ev[2]) * 1e-3
             self.last_iteration_stats = dict(collection_time=collection_time, learn_time=learn_time,
                                              value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
                                              learning_rate=self.alg.learning_rate)

@@ -38,3 +38,22 @@ for rep in range(3):
     t2 = time.perf_counter()
     print(f"rep {rep}: host {host / 24 * 1e6:.1f} us/step (loop returned after {(t1 - t0) / 24 * 1e6:.1f} us/step), "
           f"wall incl. drain {(t2 - t0) / 24 * 1e6:.1f} us/step", flush=True)
+
+# The update: host time to issue every launch of the 20 minibatches vs the update's wall time
+# (which ends with the statistics readback, i.e. when the GPU has drained).  Issue time close to
+# the wall time means the learn phase is launch-bound.
+fused = getattr(alg, "_fused", None)
+if fused is not None:
+    for rep in range(3):
+        alg.storage.clear()
+        with torch.inference_mode():
+            for _ in range(24):
+                a = alg.act(obs, obs)
+                obs, _, rew, dones, infos = env.step(a)
+                alg.process_env_step(rew, dones, infos)
+            alg.compute_returns(obs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        alg.update()
+        t1 = time.perf_counter()
+        print(f"update rep {rep}: host issue {fused.host_issue_s * 1e3:.2f} ms, wall {(t1 - t0) * 1e3:.2f} ms", flush=True)
