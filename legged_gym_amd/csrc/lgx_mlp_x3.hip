@@ -42,6 +42,7 @@ constexpr int XM_LDS_MAX = 160 * 1024;
 __host__ __device__ inline int xm_kp(int k) { return (k + 63) & ~63; }         // padded width (image / weight K)
 __host__ __device__ inline int xm_rs(int k) { return xm_kp(k) * 2 + 16; }       // image row stride, bytes
 __host__ __device__ inline int xm_img(int k) { return 3 * XM_BM * xm_rs(k); }   // limb image bytes
+__host__ __device__ inline int xm_bp(int n) { return (n + 31) & ~31; }         // bias floats of a layer in LDS
 
 struct XmNet {
   const float* x;
@@ -55,6 +56,7 @@ struct XmNet {
 struct XmBatch {
   XmNet m[2];
   int32_t region;   // byte offset of the second image region (the first at 0)
+  int32_t bias_region;   // byte offset of the biases (each layer's zero-padded to 32 columns)
 };
 
 // three RNE bf16 limbs of two floats, packed (low half = first element); both subtractions exact
@@ -73,27 +75,52 @@ __device__ __forceinline__ float xm_act(float v, int act) {
   return v;
 }
 
-// One layer's products for the TPW column blocks of this wave: acc[t] (+)= W[cb_t] . X over KB
-// k blocks of 16 (KB % 4 == 0).  G k blocks per load group, two groups of B fragments in flight.
+// One load group of a wave's weight fragments: G = 4 / TPW k blocks x TPW column blocks x 3 limbs
+// (12 registers of 16 bytes for TPW 1 or 2), k blocks kb0 .. kb0 + G - 1
+constexpr int XM_PF = 12;
+
 template <int TPW>
-__device__ __forceinline__ void xm_layer(const char* __restrict__ img, int rs, const char* __restrict__ W, int KB,
-                                         int wave, int lane, f32x16 (&acc)[2]) {
+__device__ __forceinline__ void xm_load(bf16x8 (&b)[XM_PF], const char* __restrict__ W, int KB, int kb0, int wave,
+                                        int lane) {
   constexpr int G = 4 / TPW;
   const int lo = (lane & 31) * 32 + (lane >> 5) * 16;     // B fragment lane offset in a 1 KB limb block
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t)
+#pragma unroll
+      for (int l = 0; l < 3; ++l)
+        b[(g * TPW + t) * 3 + l] = *reinterpret_cast<const bf16x8*>(
+            W + ((int64_t)((wave + XM_NW * t) * KB + kb0 + g) * 3 + l) * 1024 + lo);
+}
+
+// column blocks of this wave in a layer of N outputs (wave w owns blocks w, w + 8; N <= 512)
+__device__ __forceinline__ int xm_tpw(int N, int wave) {
+  const int ncb = (N + 31) / 32;
+  return wave < ncb ? (ncb - wave + XM_NW - 1) / XM_NW : 0;
+}
+
+// Layer l's first load group, issued ahead of the work before its products (the input staging for
+// layer 0, the previous layer's epilogue and barrier otherwise): the weights do not depend on the
+// activations, so the L2 latency of each layer's first fragments hides under that work.
+__device__ __forceinline__ void xm_prefetch(bf16x8 (&b)[XM_PF], const XmNet& a, int l, int wave, int lane) {
+  const int tpw = xm_tpw(a.dims[l + 1], wave), KB = xm_kp(a.dims[l]) / 16;
+  const char* W = reinterpret_cast<const char*>(a.w[l]);
+  if (tpw == 2) xm_load<2>(b, W, KB, 0, wave, lane);
+  else if (tpw == 1) xm_load<1>(b, W, KB, 0, wave, lane);
+}
+
+// One layer's products for the TPW column blocks of this wave: acc[t] (+)= W[cb_t] . X over KB
+// k blocks of 16 (KB % 4 == 0).  G k blocks per load group, two groups of B fragments in flight;
+// bA arrives holding group 0 (xm_prefetch).
+template <int TPW>
+__device__ __forceinline__ void xm_layer(const char* __restrict__ img, int rs, const char* __restrict__ W, int KB,
+                                         int wave, int lane, f32x16 (&acc)[2], bf16x8 (&bA)[XM_PF]) {
+  constexpr int G = 4 / TPW;
   const int ao = (lane & 31) * rs + (lane >> 5) * 16;     // A fragment lane offset in an image limb
   const int limb_bytes = XM_BM * rs;
-  bf16x8 bA[G][TPW][3], bB[G][TPW][3];
-  auto load = [&](bf16x8 (&b)[G][TPW][3], int kb0) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int t = 0; t < TPW; ++t)
-#pragma unroll
-        for (int l = 0; l < 3; ++l)
-          b[g][t][l] = *reinterpret_cast<const bf16x8*>(
-              W + ((int64_t)((wave + XM_NW * t) * KB + kb0 + g) * 3 + l) * 1024 + lo);
-  };
-  auto compute = [&](const bf16x8 (&b)[G][TPW][3], int kb0) {
+  bf16x8 bB[XM_PF];
+  auto compute = [&](const bf16x8 (&b)[XM_PF], int kb0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       const char* pa = img + ao + (kb0 + g) * 32;
@@ -102,23 +129,23 @@ __device__ __forceinline__ void xm_layer(const char* __restrict__ img, int rs, c
       const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(pa + 2 * limb_bytes);
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
+        const bf16x8* w = b + (g * TPW + t) * 3;
         f32x16 c = acc[t];   // small limb products first
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][2], a0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][1], a1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][0], a2, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][1], a0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][0], a1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(b[g][t][0], a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a2, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a1, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a0, c, 0, 0, 0);
         acc[t] = c;
       }
     }
   };
-  load(bA, 0);
   for (int kb0 = 0; kb0 < KB; kb0 += 2 * G) {
-    if (kb0 + G < KB) load(bB, kb0 + G);
+    if (kb0 + G < KB) xm_load<TPW>(bB, W, KB, kb0 + G, wave, lane);
     compute(bA, kb0);
     if (kb0 + G >= KB) break;
-    if (kb0 + 2 * G < KB) load(bA, kb0 + 2 * G);
+    if (kb0 + 2 * G < KB) xm_load<TPW>(bA, W, KB, kb0 + 2 * G, wave, lane);
     compute(bB, kb0 + G);
   }
 }
@@ -136,29 +163,58 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
   if (r0 >= a.rows) return;   // (the other network of the launch may have more rows)
   char* const img0 = xm_lds;
   char* const img1 = xm_lds + batch.region;
+  float* const bias_lds = reinterpret_cast<float*>(xm_lds + batch.bias_region);
   LGX_CLK_DECL(8)
-  // ---- input rows -> limb image 0 (zero rows past M, zero columns past K0)
+  bf16x8 pre[XM_PF];   // the next layer's first weight load group (xm_prefetch)
+  xm_prefetch(pre, a, 0, wave, lane);
+  // biases -> LDS (read by the epilogues, not held in registers across the products): this
+  // thread's XM_BU entries of the concatenated zero-padded bias rows, loaded with the input rows
+  float bvals[XM_MAXL];   // entry tid of each layer's bias row (XM_MAXW <= XM_NT)
+  static_assert(XM_MAXW <= XM_NT, "one bias entry per thread and layer");
+#pragma unroll
+  for (int l = 0; l < XM_MAXL; ++l) bvals[l] = l < a.nl && tid < a.dims[l + 1] ? a.b[l][tid] : 0.f;
+  // ---- input rows -> limb image 0 (zero rows past M, zero columns past K0); XM_SU pairs per
+  // thread loaded before any is split, so their HBM latencies overlap
   {
-    const int K0 = a.dims[0], rs = xm_rs(K0), pairs = xm_kp(K0) / 2;
-    for (int i = tid; i < XM_BM * pairs; i += XM_NT) {
-      const int row = i / pairs, k = 2 * (i - row * pairs);
-      const int64_t gr = r0 + row;
-      float v0 = 0.f, v1 = 0.f;
-      if (gr < a.rows) {
-        if (k < K0) v0 = a.x[gr * K0 + k];
-        if (k + 1 < K0) v1 = a.x[gr * K0 + k + 1];
+    constexpr int XM_SU = 8;
+    const int K0 = a.dims[0], rs = xm_rs(K0), pairs = xm_kp(K0) / 2, total = XM_BM * pairs;
+    for (int base = 0; base < total; base += XM_SU * XM_NT) {
+      float v[XM_SU][2];
+#pragma unroll
+      for (int u = 0; u < XM_SU; ++u) {
+        const int i = base + u * XM_NT + tid;
+        const int row = i / pairs, k = 2 * (i - row * pairs);
+        const int64_t gr = r0 + row;
+        const bool in = i < total && gr < a.rows;
+        v[u][0] = in && k < K0 ? a.x[gr * K0 + k] : 0.f;
+        v[u][1] = in && k + 1 < K0 ? a.x[gr * K0 + k + 1] : 0.f;
       }
-      uint32_t l0, l1, l2;
-      split2(v0, v1, l0, l1, l2);
-      char* p = img0 + row * rs + 2 * k;
-      *reinterpret_cast<uint32_t*>(p) = l0;
-      *reinterpret_cast<uint32_t*>(p + XM_BM * rs) = l1;
-      *reinterpret_cast<uint32_t*>(p + 2 * XM_BM * rs) = l2;
+#pragma unroll
+      for (int u = 0; u < XM_SU; ++u) {
+        const int i = base + u * XM_NT + tid;
+        if (i < total) {
+          const int row = i / pairs, k = 2 * (i - row * pairs);
+          uint32_t l0, l1, l2;
+          split2(v[u][0], v[u][1], l0, l1, l2);
+          char* p = img0 + row * rs + 2 * k;
+          *reinterpret_cast<uint32_t*>(p) = l0;
+          *reinterpret_cast<uint32_t*>(p + XM_BM * rs) = l1;
+          *reinterpret_cast<uint32_t*>(p + 2 * XM_BM * rs) = l2;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int l = 0, off = 0; l < XM_MAXL; ++l) {
+    if (l < a.nl) {
+      if (tid < xm_bp(a.dims[l + 1])) bias_lds[off + tid] = bvals[l];
+      off += xm_bp(a.dims[l + 1]);
     }
   }
   LGX_CLK(0);
   __syncthreads();
   LGX_CLK(1);
+  int boff = 0;   // layer l's bias offset in bias_lds
   const int row = lane & 31, h = lane >> 5;
   for (int l = 0; l < a.nl; ++l) {
     const int K = a.dims[l], N = a.dims[l + 1];
@@ -166,28 +222,16 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
     const char* in = (l & 1) ? img1 : img0;
     char* out = (l & 1) ? img0 : img1;
     const int ncb = (N + 31) / 32;
-    const int tpw = wave < ncb ? (ncb - wave + XM_NW - 1) / XM_NW : 0;   // column blocks of this wave
+    const int tpw = xm_tpw(N, wave);   // column blocks of this wave
     f32x16 acc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
     const char* W = reinterpret_cast<const char*>(a.w[l]);
-    // this lane's bias values, loaded before the products so their latency hides under them
-    // (clamped index + mask: no branch, no wait inside the epilogue)
-    const float* bias = a.b[l];
-    float bv[2][4][4];
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int c = (wave + XM_NW * t) * 32 + 8 * q + 4 * h + i;
-          bv[t][q][i] = bias[min(c, N - 1)];
-        }
-    if (tpw == 2) xm_layer<2>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc);
-    else if (tpw == 1) xm_layer<1>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc);
+    if (tpw == 2) xm_layer<2>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc, pre);
+    else if (tpw == 1) xm_layer<1>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc, pre);
+    if (!last) xm_prefetch(pre, a, l + 1, wave, lane);
     LGX_CLK(2 + (l < 3 ? l : 2));
     // epilogue: lane holds row `row`, columns cb*32 + 8q + 4h + (0..3) in acc[t][4q .. 4q+3]
     const int rs_out = xm_rs(N);
@@ -199,8 +243,11 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
       for (int q = 0; q < 4; ++q) {
         const int c0 = cb * 32 + 8 * q + 4 * h;
         float v[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[t][4 * q + i] + (c0 + i < N ? bv[t][q][i] : 0.f);
+        const float4 bq = *reinterpret_cast<const float4*>(bias_lds + boff + c0);   // (zero past N)
+        v[0] = acc[t][4 * q] + bq.x;
+        v[1] = acc[t][4 * q + 1] + bq.y;
+        v[2] = acc[t][4 * q + 2] + bq.z;
+        v[3] = acc[t][4 * q + 3] + bq.w;
         if (!last) {   // padding columns: zero weights and bias -> act(0) = 0
 #pragma unroll
           for (int i = 0; i < 4; ++i) v[i] = xm_act(v[i], a.act);
@@ -229,6 +276,7 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
         *reinterpret_cast<uint32_t*>(out + lr * rs_out + 2 * k) = 0u;
       }
     }
+    boff += xm_bp(N);
     LGX_CLK(5);
     __syncthreads();   // the output image is complete; the input region is free for the next layer
     LGX_CLK(6);
@@ -256,13 +304,16 @@ __global__ void __launch_bounds__(256) xm_split_kernel(const float* __restrict__
   d[512] = l2;
 }
 
-int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region) {
-  int64_t r0 = 0, r1 = 0;
+int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region, int32_t* bias_region = nullptr) {
+  int64_t r0 = 0, r1 = 0, rb = 0;
   for (int i = 0; i < count; ++i) {
     const lgx_mlp_x3_desc& m = d[i];
     if (m.nl < 1 || m.nl > XM_MAXL || m.rows < 0 || m.act < 0 || m.act > 2) return -1;
     for (int l = 0; l <= m.nl; ++l)
       if (m.dims[l] <= 0 || m.dims[l] > XM_MAXW) return -1;
+    int64_t bb = 0;
+    for (int l = 0; l < m.nl; ++l) bb += 4 * xm_bp(m.dims[l + 1]);
+    rb = std::max(rb, bb);
     for (int l = 0; l < m.nl; ++l) {   // the image of width dims[l] lives in region l & 1
       const int64_t b = xm_img(m.dims[l]);
       if (l & 1) r1 = std::max(r1, b);
@@ -270,7 +321,8 @@ int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region) {
     }
   }
   if (region) *region = (int32_t)r0;
-  return r0 + r1 <= XM_LDS_MAX ? r0 + r1 : -1;
+  if (bias_region) *bias_region = (int32_t)(r0 + r1);
+  return r0 + r1 + rb <= XM_LDS_MAX ? r0 + r1 + rb : -1;
 }
 
 }  // namespace
@@ -297,7 +349,7 @@ extern "C" int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* d, int32_t count)
 extern "C" int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* d, int32_t count, void* stream) {
   if (!d || count < 1 || count > 2) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: count must be 1 or 2");
   XmBatch b{};
-  const int64_t lds = lds_bytes(d, count, &b.region);
+  const int64_t lds = lds_bytes(d, count, &b.region, &b.bias_region);
   if (lds < 0) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: bad dims or activations exceed the LDS (160 KB)");
   int64_t rows = 0;
   for (int i = 0; i < count; ++i) {
