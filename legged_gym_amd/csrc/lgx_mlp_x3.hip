@@ -172,7 +172,12 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
   float bvals[XM_MAXL];   // entry tid of each layer's bias row (XM_MAXW <= XM_NT)
   static_assert(XM_MAXW <= XM_NT, "one bias entry per thread and layer");
 #pragma unroll
-  for (int l = 0; l < XM_MAXL; ++l) bvals[l] = l < a.nl && tid < a.dims[l + 1] ? a.b[l][tid] : 0.f;
+  for (int l = 0; l < XM_MAXL; ++l) {   // clamped, unconditional loads (a per-lane load condition
+    if (l < a.nl) {                         // costs a vmcnt(0) round trip per load; §4 of DESIGN.md)
+      const float b = a.b[l][min(tid, a.dims[l + 1] - 1)];
+      bvals[l] = tid < a.dims[l + 1] ? b : 0.f;
+    }
+  }
   // ---- input rows -> limb image 0 (zero rows past M, zero columns past K0); XM_SU pairs per
   // thread loaded before any is split, so their HBM latencies overlap
   {
@@ -186,8 +191,11 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
         const int row = i / pairs, k = 2 * (i - row * pairs);
         const int64_t gr = r0 + row;
         const bool in = i < total && gr < a.rows;
-        v[u][0] = in && k < K0 ? a.x[gr * K0 + k] : 0.f;
-        v[u][1] = in && k + 1 < K0 ? a.x[gr * K0 + k + 1] : 0.f;
+        // clamped, always-valid addresses loaded unconditionally, padding zeroed afterwards
+        const int64_t gc = std::min<int64_t>(gr, a.rows - 1) * K0;
+        const float x0 = a.x[gc + std::min(k, K0 - 1)], x1 = a.x[gc + std::min(k + 1, K0 - 1)];
+        v[u][0] = in && k < K0 ? x0 : 0.f;
+        v[u][1] = in && k + 1 < K0 ? x1 : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < XM_SU; ++u) {

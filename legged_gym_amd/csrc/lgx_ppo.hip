@@ -721,30 +721,14 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin,
 
 // ---------------------------------------------------------------------------------------- clip + Adam
 // stage 1: per-block sums of squares of (scale * g); block 0 also advances the step counter
-// VEC: g 16-byte aligned, read as float4 (the scalar tail past the last whole float4 by block 0)
-template <bool VEC>
 __global__ void __launch_bounds__(TPB)
 sumsq_kernel(const float* __restrict__ g, int64_t n, float scale, float* __restrict__ partials,
              int64_t* __restrict__ step) {
   __shared__ float red[TPB];
   float s = 0.f;
-  if (VEC) {
-    const int64_t nv = n >> 2;
-    const float4* g4 = reinterpret_cast<const float4*>(g);
-    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < nv; i += (int64_t)gridDim.x * TPB) {
-      const float4 q = g4[i];
-      const float a = q.x * scale, b = q.y * scale, c = q.z * scale, d = q.w * scale;
-      s += a * a + b * b + c * c + d * d;
-    }
-    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
-      const float v = g[4 * nv + threadIdx.x] * scale;
-      s += v * v;
-    }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
-      float v = g[i] * scale;
-      s += v * v;
-    }
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    float v = g[i] * scale;
+    s += v * v;
   }
   red[threadIdx.x] = s;
   __syncthreads();
@@ -799,25 +783,9 @@ __device__ __forceinline__ void mirror_store(const Mirror& J, int32_t b, int32_t
   }
 }
 
-// the mirror copies of updated parameter i
-__device__ __forceinline__ void mirror_all(const Mirrors& mir, int64_t i, float pi) {
-  for (int q = 0; q < mir.n; ++q) {
-    const Mirror& J = mir.mj[q];
-    const uint64_t li = (uint64_t)(i - J.off);
-    if (li < (uint64_t)J.count) {
-      const int32_t l = (int32_t)li, rc = J.rows * J.cols;
-      const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
-      mirror_store(J, b, rr, cc, pi);
-    }
-  }
-}
-
-// One parameter per thread, or (VEC: p, g, m, v 16-byte aligned) four consecutive parameters per
-// thread with float4 loads and stores, so one pass of the grid covers every parameter;
-// consecutive lanes hold consecutive elements (a non-transposed limb mirror's 2-byte stores
-// coalesce). The clip coefficient and the bias corrections (double pow) computed once per
-// workgroup.
-template <bool VEC>
+// One parameter per thread (consecutive lanes: consecutive elements, so a non-transposed limb
+// mirror's 2-byte stores coalesce); the clip coefficient and the bias corrections (double pow)
+// computed once per workgroup.
 __global__ void __launch_bounds__(TPB)
 adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m, float* __restrict__ v, int64_t n,
                  const float* __restrict__ partials, int32_t nparts, float grad_scale, float max_norm,
@@ -845,79 +813,26 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
   }
   __syncthreads();
   const float coef = coef_s, step_size = step_size_s, bc2_sqrt = bc2_sqrt_s;
-  // torch Adam on one element (g scaled by the clip coefficient in place)
-  auto upd = [&](float& gi, float& mi, float& vi, float& pi) {
-    gi *= coef;
-    mi = beta1 * mi + (1.f - beta1) * gi;
-    vi = beta2 * vi + (1.f - beta2) * gi * gi;
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
+    const float gi = g[i] * coef;
+    g[i] = gi;
+    const float mi = beta1 * m[i] + (1.f - beta1) * gi;
+    const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi = pi - step_size * mi / denom;
-  };
-  if (VEC) {
-    const int64_t nv = (n + 3) >> 2;
-    for (int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x; t < nv; t += (int64_t)gridDim.x * TPB) {
-      const int64_t i0 = 4 * t;
-      if (i0 + 4 <= n) {
-        float4 g4 = reinterpret_cast<const float4*>(g)[t], m4 = reinterpret_cast<const float4*>(m)[t];
-        float4 v4 = reinterpret_cast<const float4*>(v)[t], p4 = reinterpret_cast<const float4*>(p)[t];
-        upd(g4.x, m4.x, v4.x, p4.x);
-        upd(g4.y, m4.y, v4.y, p4.y);
-        upd(g4.z, m4.z, v4.z, p4.z);
-        upd(g4.w, m4.w, v4.w, p4.w);
-        reinterpret_cast<float4*>(g)[t] = g4;
-        reinterpret_cast<float4*>(m)[t] = m4;
-        reinterpret_cast<float4*>(v)[t] = v4;
-        reinterpret_cast<float4*>(p)[t] = p4;
-        if (mir.n) {
-          mirror_all(mir, i0, p4.x);
-          mirror_all(mir, i0 + 1, p4.y);
-          mirror_all(mir, i0 + 2, p4.z);
-          mirror_all(mir, i0 + 3, p4.w);
-        }
-      } else {
-        for (int64_t i = i0; i < n; ++i) {
-          float gi = g[i], mi = m[i], vi = v[i], pi = p[i];
-          upd(gi, mi, vi, pi);
-          g[i] = gi;
-          m[i] = mi;
-          v[i] = vi;
-          p[i] = pi;
-          mirror_all(mir, i, pi);
-        }
+    const float pi = p[i] - step_size * mi / denom;
+    p[i] = pi;
+    for (int q = 0; q < mir.n; ++q) {
+      const Mirror& J = mir.mj[q];
+      const uint64_t li = (uint64_t)(i - J.off);
+      if (li < (uint64_t)J.count) {
+        const int32_t l = (int32_t)li, rc = J.rows * J.cols;
+        const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
+        mirror_store(J, b, rr, cc, pi);
       }
     }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
-      float gi = g[i], mi = m[i], vi = v[i], pi = p[i];
-      upd(gi, mi, vi, pi);
-      g[i] = gi;
-      m[i] = mi;
-      v[i] = vi;
-      p[i] = pi;
-      mirror_all(mir, i, pi);
-    }
   }
-}
-
-// both kernels of one clipped Adam step (sum of squares, then the update), float4 forms when
-// every array is 16-byte aligned
-int adam_launch(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts, float grad_scale,
-                float max_norm, const double* lr, int64_t* step, float beta1, float beta2, float eps,
-                const Mirrors& mir, hipStream_t stream) {
-  const bool vec = ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
-                     reinterpret_cast<uintptr_t>(m) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
-  if (vec) {
-    hipLaunchKernelGGL(sumsq_kernel<true>, dim3(nparts), dim3(TPB), 0, stream, g, n, grad_scale, partials, step);
-    const int blocks = (int)std::min<int64_t>(((n + 3) / 4 + TPB - 1) / TPB, 4096);
-    hipLaunchKernelGGL(adam_clip_kernel<true>, dim3(blocks), dim3(TPB), 0, stream, p, g, m, v, n, partials, nparts,
-                       grad_scale, max_norm, lr, step, beta1, beta2, eps, mir);
-  } else {
-    hipLaunchKernelGGL(sumsq_kernel<false>, dim3(nparts), dim3(TPB), 0, stream, g, n, grad_scale, partials, step);
-    const int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
-    hipLaunchKernelGGL(adam_clip_kernel<false>, dim3(blocks), dim3(TPB), 0, stream, p, g, m, v, n, partials, nparts,
-                       grad_scale, max_norm, lr, step, beta1, beta2, eps, mir);
-  }
-  return LGX_OK;
 }
 
 }  // namespace
@@ -1141,9 +1056,11 @@ extern "C" int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, 
                              float beta2, float eps, void* stream) {
   if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 || nparts > 1024)
     return lgx_fail(LGX_EINVAL, "lgx_adam_clip: bad args");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
+  int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
   Mirrors none{};
-  adam_launch(p, g, m, v, n, partials, nparts, grad_scale, max_norm, lr, step, beta1, beta2, eps, none,
-              LGX_STREAM(stream));
+  hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
+                     grad_scale, max_norm, lr, step, beta1, beta2, eps, none);
   return lgx_hip_status("lgx_adam_clip");
 }
 
@@ -1167,7 +1084,9 @@ extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int6
       return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: a limb mirror needs output rows % 128 == 0");
     M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose};
   }
-  adam_launch(p, g, m, v, n, partials, nparts, grad_scale, max_norm, lr, step, beta1, beta2, eps, M,
-              LGX_STREAM(stream));
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
+  int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
+  hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
+                     grad_scale, max_norm, lr, step, beta1, beta2, eps, M);
   return lgx_hip_status("lgx_adam_clip_mirror");
 }
