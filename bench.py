@@ -149,37 +149,97 @@ def mlp_flop_per_sample(dims):
     return 2 * sum(a * b for a, b in zip(dims[:-1], dims[1:]))
 
 
-def cpu_baseline(task, n_envs):
-    """Oracle env (C restatement, OpenMP over envs) + torch-CPU PPO, one PPO iteration."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+def _host_cpu_info():
+    """lscpu-style facts of the host the CPU baseline runs on (model, sockets, physical cores,
+    hardware threads) plus the CPUs this process may use (affinity, cgroup quota)."""
+    info = {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
+    try:
+        phys, model = set(), ""
+        with open("/proc/cpuinfo") as f:
+            pid = cid = None
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and not model:
+                    model = v
+                elif k == "physical id":
+                    pid = v
+                elif k == "core id":
+                    cid = v
+                elif not k and pid is not None:
+                    phys.add((pid, cid))
+                    pid = cid = None
+        info.update(cpu_model=model, sockets=len({p for p, _ in phys}) or None, physical_cores=len(phys) or None)
+    except OSError:
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpu_quota"] = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    return info
+
+
+def _cpu_iteration(task, n_envs, steps_per_env, threads):
+    """Env-steps/s of one PPO iteration (collection + learn) of the C oracle env (OpenMP over envs)
+    + torch-CPU ActorCritic/PPO at `threads` threads, after one untimed warm-up iteration."""
     import torch
-    from oracle_backend import make_env
+    from oracle_backend import make_env, load_oracle
     from legged_gym_amd.rl.runner import OnPolicyRunner
     from legged_gym_amd.utils.helpers import class_to_dict
     from legged_gym_amd.utils.task_registry import task_registry
-    from oracle_backend import load_oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
     torch.set_num_threads(threads)
     load_oracle().lgxo_set_threads(C.c_int(threads))   # the oracle's OpenMP env loops
     env = make_env(task, num_envs=n_envs, device="cpu", backend="oracle")
     _, train_cfg = task_registry.get_cfgs(task)
-    runner = OnPolicyRunner(env, class_to_dict(type(train_cfg)()), None, device="cpu")
+    tc = class_to_dict(type(train_cfg)())
+    tc["runner"]["num_steps_per_env"] = steps_per_env
+    runner = OnPolicyRunner(env, tc, None, device="cpu")
     runner.learn(1)  # warm
     t0 = time.time()
     runner.learn(1)
     dt = time.time() - t0
-    steps = runner.num_steps_per_env * n_envs
-    cpu_model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
-    except OSError:
-        pass
-    return dict(value=steps / dt, unit="env-steps/s", cores=threads, kind="port",
-                sample=f"1 PPO iteration ({runner.num_steps_per_env} steps x {n_envs} envs, {task}) of the C oracle "
-                       f"env (OpenMP {threads} threads over envs: physics, actuator net, rewards, observations) + "
-                       f"torch-CPU ActorCritic/PPO ({threads} threads); {dt:.1f}s",
-                cpu_model=cpu_model, nproc=os.cpu_count())
+    return steps_per_env * n_envs / dt, dt
+
+
+# SURVEY.md 8(d) CPU-baseline plan: C1 (64 envs) and C2 (4096 envs flat) besides the bench's C3
+# workload, at the CPU share of the box and at 1 thread.  A sample is one PPO iteration; the
+# throughput of an iteration does not depend on its length (collection and learn both scale with
+# the sample count), so the 1-thread runs of the large configs use fewer steps per env to keep the
+# whole baseline at ~1 minute of CPU time.
+CPU_RUNS = [  # (label, task, envs, steps per env at full share, steps per env at 1 thread)
+    ("C1", "go1_flat_bench", 64, 24, 24),
+    ("C2", "go1_flat_bench", 4096, 24, 2),
+    ("C3", "go1_rough", 1024, 24, 4),
+]
+
+
+def cpu_baseline(task, n_envs):
+    """The C oracle env + torch-CPU PPO ("port": the reference CPU path needs Isaac Gym, absent),
+    timed on this host at the configs of CPU_RUNS; value = the bench workload's config (C3) at the
+    full CPU share.  threads = the CPUs this job may use: OMP_NUM_THREADS (the GPU box's per-GPU
+    CPU share), else the affinity set, capped by the physical cores."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    info = _host_cpu_info()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or info["affinity_cpus"]
+    if info.get("physical_cores"):
+        share = min(share, info["physical_cores"])
+    runs = []
+    t_all = time.time()
+    for label, t, n, spe_full, spe_one in CPU_RUNS:
+        if label == "C3":
+            t, n = task, n_envs
+        for threads, spe in ((share, spe_full), (1, spe_one)):
+            v, dt = _cpu_iteration(t, n, spe, threads)
+            runs.append({"config": label, "task": t, "envs": n, "steps_per_env": spe, "threads": threads,
+                         "value": v, "seconds": round(dt, 3)})
+    head = next(r for r in runs if r["config"] == "C3" and r["threads"] == share)
+    return dict(value=head["value"], unit="env-steps/s", cores=share, kind="port",
+                sample=f"1 PPO iteration ({head['steps_per_env']} steps x {head['envs']} envs, {head['task']}) of the C "
+                       f"oracle env (OpenMP over envs: physics, actuator net, rewards, observations) + torch-CPU "
+                       f"ActorCritic/PPO, {share} threads; `runs` adds C1 / C2 and 1-thread runs "
+                       f"({time.time() - t_all:.0f} s of baseline in total, warm-ups included)",
+                runs=runs, host=info)
 
 
 def standalone_actuator_ms(lib, env, torch, launches=50):
@@ -348,13 +408,16 @@ def main():
     kernels = {n: {"avg_ms": round(a, 4), "launches_timed": int(c),
                    "share_of_iteration": round(a * steps_per_iter / it_ms, 4) if c else None}
                for n, a, c in zip(names, avg, cnt)}
-    # `roofline` = the critical-path lgx kernel with the largest share of the iteration (kernels
-    # running concurrently on a second stream follow it in `roofline_others`)
+    # `roofline` = the lgx kernel with the largest GPU-time share of the iteration, kernels that run
+    # concurrently on the update's second stream included (their share is co-resident GPU time);
+    # the others follow in `roofline_others`, in the same order
     phys_share = avg[0] * steps_per_iter / it_ms      # one launch per env step (timing is sampled)
     roof["share_of_iteration"] = phys_share
-    cands = [roof] + [g for g in gemm_roofs if not g.get("concurrent")]
+    cands = [roof] + gemm_roofs
     cands.sort(key=lambda r: -r.get("share_of_iteration", 0.0))
-    roof, others = cands[0], cands[1:] + [g for g in gemm_roofs if g.get("concurrent")]
+    roof, others = cands[0], cands[1:]
+    roof["selection"] = ("largest GPU-time share of the iteration among the physics kernel and the PPO-update GEMM "
+                         "families (second-stream launches included)")
     out = {
         "metric": (BASELINE_METRIC if (args.task == "go1_rough" and N == 4096)
                    else f"env-steps/sec (whole node), {args.task} {N} envs/GPU"),

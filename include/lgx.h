@@ -204,6 +204,11 @@ int lgx_version(void);
  * sizeof(lgx_gemm_tn_args), sizeof(lgx_mlp_x3_desc): lets bindings verify layout */
 void lgx_struct_sizes(int64_t out[12]);
 
+/* Lanes per leg (1, 2, 4 or 8) of the physics launch at `num_envs` envs, i.e. which
+ * lgx_physics_kernel<PP> instantiation lgx_step / lgx_simulate run: 4 below 8192 envs, 2 below
+ * 16384, 1 above (env LGX_PHYS_PP overrides); LGX_EINVAL for num_envs <= 0. */
+int32_t lgx_physics_lane_split(int32_t num_envs);
+
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */
 int64_t lgx_scratch_floats(int32_t num_envs, int32_t num_terms);
 

@@ -76,6 +76,7 @@ extern "C" {
 
 const char* lgx_last_error(void) { return g_err.c_str(); }
 int lgx_version(void) { return 1; }
+int32_t lgx_physics_lane_split(int32_t num_envs) { return num_envs > 0 ? lgx_physics_pp(num_envs) : LGX_EINVAL; }
 
 void lgx_struct_sizes(int64_t out[12]) {
   out[0] = (int64_t)sizeof(lgx_model);

@@ -16,6 +16,7 @@ struct lgx_dev_model {
   int32_t lane_pts[4][LGX_MAX_LANE_PTS];
 };
 
+int lgx_physics_pp(int32_t n_envs);   // lanes per leg of the physics launch at n_envs
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                        int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream);
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,

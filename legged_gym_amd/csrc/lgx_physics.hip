@@ -729,13 +729,19 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   LGX_CLK_PRINT("physics", 8)
 }
 
+// lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches;
+// LGX_PHYS_PP (1, 2, 4, 8) overrides it for A/B runs and for the parity tests of every split
+int lgx_physics_pp(int32_t n_envs) {
+  const int pp = n_envs >= 16384 ? 1 : (n_envs >= 8192 ? 2 : 4);
+  const char* force = getenv("LGX_PHYS_PP");
+  const int f = force ? atoi(force) : 0;
+  return (f == 1 || f == 2 || f == 4 || f == 8) ? f : pp;
+}
+
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                        int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream) {
   if (!act_src) act_src = b.actions;
-  // lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches
-  const int pp = n_envs >= 16384 ? 1 : (n_envs >= 8192 ? 2 : 4);
-  const char* force = getenv("LGX_PHYS_PP");  // A/B switch for measurements
-  const int ppx = force ? atoi(force) : pp;
+  const int ppx = lgx_physics_pp(n_envs);
   const int blocks = (n_envs + 15) / 16;       // 16 envs per workgroup of 64*PP lanes
   if (ppx == 8)
     LGX_LAUNCH(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions, act_src);

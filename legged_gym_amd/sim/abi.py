@@ -182,6 +182,7 @@ def declare(lib, prefix="lgx"):
     }
     if prefix == "lgx":  # PPO update entry points: product library only
         sigs.update({
+            "physics_lane_split": (i32, [i32]),
             "step_from": (C.c_int, [vp, vp, i64, vp]),
             "sync_aux": (C.c_int, [vp, vp]),
             "rebind_extras": (C.c_int, [vp, vp]),
@@ -225,7 +226,7 @@ def declare(lib, prefix="lgx"):
     return lib
 
 
-EXPORTED = ["lgx_last_error", "lgx_version", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
+EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
             "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_step_from", "lgx_sync_aux",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",

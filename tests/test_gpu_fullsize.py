@@ -1,6 +1,7 @@
-"""GPU at the benchmark size (C3: go1_rough, 4096 envs): size-independent properties of a
-rollout, oracle parity of a strided env subset taken from the full-size run, and the
-every-env-resets-at-once edge case.
+"""GPU at the benchmark sizes: C3 (go1_rough, 4096 envs/GPU: lgx_physics_kernel<4>), C5
+(anymal_c_rough with friction / base-mass / push randomisation, 8192 envs/GPU: <2>) and 16384
+envs (<1>): size-independent properties of a rollout, oracle parity of a strided 64-env subset
+taken from the full-size run, and the every-env-resets-at-once edge case.
 
 Tolerances as test_gpu_parity.py (physics model identical, algorithms differ: dense vs Schur).
 """
@@ -13,13 +14,24 @@ from test_gpu_parity import close, randomize_state, sync
 pytestmark = pytest.mark.gpu
 
 N = 4096
+SIZES = [("go1_rough", 4096), ("anymal_c_rough", 8192), ("anymal_c_rough", 16384)]
+_ENVS = {}
+
+
+def _big(task, n):
+    """One full-size env at a time (built on first use, the previous one released)."""
+    if (task, n) not in _ENVS:
+        _ENVS.clear()
+        torch.cuda.empty_cache()
+        env = make_env(task, num_envs=n, device="cuda:0", backend="lgx", overrides=_no_noise)
+        env.reset()
+        _ENVS[(task, n)] = env
+    return _ENVS[(task, n)]
 
 
 @pytest.fixture(scope="module")
 def big(gpu):
-    env = make_env("go1_rough", num_envs=N, device="cuda:0", backend="lgx", overrides=_no_noise)
-    env.reset()
-    return env
+    return _big("go1_rough", N)
 
 
 def _no_noise(cfg):
@@ -48,13 +60,18 @@ def test_full_size_rollout_properties(big):
     assert resets < 0.5 * N * 60
 
 
-def test_full_size_subset_matches_oracle(big):
-    """Envs 0, 64, 128, ... of the 4096-env device state, stepped by the 64-env oracle.  Draws
+@pytest.mark.parametrize("task,n", SIZES)
+def test_full_size_subset_matches_oracle(gpu, task, n):
+    """Envs 0, n/64, 2n/64, ... of the n-env device state, stepped by the 64-env oracle.  Draws
     are keyed by env index, so observation noise is off (both envs) and only non-resetting envs
-    are compared in full."""
-    dev = big
+    are compared in full.  The physics launch at n envs picks its lane split from n (PP = 4 / 2 /
+    1 at 4096 / 8192 / 16384), so each size runs its own kernel instantiation."""
+    from legged_gym_amd.sim import lib as lgxlib
+    dev = _big(task, n)
+    N = n
+    assert lgxlib.load().lgx_physics_lane_split(N) == {4096: 4, 8192: 2, 16384: 1}[N]
     idx = torch.arange(0, N, N // 64)
-    ora = make_env("go1_rough", num_envs=64, device="cpu", backend="oracle", overrides=_no_noise)
+    ora = make_env(task, num_envs=64, device="cpu", backend="oracle", overrides=_no_noise)
     if not torch.equal(ora.height_samples, dev.height_samples.cpu()):
         pytest.skip("heightfield depends on num_envs")
     gen = torch.Generator().manual_seed(5)
@@ -67,6 +84,8 @@ def test_full_size_subset_matches_oracle(big):
     if hasattr(dev, "actuator_history"):
         ora.actuator_history.copy_(dev.actuator_history[idx.cuda()].cpu())
     ora.common_step_counter = dev.common_step_counter = 100
+    if task.startswith("anymal"):   # the randomisation tables were copied in from the device run
+        assert dev.friction_coeffs.unique().numel() > 8 and (dev.body_mass_scale[:, 0] - 1).abs().max() > 0.1
     a_sub = (torch.rand(64, 12, generator=gen) - 0.5) * 2
     a_full = torch.zeros(N, 12)
     a_full[idx] = a_sub

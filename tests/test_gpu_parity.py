@@ -434,6 +434,53 @@ def test_other_robots_step_matches_oracle(gpu, task):
     assert ok, f"rew max err {e}"
 
 
+@pytest.mark.parametrize("pp", ["4", "2", "1"])
+def test_anymal_c_rough_dr_step_matches_oracle(gpu, monkeypatch, pp):
+    """BASELINE C5 (anymal_c_rough_config.py:33-94): ANYmal-C on the curriculum trimesh with the
+    full domain randomisation - friction buckets U[0.5, 1.25] (legged_robot.py:259-282), base mass
+    +U[-5, 5] kg (anymal_c_rough_config.py:80-81, legged_robot.py:312-335) and the push at step
+    751 (legged_robot.py:436-441) - two env steps, HIP path vs oracle.  pp = LGX_PHYS_PP: every
+    lane split of lgx_physics_kernel (4 below 8192 envs, 2 at 8192 = C5's size, 1 from 16384)."""
+    monkeypatch.setenv("LGX_PHYS_PP", pp)
+    ora = make_env("anymal_c_rough", num_envs=64, device="cpu", backend="oracle")
+    dev = make_env("anymal_c_rough", num_envs=64, device="cuda:0", backend="lgx")
+    assert torch.equal(ora.height_samples, dev.height_samples.cpu()), "same seed -> same heightfield"
+    # the randomisation is live: per-env friction from the 64 buckets, base masses spread over +-5 kg
+    assert ora.friction_coeffs.unique().numel() > 8 and ora.friction_coeffs.min() >= 0.5 and ora.friction_coeffs.max() <= 1.25
+    base = ora.body_masses[:, 0] - ora.asset.data["report_bodies"][0]["mass"]
+    assert base.min() >= -5 and base.max() <= 5 and base.std() > 1.5
+    assert ora.cfg.domain_rand.push_robots and int(ora.cfg.domain_rand.push_interval) == 751
+    gen = torch.Generator().manual_seed(77)
+    randomize_state(ora, gen)
+    sync(ora, dev)
+    dev.terrain_types.copy_(ora.terrain_types)
+    ora.common_step_counter = dev.common_step_counter = 749       # the second step is the push step
+    for it in range(2):
+        a = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+        ora.step(a)
+        dev.step(a.cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf), it
+        assert torch.equal(dev._episode_length_buf.cpu(), ora._episode_length_buf), it
+        keep = ~ora.reset_buf
+        ok, e = close(dev.root_states.cpu()[keep], ora.root_states[keep], 2e-3, 2e-3)
+        assert ok, f"step {it}: root max err {e}"
+        ok, e = close(dev.dof_state.view(64, 12, 2).cpu()[keep], ora.dof_state.view(64, 12, 2)[keep], 5e-3, 2e-3)
+        assert ok, f"step {it}: dof max err {e}"
+        ok, e = close(dev.measured_heights, ora.measured_heights, 1e-6)
+        assert ok, f"step {it}: heights max err {e}"
+        ok, e = close(dev.obs_buf.cpu()[keep], ora.obs_buf[keep], 5e-3, 5e-3)
+        assert ok, f"step {it}: obs max err {e}"
+        ok, e = close(dev.rew_buf.cpu()[keep], ora.rew_buf[keep], 1e-4, 1e-3)
+        assert ok, f"step {it}: rew max err {e}"
+        # reset envs: the reset state itself (Philox draws keyed by env index)
+        ok, e = close(dev.root_states.cpu()[~keep], ora.root_states[~keep], 1e-4, 1e-5)
+        assert ok, f"step {it}: reset root max err {e}"
+        if it == 0:   # the push step starts from identical states (contacts amplify rounding)
+            sync(ora, dev)
+    assert torch.equal(dev.terrain_levels.cpu(), ora.terrain_levels)
+
+
 def test_direct_actions_and_extras_snapshots(gpu):
     """lgx_step_from (policy tensor read in place) == copy-then-lgx_step, the caller's tensor is not
     clipped in place, and every step publishes its own extras snapshot (kernel-written) that
