@@ -249,12 +249,15 @@ LGX_DEV void extras_finalize_body(const lgx_env_params* __restrict__ P, const lg
 // finalize, so the reduction needs no second launch.  Release: every thread's partial /
 // time_out / level writes are fenced at device scope before the ticket; acquire: the last
 // workgroup fences again before reading them (the L2s of the 8 XCDs are not coherent).
-// The release fence (an L2 write-back at agent scope) is taken by wave 0 only: the block's
-// partial row was written by threads < T + 2 <= 64 (block_partials), and every other wave skips
-// the write-back (measured: all four waves fencing took ~15 us of each workgroup's timeline).
+// The release fence (an L2 write-back at agent scope) is taken by wave 0 only: every write the
+// finalize reads comes from wave 0 - the block's partial row from threads < T + 2 <= 64
+// (block_partials), time_out / extras_time_outs and the curriculum levels from the env lanes
+// (threads < LGX_ENV_BLOCK <= 64) - and every other wave skips the write-back (measured: all
+// four waves fencing took ~15 us of each workgroup's timeline).
 LGX_DEV bool take_last_ticket(const lgx_buffers& B, int nblocks) {
   __shared__ int last;
   static_assert(LGX_PARTIAL_STRIDE <= 64, "the partial-row writers are wave 0");
+  static_assert(LGX_ENV_BLOCK <= 64, "the env lanes (time_out, levels) are wave 0");
   if (threadIdx.x < 64) __threadfence();
   __syncthreads();
   if (threadIdx.x == 0) {

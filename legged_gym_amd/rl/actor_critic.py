@@ -82,41 +82,47 @@ class _FusedMLP:
         self.act = self.ACT.get(next(iter(acts)), 0) if len(acts) == 1 else 0
         self.dims = [self.linears[0].in_features] + [l.out_features for l in self.linears]
         self.ok = self.act != 0 and max(self.dims) <= 512 and len(self.linears) <= 6
-        self.x3 = self.ok and os.environ.get("LGX_MLP_X3", "1") != "0"
-        self._ver = None
+        self.x3 = self.ok and os.environ.get("LGX_MLP_X3", "1") != "0"   # split-bf16 kernel allowed
+        self.last_x3 = None          # which kernel the last launch with this network ran (tests)
+        self._ver = {}               # parameter version each weight image was built from
         self._wt = self._b = self._wl = None
 
-    def _refresh(self):
+    def _refresh(self, x3):
+        """Biases and the weight image of the requested kernel, rebuilt when the parameters changed
+        (optimizer step, load) - split-bf16 limb images for lgx_mlp_x3_forward, transposed f32
+        weights for lgx_mlp_forward_batch; a network may launch with either, per launch."""
         ver = tuple(l.weight._version for l in self.linears) + tuple(l.bias._version for l in self.linears)
-        if ver != self._ver or self._b is None or self._b[0].device != self.linears[0].weight.device:
-            with torch.no_grad():
+        dev = self.linears[0].weight.device
+        n = len(self.linears)
+        with torch.no_grad():
+            if self._ver.get("b") != ver or self._b is None or self._b[0].device != dev:
                 self._b = [l.bias.detach().contiguous() for l in self.linears]
-                if self.x3:
-                    from legged_gym_amd.sim import lib as lgxlib
-                    lib = lgxlib.load()
-                    dev = self.linears[0].weight.device
-                    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-                    if self._wl is None or self._wl[0].device != dev:
-                        self._wl = [torch.empty(int(lib.lgx_mlp_x3_weight_elems(l.out_features, l.in_features)),
-                                                dtype=torch.int16, device=dev) for l in self.linears]
-                    for l, wl in zip(self.linears, self._wl):
-                        w = l.weight.detach().contiguous()
-                        lgxlib.check(lib.lgx_mlp_x3_split(C.c_void_p(w.data_ptr()), l.out_features, l.in_features,
-                                                          C.c_void_p(wl.data_ptr()), stream), "lgx_mlp_x3_split")
-                    self._wt = None
-                else:
-                    self._wt = [l.weight.detach().t().contiguous() for l in self.linears]
-            self._ver = ver
-            n = len(self.linears)
-            self._dims_c = (C.c_int32 * (n + 1))(*self.dims)
-            if self._wt is not None:
+                self._bp = (C.c_void_p * n)(*[t.data_ptr() for t in self._b])
+                self._dims_c = (C.c_int32 * (n + 1))(*self.dims)
+                self._ver["b"] = ver
+            if x3 and (self._ver.get("wl") != ver or self._wl is None or self._wl[0].device != dev):
+                from legged_gym_amd.sim import lib as lgxlib
+                lib = lgxlib.load()
+                stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+                if self._wl is None or self._wl[0].device != dev:
+                    self._wl = [torch.empty(int(lib.lgx_mlp_x3_weight_elems(l.out_features, l.in_features)),
+                                            dtype=torch.int16, device=dev) for l in self.linears]
+                for l, wl in zip(self.linears, self._wl):
+                    w = l.weight.detach().contiguous()
+                    lgxlib.check(lib.lgx_mlp_x3_split(C.c_void_p(w.data_ptr()), l.out_features, l.in_features,
+                                                      C.c_void_p(wl.data_ptr()), stream), "lgx_mlp_x3_split")
+                self._ver["wl"] = ver
+            if not x3 and (self._ver.get("wt") != ver or self._wt is None or self._wt[0].device != dev):
+                self._wt = [l.weight.detach().t().contiguous() for l in self.linears]
                 self._wp = (C.c_void_p * n)(*[t.data_ptr() for t in self._wt])
-            self._bp = (C.c_void_p * n)(*[t.data_ptr() for t in self._b])
+                self._ver["wt"] = ver
 
-    def desc(self, x, y):
+    def desc(self, x, y, x3=None):
         from legged_gym_amd.sim import abi
-        self._refresh()
-        if self.x3:
+        x3 = self.x3 if x3 is None else x3
+        self._refresh(x3)
+        self.last_x3 = x3
+        if x3:
             d = abi.LgxMlpX3Desc()
             d.x, d.y, d.rows, d.nl, d.act = x.data_ptr(), y.data_ptr(), x.shape[0], len(self.linears), self.act
             for i, v in enumerate(self.dims):
@@ -135,7 +141,7 @@ class _FusedMLP:
         return d
 
     def invalidate(self):
-        self._ver = None
+        self._ver = {}
 
     def __call__(self, x):
         return run_fused([(self, x)])[0]
@@ -176,16 +182,14 @@ _X3_FIT = {}
 def make_descs(triples):
     """Descriptor array of one fused launch over up to two (fused_mlp, input, output) triples:
     split-bf16 (lgx_mlp_x3_forward) when every network takes it and their activations fit the LDS
-    together, else f32 MFMA (lgx_mlp_forward_batch) for all of them."""
+    together, else f32 MFMA (lgx_mlp_forward_batch) for all of them.  Decided per launch: a pair
+    that does not fit together leaves each network's own (single-network) launches on split-bf16."""
     from legged_gym_amd.sim import abi
     mlps = [m for m, _, _ in triples]
-    if any(m.x3 for m in mlps) and not (all(m.x3 for m in mlps) and _x3_fits(mlps)):
-        for m in mlps:
-            if m.x3:
-                m.x3, m._ver = False, None
-    descs = ((abi.LgxMlpX3Desc if mlps[0].x3 else abi.LgxMlpDesc) * len(triples))()
+    x3 = all(m.x3 for m in mlps) and _x3_fits(mlps)
+    descs = ((abi.LgxMlpX3Desc if x3 else abi.LgxMlpDesc) * len(triples))()
     for i, (m, x, y) in enumerate(triples):
-        descs[i] = m.desc(x, y)
+        descs[i] = m.desc(x, y, x3)
     return descs
 
 

@@ -35,10 +35,11 @@ from legged_gym_amd.sim import abi
 class _TunedGemms:
     """The GEMM solution table tuned on MI355X for the PPO-update shapes (torch TunableOp,
     rocBLAS / hipBLASLt solutions; regenerate with tools/tune_gemms.sh), scoped: TunableOp is
-    switched on only inside `with` blocks around the update's library GEMMs and restored to the
-    caller's setting afterwards, so other torch GEMMs of the process are unaffected.  Read-only
-    (no tuning, no recording); shapes not in the table run the library
-    default.  LGX_TUNED_GEMMS=0 disables."""
+    switched on, read-only (no tuning, no recording of untuned shapes), with this table's file
+    name, only inside `with` blocks around the update's library GEMMs; every TunableOp setting
+    the caller had (enable, tuning, recording, file name) is restored on exit, so other torch GEMMs
+    of the process are unaffected.  Shapes not in the table run the library default.
+    LGX_TUNED_GEMMS=0 disables."""
     _loaded = None
 
     def __init__(self):
@@ -50,26 +51,43 @@ class _TunedGemms:
         path = os.path.join(LEGGED_GYM_ROOT_DIR, "resources", "tunableop", "ppo_gemms_gfx950.csv")
         if not os.path.exists(path):
             return
-        self.tunable = tunable
+        self.tunable, self.path = tunable, path
         if _TunedGemms._loaded is None:
-            prev = tunable.is_enabled()
-            tunable.enable(True)
-            tunable.tuning_enable(False)
-            tunable.record_untuned_enable(False)
-            tunable.set_filename(path, insert_device_ordinal=False)
+            saved = self._save()
+            self._apply()
             _TunedGemms._loaded = bool(tunable.read_file(path))
-            tunable.enable(prev)
+            self._restore(saved)
         self.ok = _TunedGemms._loaded
+
+    def _save(self):
+        t = self.tunable
+        return (t.is_enabled(), t.tuning_is_enabled(), t.record_untuned_is_enabled(), t.get_filename())
+
+    def _apply(self):
+        t = self.tunable
+        t.enable(True)
+        t.tuning_enable(False)
+        t.record_untuned_enable(False)
+        t.set_filename(self.path, insert_device_ordinal=False)
+
+    def _restore(self, saved):
+        t = self.tunable
+        enabled, tuning, record, filename = saved
+        t.tuning_enable(tuning)
+        t.record_untuned_enable(record)
+        if filename:
+            t.set_filename(filename, insert_device_ordinal=False)
+        t.enable(enabled)
 
     def __enter__(self):
         if self.ok:
-            self.prev = self.tunable.is_enabled()
-            self.tunable.enable(True)
+            self.saved = self._save()
+            self._apply()
         return self
 
     def __exit__(self, *exc):
         if self.ok:
-            self.tunable.enable(self.prev)
+            self._restore(self.saved)
         return False
 
 

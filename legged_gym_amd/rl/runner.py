@@ -166,10 +166,11 @@ class OnPolicyRunner:
         if hasattr(self.alg.actor_critic, "invalidate_fused"):
             self.alg.actor_critic.invalidate_fused()
         if load_optimizer:
+            # as upstream rsl_rl: the optimizer state (its param_groups' lr included) is restored and
+            # alg.learning_rate keeps the config value - the adaptive schedule's first update then
+            # adapts from the config value and overwrites the restored lr, a fixed schedule steps
+            # with the restored lr (tests/test_ppo.py::test_resume_learning_rate_follows_upstream)
             self.alg.optimizer.load_state_dict(d["optimizer_state_dict"])
-            # continue from the checkpoint's learning rate (the adaptive schedule adapts from it;
-            # a fixed schedule keeps it, as torch.optim.Adam's restored param_groups do)
-            self.alg.learning_rate = float(self.alg.optimizer.param_groups[0]["lr"])
         self.current_learning_iteration = d["iter"]
         return d["infos"]
 

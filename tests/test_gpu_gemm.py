@@ -328,3 +328,29 @@ def test_copy2d_and_padded_gather(gpu):
                                                    C.c_void_p(idx.data_ptr()), 37, 235, 240, _stream()), "gather")
     torch.cuda.synchronize()
     assert torch.equal(dst[:, :235], src[idx]) and torch.all(dst[:, 235:] == 0)
+
+
+def test_elu_near_zero_bound(gpu):
+    """lgx_elu (lgx_internal.h: exp(x) - 1 on v_exp_f32, shared by every ELU epilogue: rollout MLP,
+    PPO forward GEMMs, lgx_bias_act) against float64 ELU for pre-activations concentrated near 0,
+    where exp(x) - 1 cancels: the documented bound is an ABSOLUTE error of at most
+    1.5e-7 (a few ulp of 1), i.e. relative error <= 1.5e-7 / |x| - tiny outputs carry large relative
+    error but stay below the rounding of the O(1) sums of the next layer; x >= 0 is exact."""
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    mag = 10 ** (-8 + 7 * torch.rand(64 * 1024, device="cuda:0", generator=g))     # 1e-8 .. 0.1
+    sign = torch.where(torch.rand(64 * 1024, device="cuda:0", generator=g) < 0.8, -1.0, 1.0)
+    x = (mag * sign).view(1024, 64).contiguous()
+    z = x.clone()
+    zero_b = torch.zeros(64, device="cuda:0")
+    lgxlib.check(_lib().lgx_bias_act(C.c_void_p(z.data_ptr()), C.c_void_p(zero_b.data_ptr()), 1024, 64, 1, 1,
+                                     _stream()), "bias_act")
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.elu(x.double())
+    err = (z.double() - ref).abs()
+    assert err.max().item() <= 1.5e-7, err.max().item()
+    assert (err[x > 0] == 0).all()
+    rel = err / ref.abs().clamp_min(1e-30)
+    assert (rel <= 1.5e-7 / x.double().abs() + 1e-7).all()
+    # and where the cancellation is mild (|x| >= 2^-8) the relative error is f32-level
+    mild = x.abs() >= 2 ** -8
+    assert rel[mild].max().item() <= 6e-5, rel[mild].max().item()

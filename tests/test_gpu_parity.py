@@ -254,11 +254,39 @@ def test_mlp_x3_falls_back_when_lds_is_short(gpu):
     with torch.inference_mode():
         mean, value = ac.rollout_forward(obs, obs)
         ref_mean, ref_v = ac.actor(obs), ac.critic(obs)
-    assert not ac._fused_actor.x3 and not ac._fused_critic.x3
+    assert ac._fused_actor.last_x3 is False and ac._fused_critic.last_x3 is False
     ok, e = close(mean, ref_mean, 2e-4, 2e-4)
     assert ok, f"actor mean max err {e}"
     ok, e = close(value, ref_v, 2e-4, 2e-4)
     assert ok, f"critic value max err {e}"
+
+
+def test_mlp_x3_single_network_after_pair_fallback(gpu):
+    """A pair that does not fit the LDS together runs f32 for that launch only: each network's own
+    launch (act_inference) still takes the split-bf16 kernel when it fits alone, and a parameter
+    update refreshes whichever weight image the next launch uses."""
+    from legged_gym_amd.rl.actor_critic import ActorCritic, _x3_fits
+    torch.manual_seed(2)
+    ac = ActorCritic(235, 235, 12, [512, 512, 256], [512, 512, 256]).to(gpu)
+    if _x3_fits([ac._fused_actor, ac._fused_critic]) or not _x3_fits([ac._fused_actor]):
+        pytest.skip("this stack fits as a pair / not alone on this LDS budget")
+    obs = torch.randn(300, 235, device=gpu)
+    with torch.inference_mode():
+        ac.rollout_forward(obs, obs)
+        assert ac._fused_actor.last_x3 is False
+        m1 = ac.act_inference(obs)
+        assert ac._fused_actor.last_x3 is True
+        ok, e = close(m1, ac.actor(obs), 2e-4, 2e-4)
+        assert ok, f"actor mean max err {e}"
+    with torch.no_grad():
+        for p in ac.actor.parameters():
+            p.add_(0.01)
+    with torch.inference_mode():
+        mean, _ = ac.rollout_forward(obs, obs)
+        ok, e = close(mean, ac.actor(obs), 2e-4, 2e-4)
+        assert ok, f"actor mean after update max err {e}"
+        ok, e = close(ac.act_inference(obs), ac.actor(obs), 2e-4, 2e-4)
+        assert ok, f"actor mean (split-bf16) after update max err {e}"
 
 
 def test_lstm_matches_oracle(gpu):
@@ -341,7 +369,7 @@ def test_mlp_forward_batch_actor_critic(gpu):
     assert ok, f"actor mean max err {e}"
     ok, e = close(v, ref_v, 2e-4, 2e-4)
     assert ok, f"critic value max err {e}"
-    assert ac._fused_actor.x3 and ac._fused_critic.x3   # the split-bf16 kernel ran
+    assert ac._fused_actor.last_x3 and ac._fused_critic.last_x3   # the split-bf16 kernel ran
 
 
 def test_gae_kernel_matches_torch_loop(gpu):

@@ -255,3 +255,44 @@ def test_policy_export_is_plain_torchscript(tmp_path):
     pol = torch.jit.load(str(tmp_path / "policy_1.pt"))
     x = torch.randn(5, OBS)
     assert torch.allclose(pol(x), ac.actor(x), atol=1e-6)
+
+
+@pytest.mark.parametrize("schedule", ["adaptive", "fixed"])
+def test_resume_learning_rate_follows_upstream(tmp_path, schedule):
+    """rsl_rl v1.0.x OnPolicyRunner.load restores the optimizer state only; alg.learning_rate keeps
+    the config value.  Adaptive schedule: the first update after a resume adapts from the config
+    value and writes it into the optimizer (the restored lr is overwritten); fixed schedule: the
+    update steps with the restored optimizer lr."""
+    from oracle_backend import make_env
+    from legged_gym_amd.rl.runner import OnPolicyRunner
+    from legged_gym_amd.utils.helpers import class_to_dict
+    from legged_gym_amd.envs.go1.go1_config import Go1RoughCfgPPO
+    env = make_env("go1_flat_bench", num_envs=8, device="cpu", backend="oracle")
+    cfg = class_to_dict(Go1RoughCfgPPO())
+    cfg["runner"]["num_steps_per_env"] = 4
+    cfg["algorithm"]["schedule"] = schedule
+    runner = OnPolicyRunner(env, cfg, None, device="cpu")
+    for g in runner.alg.optimizer.param_groups:
+        g["lr"] = 3.3e-4                           # a trained-run lr that differs from the config's
+    path = str(tmp_path / "model_7.pt")
+    runner.save(path)
+    resumed = OnPolicyRunner(env, cfg, None, device="cpu")
+    resumed.load(path)
+    lr_cfg = cfg["algorithm"]["learning_rate"]
+    assert resumed.alg.learning_rate == lr_cfg
+    assert resumed.alg.optimizer.param_groups[0]["lr"] == 3.3e-4
+    seen = []
+    step = resumed.alg.optimizer.step
+
+    def spy(*a, **k):
+        seen.append(resumed.alg.optimizer.param_groups[0]["lr"])
+        return step(*a, **k)
+    resumed.alg.optimizer.step = spy
+    resumed.learn(1)
+    if schedule == "fixed":
+        assert seen and all(lr == 3.3e-4 for lr in seen)
+    else:   # adapted from the config value by factors of 1.5 (or kept), never the restored 3.3e-4
+        # (clamped to [1e-5, 1e-2])
+        ratios = [np.log(lr / lr_cfg) / np.log(1.5) for lr in seen if 1e-5 < lr < 1e-2]
+        assert seen and ratios and all(abs(r - round(r)) < 1e-6 for r in ratios), seen
+        assert 3.3e-4 not in seen
