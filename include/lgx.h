@@ -250,6 +250,14 @@ int lgx_sync_aux(lgx_sim* sim, void* stream);
 /* Physics only: `n` substeps with the currently bound dof_targets (gym.simulate x n). */
 int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
 
+/* The drive inputs of lgx_step's physics launch with the dynamics frozen: clip the actions
+ * (`actions`, or the bound buffer when NULL) into the bound actions buffer, the position targets
+ * (_compute_poses, legged_robot.py:394-397) into dof_targets, and `decimation` substeps of the Go1
+ * actuator-net history (go1.py:79-98) into act_hist / model_ins, all from the CURRENT dof state,
+ * which stays unchanged (as the reference's decimation loop sees it when the physics does not move:
+ * the golden replay).  Same device code as the physics launch's load stage. */
+int lgx_drive_inputs(lgx_sim* sim, const float* actions, void* stream);
+
 /* post_physics_step only (legged_robot.py:109-141) on the current state buffers. */
 int lgx_post_physics(lgx_sim* sim, int64_t common_step_counter, void* stream);
 

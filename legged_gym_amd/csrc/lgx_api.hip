@@ -246,6 +246,14 @@ int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
                       "lgx_simulate: physics launch");
 }
 
+int lgx_drive_inputs(lgx_sim* s, const float* actions, void* stream) {
+  if (!s) return fail(LGX_EINVAL, "lgx_drive_inputs: null sim");
+  if (int rc = join_aux(s, (hipStream_t)stream)) return rc;   // the last actuator net still reads model_ins
+  return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, s->params.decimation, 1,
+                                         actions, (hipStream_t)stream, 1),
+                      "lgx_drive_inputs: launch");
+}
+
 int lgx_post_physics(lgx_sim* s, int64_t step, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_post_physics: null sim");
   return launch_check(lgx_launch_post_physics(s->d_params, s->bufs, s->params.num_envs, s->params.num_obs, s->n_term_rows,

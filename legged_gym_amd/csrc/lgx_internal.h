@@ -17,8 +17,11 @@ struct lgx_dev_model {
 };
 
 int lgx_physics_pp(int32_t n_envs);   // lanes per leg of the physics launch at n_envs
+// frozen != 0: only the drive inputs of `nsub` substeps (clip, targets, actuator-net history and
+// model_ins rows) with the state held fixed (lgx_drive_inputs)
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
-                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream);
+                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
+                       int32_t frozen = 0);
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
                             int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
                             float* extras_snapshot, hipStream_t stream);

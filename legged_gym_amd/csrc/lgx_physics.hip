@@ -248,7 +248,7 @@ LGX_DEV float psum(float v) {
 template <int PP>
 __global__ void __launch_bounds__(64 * PP, LGX_PHYS_WAVES_PER_SIMD)
 lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* __restrict__ P, lgx_buffers B,
-                   int32_t nsub, int32_t from_actions, const float* __restrict__ act_src) {
+                   int32_t nsub, int32_t from_actions, const float* __restrict__ act_src, int32_t frozen) {
   constexpr int PHYS_BLOCK = 64 * PP;               // 16 envs per workgroup
   constexpr int LPE = 4 * PP;                       // lanes per env
   constexpr int SLOTS = (MAX_LANE_PTS + PP - 1) / PP;
@@ -399,6 +399,9 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       }
     }
     LGX_CLK(0);
+    // frozen (lgx_drive_inputs): the drive inputs above - clipped actions, targets, actuator-net
+    // history / model_ins rows - with the state held fixed, no dynamics (uniform branch)
+    if (frozen) continue;
     // ---- kinematics
     m33 R0 = quat_to_mat(qx, qy, qz, qw);
     m33 Rb[3];
@@ -697,6 +700,18 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     float* ao = B.actions + (int64_t)e * 12 + leg * 3;
     ao[0] = act[0]; ao[1] = act[1]; ao[2] = act[2];
   }
+  if (frozen) {
+    if (ctrl == LGX_CTRL_POS_DRIVE && from_actions) {
+      float* to = B.dof_targets + (int64_t)e * 12 + leg * 3;
+      to[0] = tgt[0]; to[1] = tgt[1]; to[2] = tgt[2];
+    }
+    if (use_hist) {
+      float* h = B.act_hist + (int64_t)e * 120 + leg * 30;
+#pragma unroll
+      for (int i = 0; i < 30; i += 2) *reinterpret_cast<float2*>(h + i) = make_float2(hist[i], hist[i + 1]);
+    }
+    return;
+  }
   float* dso = B.dof_state + (int64_t)e * 24 + leg * 6;
 #pragma unroll
   for (int k = 0; k < 3; ++k) *reinterpret_cast<float2*>(dso + 2 * k) = make_float2(th[k], thd[k]);
@@ -739,18 +754,18 @@ int lgx_physics_pp(int32_t n_envs) {
 }
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
-                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream) {
+                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream, int32_t frozen) {
   if (!act_src) act_src = b.actions;
   const int ppx = lgx_physics_pp(n_envs);
   const int blocks = (n_envs + 15) / 16;       // 16 envs per workgroup of 64*PP lanes
   if (ppx == 8)
-    LGX_LAUNCH(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions, act_src);
+    LGX_LAUNCH(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);
   else if (ppx == 4)
-    LGX_LAUNCH(lgx_physics_kernel<4>, dim3(blocks), dim3(256), 0, stream, dm, dp, b, nsub, from_actions, act_src);
+    LGX_LAUNCH(lgx_physics_kernel<4>, dim3(blocks), dim3(256), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);
   else if (ppx == 2)
-    LGX_LAUNCH(lgx_physics_kernel<2>, dim3(blocks), dim3(128), 0, stream, dm, dp, b, nsub, from_actions, act_src);
+    LGX_LAUNCH(lgx_physics_kernel<2>, dim3(blocks), dim3(128), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);
   else
-    LGX_LAUNCH(lgx_physics_kernel<1>, dim3(blocks), dim3(64), 0, stream, dm, dp, b, nsub, from_actions, act_src);
+    LGX_LAUNCH(lgx_physics_kernel<1>, dim3(blocks), dim3(64), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

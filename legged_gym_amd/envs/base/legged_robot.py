@@ -61,6 +61,10 @@ class LgxBackend:
     def simulate(self, n):
         self._check(self.lib.lgx_simulate(self.handle, n, self.stream()), "lgx_simulate")
 
+    def drive_inputs(self, actions=None):
+        self._check(self.lib.lgx_drive_inputs(self.handle, C.c_void_p(actions.data_ptr()) if actions is not None
+                                              else None, self.stream()), "lgx_drive_inputs")
+
     def post_physics(self, counter):
         self._check(self.lib.lgx_post_physics(self.handle, counter, self.stream()), "lgx_post_physics")
 

@@ -267,9 +267,9 @@ def test_mlp_x3_single_network_after_pair_fallback(gpu):
     update refreshes whichever weight image the next launch uses."""
     from legged_gym_amd.rl.actor_critic import ActorCritic, _x3_fits
     torch.manual_seed(2)
-    ac = ActorCritic(235, 235, 12, [512, 512, 256], [512, 512, 256]).to(gpu)
-    if _x3_fits([ac._fused_actor, ac._fused_critic]) or not _x3_fits([ac._fused_actor]):
-        pytest.skip("this stack fits as a pair / not alone on this LDS budget")
+    # the actor's 32-row limb images fit the LDS alone, the critic's (512-512-256) do not
+    ac = ActorCritic(235, 235, 12, [512, 256, 128], [512, 512, 256]).to(gpu)
+    assert not _x3_fits([ac._fused_actor, ac._fused_critic]) and _x3_fits([ac._fused_actor])
     obs = torch.randn(300, 235, device=gpu)
     with torch.inference_mode():
         ac.rollout_forward(obs, obs)
@@ -480,6 +480,7 @@ def test_anymal_c_rough_dr_step_matches_oracle(gpu, monkeypatch, pp):
     assert ora.cfg.domain_rand.push_robots and int(ora.cfg.domain_rand.push_interval) == 751
     gen = torch.Generator().manual_seed(77)
     randomize_state(ora, gen)
+    ora._episode_length_buf[:4] = int(ora.max_episode_length)     # envs 0-3 time out in the first step
     sync(ora, dev)
     dev.terrain_types.copy_(ora.terrain_types)
     ora.common_step_counter = dev.common_step_counter = 749       # the second step is the push step
@@ -502,8 +503,10 @@ def test_anymal_c_rough_dr_step_matches_oracle(gpu, monkeypatch, pp):
         ok, e = close(dev.rew_buf.cpu()[keep], ora.rew_buf[keep], 1e-4, 1e-3)
         assert ok, f"step {it}: rew max err {e}"
         # reset envs: the reset state itself (Philox draws keyed by env index)
-        ok, e = close(dev.root_states.cpu()[~keep], ora.root_states[~keep], 1e-4, 1e-5)
-        assert ok, f"step {it}: reset root max err {e}"
+        assert it == 1 or (~keep).sum() >= 4
+        if (~keep).any():
+            ok, e = close(dev.root_states.cpu()[~keep], ora.root_states[~keep], 1e-4, 1e-5)
+            assert ok, f"step {it}: reset root max err {e}"
         if it == 0:   # the push step starts from identical states (contacts amplify rounding)
             sync(ora, dev)
     assert torch.equal(dev.terrain_levels.cpu(), ora.terrain_levels)

@@ -217,11 +217,13 @@ def test_fused_update_matches_autograd_update(gpu, monkeypatch, schedule, cobs, 
     vl_f, sl_f = fus.update()
     assert fus.learning_rate == ref.learning_rate
     assert abs(vl_f - vl_r) <= 1e-4 * abs(vl_r) + 1e-6 and abs(sl_f - sl_r) <= 1e-4 * abs(sl_r) + 1e-6
+    # end to end after 8 Adam steps the two runs differ only where Adam normalised a rounding-level
+    # gradient into a full step of either sign (and what that feeds): a few coordinates.  Every
+    # coordinate of every step is checked exactly in test_fused_update_every_step_is_exact.
     big = 0
     total = 0
     for (n, a), b in zip(fus.actor_critic.named_parameters(), ref.actor_critic.parameters()):
         d = (a - b).abs()
-        assert d.max().item() <= 2 * 8 * 1e-3, n
         big += (d > 1e-5).sum().item()
         total += d.numel()
     assert big <= 1e-3 * total, (big, total)
@@ -329,5 +331,46 @@ def test_fused_update_matches_numpy_oracle(gpu, schedule):
     assert fus.learning_rate == pytest.approx(want[3], rel=1e-9)
     assert abs(vl - want[4]) <= 1e-4 * abs(want[4]) + 1e-6 and abs(sl - want[5]) <= 1e-4 * abs(want[5]) + 1e-6
     dmax, big, total = param_deviation(fus.actor_critic, want)
-    assert dmax <= 2 * 8 * 1e-3, dmax
-    assert big <= 1e-3 * total, (big, total)
+    assert big <= 1e-3 * total, (big, total, dmax)
+
+
+@pytest.mark.parametrize("schedule,cobs,algo", [("adaptive", None, "split"), ("fixed", None, "split"),
+                                                ("adaptive", 252, "split"), ("adaptive", None, "f32")])
+def test_fused_update_every_step_is_exact(gpu, monkeypatch, schedule, cobs, algo):
+    """Every coordinate of every optimizer step of a full fused update (2 epochs x 4 minibatches),
+    recorded as it runs (tests/ppo_trace.py):
+      * the flat gradient the step consumed == the autograd gradient (rl/ppo.py's loss, pinned
+        against the numpy oracle on CPU) at the SAME parameters and rows: |d| <= 1e-5 + 2e-3 |g|,
+        so the GEMM weight mirrors the previous Adam step wrote (limb images) are checked too;
+      * the parameters / moments after the step == float64 clip_grad_norm_ + torch Adam applied
+        to that gradient from the recorded state: |d| <= 1e-6 + 1e-3 lr (p), 1e-5 relative (m, v:
+        the f32 global norm);
+      * the learning rate the step used == the adaptive schedule's (same sequence as autograd)."""
+    from ppo_trace import StepTrace, adam64, flat_view
+    monkeypatch.setenv("LGX_GEMM_ALGO", algo)
+    ref, fus = make_pair(schedule, cobs)
+    tr = StepTrace(fus._fused)
+    torch.manual_seed(11)
+    fus.update()
+    tr.close()
+    torch.manual_seed(11)
+    ref.update()
+    assert fus.learning_rate == ref.learning_rate
+    assert len(tr.steps) == 8
+    params = list(ref.actor_critic.parameters())
+    for t, rec in enumerate(tr.steps):
+        with torch.no_grad():      # the reference network at the recorded parameters
+            for p, q in zip(params, fus._fused.optimizer.params):
+                off = fus._fused.off[id(q)]
+                p.copy_(rec["p0"][off:off + q.numel()].view_as(p))
+        g_ref = flat_view(fus._fused, list(autograd_grads(ref, rec["idx"]).values()))
+        g = rec["g"].double()
+        bad = ((g - g_ref).abs() > 1e-5 + 2e-3 * g_ref.abs()).sum().item()
+        assert bad == 0, (t, bad, (g - g_ref).abs().max().item())
+        p_want, m_want, v_want = adam64(rec, fus.max_grad_norm)
+        dp = (rec["p1"].double() - p_want).abs()
+        assert (dp <= 1e-6 + 1e-3 * rec["lr"]).all(), (t, dp.max().item(), rec["lr"])
+        assert ((rec["m1"].double() - m_want).abs() <= 1e-5 * m_want.abs() + 1e-12).all(), t
+        assert ((rec["v1"].double() - v_want).abs() <= 2e-5 * v_want.abs() + 1e-18).all(), t
+        if t > 0:   # every step starts from the previous step's result
+            assert torch.equal(rec["p0"], tr.steps[t - 1]["p1"])
