@@ -142,6 +142,8 @@ def parse():
     p.add_argument("--num_envs", type=int, default=4096)
     p.add_argument("--no_cpu_baseline", action="store_true")
     p.add_argument("--cpu_envs", type=int, default=1024)
+    p.add_argument("--actuator_net_torques", action="store_true",
+                   help="ANYmal: the SEA actuator network as the torque source (cfg.control.explicit_torques)")
     return p.parse_args()
 
 
@@ -293,6 +295,8 @@ def main():
     env_cfg = type(env_cfg)()
     train_cfg = type(train_cfg)()
     env_cfg.env.num_envs = args.num_envs
+    if args.actuator_net_torques:
+        env_cfg.control.explicit_torques = True
     env_cfg.seed = 1 + rank
     train_cfg.seed = 1 + rank
     cli = get_args(["--sim_device", device, "--rl_device", device, "--headless", "--task", args.task])
@@ -424,7 +428,9 @@ def main():
         "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": it_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (procedural curriculum terrain, random-init policy)",
-        "config": {"workload": WORKLOADS.get(args.task, args.task) + f", PPO {steps_per_iter} steps x {N} envs/GPU, "
+        "config": {"workload": WORKLOADS.get(args.task, args.task) +
+                               (", SEA actuator-net torques" if args.actuator_net_torques else "") +
+                               f", PPO {steps_per_iter} steps x {N} envs/GPU, "
                                f"{runner.alg.num_learning_epochs} epochs x {runner.alg.num_mini_batches} minibatches",
                    "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
         "roofline": roof,

@@ -53,8 +53,10 @@ enum lgx_reward_term {
 };
 
 /* control paths: position drive (the reference step path, legged_robot.py:93-96) or
- * the explicit-torque `_compute_torques` variants (legged_robot.py:370-392) */
-enum lgx_control { LGX_CTRL_POS_DRIVE = 0, LGX_CTRL_P = 1, LGX_CTRL_V = 2, LGX_CTRL_T = 3 };
+ * the explicit-torque `_compute_torques` variants (legged_robot.py:370-392): the P / V / T laws of
+ * LeggedRobot._compute_torques, or LGX_CTRL_SEA = ANYmal's override (anymal.py:71-78), the SEA
+ * actuator-network LSTM as the torque source (lgx_buffers.sea_*), advanced once per substep */
+enum lgx_control { LGX_CTRL_POS_DRIVE = 0, LGX_CTRL_P = 1, LGX_CTRL_V = 2, LGX_CTRL_T = 3, LGX_CTRL_SEA = 4 };
 
 /* Per-env uniform draws: slot layout of one env's row (stride LGX_DRAW_NOISE + num_obs).
  * In production the draws come from an in-kernel Philox4x32-10 stream keyed by
@@ -191,6 +193,13 @@ typedef struct lgx_buffers {
   float* extras;             /* [T + 2]: episode means per term, terrain_level, reset count */
   uint8_t* extras_time_outs; /* [N] time_outs as last published (stale semantics) */
   float* scratch;            /* [lgx_scratch_floats(N)] reduction partials + completion ticket */
+  /* LGX_CTRL_SEA: the packed SEA LSTM (lgx_actuator_lstm layout) and its hidden / cell state
+   * [2 layers, N*12 joints, 8] (anymal.py:65-69 sea_hidden_state / sea_cell_state); the state of
+   * an env whose episode_length is 0 when a step starts is taken as zero (the reset of
+   * anymal.py:56-60: reset envs have episode_length 0 until their next step) */
+  const float* sea_w;
+  float* sea_h;
+  float* sea_c;
 } lgx_buffers;
 
 typedef struct lgx_sim lgx_sim;

@@ -127,6 +127,10 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   if (params->measure_heights && !bufs->measured_heights) return fail(LGX_EINVAL, "lgx_sim_create: measured_heights is null");
   if (params->use_actuator_history && (!bufs->act_hist || !bufs->model_ins))
     return fail(LGX_EINVAL, "lgx_sim_create: actuator history buffers are null");
+  if (params->control_type < LGX_CTRL_POS_DRIVE || params->control_type > LGX_CTRL_SEA)
+    return fail(LGX_EINVAL, "lgx_sim_create: bad control_type");
+  if (params->control_type == LGX_CTRL_SEA && (!bufs->sea_w || !bufs->sea_h || !bufs->sea_c))
+    return fail(LGX_EINVAL, "lgx_sim_create: LGX_CTRL_SEA needs sea_w / sea_h / sea_c");
   if (params->curriculum && (!bufs->terrain_levels || !bufs->terrain_types || !bufs->terrain_origins))
     return fail(LGX_EINVAL, "lgx_sim_create: curriculum buffers are null");
 

@@ -223,6 +223,61 @@ LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon,
   xl = sym3_mul(Di, t);
 }
 
+// One step of the ANYmal SEA actuator network for joint row r of m (anymal.py:71-78; upstream
+// LSTMsea.forward): x = [a*s + q0 - q, qd] * in_scale -> 2-layer LSTM(2 -> 8) -> Linear(8 -> 1) *
+// out_scale; torch gate order i, f, g, o.  Hidden / cell state in place in global memory ([2, m, 8]:
+// the reference's sea_hidden_state layout, L2-resident across the substeps); `zero`: start from the
+// zero state (reset); `store`: write the new state (false for padding lanes).  Weights are uniform
+// (scalar loads).  Sigmoid 1/(1+exp(-x)) and tanh 1 - 2/(exp(2x)+1) on v_exp_f32 (|err| <= ~2e-7).
+LGX_DEV float sea_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+LGX_DEV float sea_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
+LGX_DEV float sea_lstm(const float* __restrict__ w, float* __restrict__ h, float* __restrict__ c, int64_t r,
+                       int64_t m, float x0, float x1, bool zero, bool store) {
+  const float* Wl = w + 3 + 64 + 256 + 32 + 32 + 256 + 256 + 32 + 32;
+  float inp[8] = {x0 * w[0], x1 * w[1], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int L = 0; L < 2; ++L) {
+    const int ni = L ? 8 : 2;
+    const float* Wih = w + 3 + (L ? 64 + 256 + 64 : 0);
+    const float* Whh = Wih + 32 * ni;
+    const float* bih = Whh + 256;
+    const float* bhh = bih + 32;
+    float4* hp = reinterpret_cast<float4*>(h + ((int64_t)L * m + r) * 8);
+    float4* cp = reinterpret_cast<float4*>(c + ((int64_t)L * m + r) * 8);
+    float4 h0 = hp[0], h1 = hp[1], c0 = cp[0], c1 = cp[1];
+    if (zero) h0 = h1 = c0 = c1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+    float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+    float g[32];
+#pragma unroll
+    for (int gi = 0; gi < 32; ++gi) {
+      float sg = bih[gi] + bhh[gi];
+#pragma unroll
+      for (int i = 0; i < ni; ++i) sg += Wih[gi * ni + i] * inp[i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sg += Whh[gi * 8 + i] * hv[i];
+      g[gi] = sg;
+    }
+    float hn[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cv[k] = sea_sigm(g[8 + k]) * cv[k] + sea_sigm(g[k]) * sea_tanh(g[16 + k]);
+      hn[k] = sea_sigm(g[24 + k]) * sea_tanh(cv[k]);
+      inp[k] = hn[k];
+    }
+    if (store) {
+      hp[0] = make_float4(hn[0], hn[1], hn[2], hn[3]);
+      hp[1] = make_float4(hn[4], hn[5], hn[6], hn[7]);
+      cp[0] = make_float4(cv[0], cv[1], cv[2], cv[3]);
+      cp[1] = make_float4(cv[4], cv[5], cv[6], cv[7]);
+    }
+  }
+  float t = Wl[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t += Wl[i] * inp[i];
+  return w[2] * t;
+}
+
 }  // namespace
 
 #define MAX_LANE_PTS 32
@@ -386,6 +441,32 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     if (ctrl != LGX_CTRL_POS_DRIVE && !from_actions) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) tex[k] = B.torques[(int64_t)ec * 12 + 3 * leg + k];  // caller-provided torques
+    } else if (ctrl == LGX_CTRL_SEA) {
+      // the leg's 3 joints dealt over its PP lanes (joint k on lane p = k % PP, pass k / PP), then
+      // every lane of the leg takes the 3 torques by shuffle; clamped to the drive's effort limit
+      // (PhysX DOF effort mode, URDF effort)
+      constexpr int PASSES = (3 + PP - 1) / PP;
+      float mine[PASSES];
+      const int64_t m = (int64_t)N * 12;
+      const bool fresh = s == 0 && B.episode_length[ec] == 0;
+#pragma unroll
+      for (int q = 0; q < PASSES; ++q) {
+        const int kk = pl + q * PP;
+        const int k = kk < 3 ? kk : 2;
+        const float a = k == 0 ? act[0] : (k == 1 ? act[1] : act[2]);
+        const float qq = k == 0 ? th[0] : (k == 1 ? th[1] : th[2]);
+        const float qd = k == 0 ? thd[0] : (k == 1 ? thd[1] : thd[2]);
+        const int j = 3 * leg + k;
+        mine[q] = sea_lstm(B.sea_w, B.sea_h, B.sea_c, (int64_t)ec * 12 + j, m,
+                           a * P->action_scale + P->default_dof_pos[j] - qq, qd, fresh, valid && kk < 3);
+      }
+      const int base = (threadIdx.x & 63) - 4 * pl;   // this leg's lane p = 0 in the wave
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float t = PP == 1 ? mine[k] : __shfl(mine[k / PP], base + 4 * (k % PP), 64);
+        const float eff = M->dof_effort[3 * leg + k];
+        tex[k] = clampf(t, -eff, eff);
+      }
     } else if (ctrl != LGX_CTRL_POS_DRIVE) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) {

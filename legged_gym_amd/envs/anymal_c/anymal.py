@@ -1,10 +1,14 @@
 """ANYmal-C env (legged_gym/envs/anymal_c/anymal.py:46-80).
 
-The SEA LSTM actuator is only reachable through `_compute_torques`, which this fork's step
-path does not call (the step uses the PhysX position drive, legged_robot.py:93-96); the
-hidden/cell state buffers and `actuator_torques()` (lgx_actuator_lstm, HIP) are provided so
-the LSTM path exists with the reference's semantics (input [a*scale + q0 - q, qd] x in_scale,
-torque = out_scale * Linear(h), state zeroed on reset).
+The SEA LSTM actuator network is only reachable through the reference's `_compute_torques`
+(anymal.py:71-78), which this fork's step path does not call (the step uses the PhysX position
+drive, legged_robot.py:93-96).  Here it is an opt-in torque source of the step itself:
+`cfg.control.explicit_torques = True` with `use_actuator_network = True` (the C5 config's default)
+runs the LSTM inside the physics launch once per substep (LGX_CTRL_SEA: input
+[a * action_scale + q0 - q, qd] x in_scale, torque = out_scale * Linear(h), clamped to the URDF
+effort limit as PhysX's effort-mode drive does), its hidden / cell state [2, N*12, 8] in
+`sea_hidden_state` / `sea_cell_state` and zeroed for envs that reset (anymal.py:56-60).
+`actuator_torques()` runs one LSTM step on its own (lgx_actuator_lstm, HIP).
 """
 import ctypes as C
 
@@ -23,15 +27,25 @@ def pack_lstm_weights(net):
 
 
 class Anymal(LeggedRobot):
+    def _sea_control(self):
+        return getattr(self.cfg.control, "explicit_torques", False) and \
+            getattr(self.cfg.control, "use_actuator_network", False)
+
     def _control_type(self):
-        # explicit torques would be the reference's Anymal._compute_torques, i.e. the SEA LSTM when
-        # use_actuator_network is set (anymal.py:62-78); the step kernel's explicit path is the
-        # P/V/T law of LeggedRobot._compute_torques only, so that combination is refused
-        if getattr(self.cfg.control, "explicit_torques", False) and \
-                getattr(self.cfg.control, "use_actuator_network", False):
-            raise ValueError("Anymal: control.explicit_torques with use_actuator_network=True (the SEA LSTM torque "
-                             "path) is not on the lgx step path; use actuator_torques() or disable one of them")
+        # explicit torques = the reference's Anymal._compute_torques: the SEA LSTM when
+        # use_actuator_network is set (anymal.py:71-78), else LeggedRobot's P / V / T law
+        if self._sea_control():
+            from legged_gym_amd.sim import abi
+            return abi.CTRL["SEA"]
         return LeggedRobot._control_type(self)
+
+    def _actuator_setup(self, params, bufs):
+        if self._sea_control():
+            from legged_gym_amd.envs.base.legged_robot import _ptr
+            bufs.sea_w = _ptr(self.actuator_net_weights)
+            bufs.sea_h = _ptr(self.sea_hidden_state)
+            bufs.sea_c = _ptr(self.sea_cell_state)
+        return super()._actuator_setup(params, bufs)
 
     def _init_buffers(self):
         super()._init_buffers()
@@ -53,7 +67,7 @@ class Anymal(LeggedRobot):
 
     def step(self, actions):
         out = super().step(actions)
-        if getattr(self, "_sea_in_use", False):
+        if getattr(self, "_sea_in_use", False) and not self._sea_control():
             # envs reset inside the step kernel (reset_buf) get the reset_idx zeroing of the LSTM
             # state (anymal.py:56-60); masked multiply, no host synchronisation
             keep = (~self.reset_buf).to(self.sea_hidden_state.dtype).view(1, self.num_envs, 1, 1)

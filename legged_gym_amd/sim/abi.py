@@ -23,7 +23,7 @@ REWARD_IDS = {
     "tracking_ang_vel": 15, "feet_air_time": 16, "stumble": 17, "stand_still": 18,
     "feet_contact_forces": 19, "hip_motion": 20,
 }
-CTRL = {"POS_DRIVE": 0, "P": 1, "V": 2, "T": 3}
+CTRL = {"POS_DRIVE": 0, "P": 1, "V": 2, "T": 3, "SEA": 4}
 
 DRAW_CMD, DRAW_PUSH, DRAW_RESET_DOF, DRAW_RESET_XY = 0, 3, 5, 17
 DRAW_RESET_VEL, DRAW_RESET_CMD, DRAW_CURRIC, DRAW_NOISE = 19, 25, 28, 32
@@ -88,6 +88,7 @@ BUFFER_FIELDS = [
     ("body_mass_scale", PF), ("friction", PF), ("act_hist", PF), ("model_ins", PF),
     ("act_net_w", PF), ("act_net_scale", PF), ("act_dvel", PF),
     ("extras", PF), ("extras_time_outs", PU8), ("scratch", PF),
+    ("sea_w", PF), ("sea_h", PF), ("sea_c", PF),
 ]
 
 

@@ -889,6 +889,40 @@ void lgxo_set_threads(int n) {
 #endif
 }
 
+void lgxo_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t m, const float* w);
+
+/* ANYmal's _compute_torques with use_actuator_network (anymal.py:71-78) as the explicit torque
+ * source of one substep (LGX_CTRL_SEA): sea_input = [a * action_scale + q0 - q, qd] per joint row
+ * (env-major, as sea_input[:, 0, :] = (...).flatten()), one step of the SEA LSTM on the
+ * [2, N*12, 8] hidden / cell state, torques clamped to the drive effort limit (PhysX DOF effort
+ * mode).  The state of an env whose episode_length is 0 when the step starts (reset at the end of
+ * the previous step, anymal.py:56-60) is zeroed first. */
+static void sea_torques(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b, int substep) {
+  const int64_t M = (int64_t)p->num_envs * 12;
+  float* x = (float*)malloc(sizeof(float) * 2 * M);
+  float* tau = (float*)malloc(sizeof(float) * M);
+  for (int e = 0; e < p->num_envs; ++e) {
+    const int fresh = substep == 0 && b->episode_length[e] == 0;
+    for (int j = 0; j < 12; ++j) {
+      const int64_t r = (int64_t)e * 12 + j;
+      x[2 * r] = b->actions[r] * p->action_scale + p->default_dof_pos[j] - b->dof_state[2 * r];
+      x[2 * r + 1] = b->dof_state[2 * r + 1];
+      if (fresh)
+        for (int L = 0; L < 2; ++L) {
+          memset(b->sea_h + ((int64_t)L * M + r) * 8, 0, 8 * sizeof(float));
+          memset(b->sea_c + ((int64_t)L * M + r) * 8, 0, 8 * sizeof(float));
+        }
+    }
+  }
+  lgxo_actuator_lstm(x, b->sea_h, b->sea_c, tau, M, b->sea_w);
+  for (int64_t r = 0; r < M; ++r) {
+    const float eff = m->dof_effort[r % 12];
+    b->torques[r] = clampf(tau[r], -eff, eff);
+  }
+  free(x);
+  free(tau);
+}
+
 /* full LeggedRobot.step (legged_robot.py:79-107) */
 int lgxo_step(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b, const float* draws, int64_t step) {
   ctx_t cx = {m, p, b, draws, LGX_DRAW_NOISE + p->num_obs};
@@ -897,6 +931,7 @@ int lgxo_step(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b,
     if (p->use_actuator_history)
       for (int e = 0; e < p->num_envs; ++e) actuator_history(&cx, e, s);
     if (p->control_type == LGX_CTRL_POS_DRIVE) lgxo_compute_targets(m, p, b);
+    else if (p->control_type == LGX_CTRL_SEA) sea_torques(m, p, b, s);
     else lgxo_explicit_torques(p, b);
 #pragma omp parallel for schedule(static)
     for (int e = 0; e < p->num_envs; ++e) physics_env(&cx, e);

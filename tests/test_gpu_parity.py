@@ -512,6 +512,58 @@ def test_anymal_c_rough_dr_step_matches_oracle(gpu, monkeypatch, pp):
     assert torch.equal(dev.terrain_levels.cpu(), ora.terrain_levels)
 
 
+@pytest.mark.parametrize("pp", ["4", "2", "1"])
+def test_anymal_sea_torque_step_matches_oracle(gpu, monkeypatch, pp):
+    """ANYmal-C with the SEA actuator network as the torque source (LGX_CTRL_SEA: anymal.py:71-78 via
+    cfg.control.explicit_torques; the LSTM advanced in the physics launch once per substep, its
+    joints dealt over the PP lanes of each leg): three env steps from a randomised state with
+    non-zero LSTM state, envs 0-3 timing out in the first step (their LSTM state restarts from zero
+    in the second, anymal.py:56-60), HIP path vs oracle; every lane split of the kernel."""
+    monkeypatch.setenv("LGX_PHYS_PP", pp)
+
+    def ov(c):
+        c.control.explicit_torques = True
+    ora = make_env("anymal_c_rough", num_envs=64, device="cpu", backend="oracle", overrides=ov)
+    dev = make_env("anymal_c_rough", num_envs=64, device="cuda:0", backend="lgx", overrides=ov)
+    from legged_gym_amd.sim import abi
+    assert dev._lgx_params.control_type == abi.CTRL["SEA"]
+    gen = torch.Generator().manual_seed(31)
+    randomize_state(ora, gen)
+    ora._episode_length_buf[:4] = int(ora.max_episode_length)
+    ora.sea_hidden_state.copy_(torch.randn(2, 64 * 12, 8, generator=gen) * 0.3)
+    ora.sea_cell_state.copy_(torch.randn(2, 64 * 12, 8, generator=gen) * 0.3)
+    sync(ora, dev)
+    dev.terrain_types.copy_(ora.terrain_types)
+    ora.common_step_counter = dev.common_step_counter = 3
+    for it in range(3):
+        dev.sea_hidden_state.copy_(ora.sea_hidden_state)
+        dev.sea_cell_state.copy_(ora.sea_cell_state)
+        a = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+        ora.step(a)
+        dev.step(a.cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf), it
+        if it == 0:
+            assert ora.reset_buf[:4].all()
+        if it == 1:   # the envs reset by step 0 restarted their LSTM state from zero
+            assert (dev._episode_length_buf[:4] == 1).all()
+        ok, e = close(dev.sea_hidden_state, ora.sea_hidden_state, 2e-5, 1e-4)
+        assert ok, f"step {it}: sea h max err {e}"
+        ok, e = close(dev.sea_cell_state, ora.sea_cell_state, 2e-5, 1e-4)
+        assert ok, f"step {it}: sea c max err {e}"
+        ok, e = close(dev.torques, ora.torques, 2e-3, 1e-3)
+        assert ok, f"step {it}: torques max err {e}"
+        assert (dev.torques.abs() <= dev.torque_limits + 1e-4).all()
+        keep = ~ora.reset_buf
+        ok, e = close(dev.dof_state.view(64, 12, 2).cpu()[keep], ora.dof_state.view(64, 12, 2)[keep], 5e-3, 2e-3)
+        assert ok, f"step {it}: dof max err {e}"
+        ok, e = close(dev.root_states.cpu()[keep], ora.root_states[keep], 2e-3, 2e-3)
+        assert ok, f"step {it}: root max err {e}"
+        ok, e = close(dev.obs_buf.cpu()[keep], ora.obs_buf[keep], 5e-3, 5e-3)
+        assert ok, f"step {it}: obs max err {e}"
+        sync(ora, dev)   # next step from identical states
+
+
 def test_direct_actions_and_extras_snapshots(gpu):
     """lgx_step_from (policy tensor read in place) == copy-then-lgx_step, the caller's tensor is not
     clipped in place, and every step publishes its own extras snapshot (kernel-written) that

@@ -68,13 +68,16 @@ def test_pd_standing(task, lo, hi):
     assert not env.reset_buf.any()
 
 
-def test_anymal_refuses_explicit_torques_with_lstm():
-    """explicit_torques + use_actuator_network on ANYmal would be the reference's SEA-LSTM
-    _compute_torques (anymal.py:62-78), which the step kernel does not run: refused loudly."""
+def test_anymal_explicit_torques_select_the_sea_network():
+    """explicit_torques on ANYmal = the reference's Anymal._compute_torques (anymal.py:71-78): the
+    SEA LSTM when use_actuator_network is set (LGX_CTRL_SEA), else LeggedRobot's P / V / T law."""
     from types import SimpleNamespace
     from legged_gym_amd.envs.anymal_c.anymal import Anymal
     ctl = SimpleNamespace(explicit_torques=True, use_actuator_network=True, control_type="P")
-    with pytest.raises(ValueError):
-        Anymal._control_type(SimpleNamespace(cfg=SimpleNamespace(control=ctl)))
+    ns = SimpleNamespace(cfg=SimpleNamespace(control=ctl))
+    ns._sea_control = lambda: Anymal._sea_control(ns)
+    assert Anymal._control_type(ns) == abi.CTRL["SEA"]
     ctl.use_actuator_network = False
-    assert Anymal._control_type(SimpleNamespace(cfg=SimpleNamespace(control=ctl))) == abi.CTRL["P"]
+    assert Anymal._control_type(ns) == abi.CTRL["P"]
+    ctl.explicit_torques, ctl.use_actuator_network = False, True
+    assert Anymal._control_type(ns) == abi.CTRL["POS_DRIVE"]
