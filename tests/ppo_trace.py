@@ -10,11 +10,34 @@ import numpy as np
 import torch
 
 
+class _LibSpy:
+    """Forwards every attribute to the product library; the Adam entry points first snapshot the
+    flat gradient they are about to consume (stream-ordered clone: after the backward and the
+    data-parallel all-reduce, before the step clips it in place as clip_grad_norm_ does)."""
+
+    def __init__(self, lib, fused, sink):
+        self._lib, self._fused, self._sink = lib, fused, sink
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        if name not in ("lgx_adam_clip", "lgx_adam_clip_mirror"):
+            return fn
+
+        def wrapped(*args):
+            grad_scale = float(args[7].value if hasattr(args[7], "value") else args[7])
+            self._sink.append((self._fused.flat_g.clone(), grad_scale))
+            return fn(*args)
+        return wrapped
+
+
 class StepTrace:
     def __init__(self, fused):
         self.fused = fused
         self.steps = []
         self._orig = fused._minibatch_body
+        self._orig_lib = fused.lib
+        self._grads = []
+        fused.lib = _LibSpy(fused.lib, fused, self._grads)
 
         def body(idx, obs, cobs, args, stream, apply=True, xs=None):
             f = self.fused
@@ -23,15 +46,19 @@ class StepTrace:
             o = f.optimizer
             rec = dict(idx=idx.clone(), p0=f.flat_p.clone(), m0=o.m.clone(), v0=o.v.clone(),
                        step0=int(o.step_dev.item()))
+            n0 = len(self._grads)
             self._orig(idx, obs, cobs, args, stream, apply, xs)
-            world = f.ppo.dist.get_world_size() if f.ppo.dist is not None else 1
-            rec.update(g=f.flat_g.clone() / world, lr=float(o.lr_dev.item()), p1=f.flat_p.clone(),
-                       m1=o.m.clone(), v1=o.v.clone())
+            assert len(self._grads) == n0 + 1, "one optimizer step per minibatch"
+            g_raw, grad_scale = self._grads[-1]
+            # the gradient of the step: the (all-reduced) sum x grad_scale = the rank average
+            rec.update(g=g_raw * grad_scale, g_clipped=f.flat_g.clone(), lr=float(o.lr_dev.item()),
+                       p1=f.flat_p.clone(), m1=o.m.clone(), v1=o.v.clone())
             self.steps.append(rec)
         fused._minibatch_body = body
 
     def close(self):
         self.fused._minibatch_body = self._orig
+        self.fused.lib = self._orig_lib
 
 
 def adam64(rec, max_norm, betas=(0.9, 0.999), eps=1e-8):
@@ -40,7 +67,7 @@ def adam64(rec, max_norm, betas=(0.9, 0.999), eps=1e-8):
     g = rec["g"].double()
     norm = g.norm().item()
     coef = min(max_norm / (norm + 1e-6), 1.0) if max_norm > 0 else 1.0
-    g = g * coef
+    g = g * coef      # (the step leaves this clipped gradient in the flat gradient buffer)
     b1, b2 = betas
     t = rec["step0"] + 1
     m = b1 * rec["m0"].double() + (1 - b1) * g

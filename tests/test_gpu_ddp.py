@@ -62,7 +62,9 @@ def _worker(rank, world, port, q, early):
         # while dW1 runs; off: one collective after the whole backward
         assert ppo._fused.bucketed == (early == "1")
         if rank == 0:
-            steps = [{k: (v.cpu() if torch.is_tensor(v) else v) for k, v in r.items()} for r in tr.steps]
+            # numpy (pickled by value): CPU tensors would go through shared-memory file descriptors
+            # that die with this process
+            steps = [{k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in r.items()} for r in tr.steps]
             q.put(([p.detach().cpu().numpy() for p in ppo.actor_critic.parameters()] + [ppo.learning_rate], steps))
         dist.barrier()
     finally:
@@ -96,6 +98,7 @@ def test_fused_update_two_ranks_equal_one_process(gpu, early):
     for p in procs:
         p.start()
     got, steps = q.get(timeout=300)
+    steps = [{k: (torch.from_numpy(v) if isinstance(v, np.ndarray) else v) for k, v in r.items()} for r in steps]
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
