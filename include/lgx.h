@@ -200,6 +200,12 @@ typedef struct lgx_buffers {
   const float* sea_w;
   float* sea_h;
   float* sea_c;
+  /* trimesh terrain with the slope correction (terrain.py:70-73: convert_heightfield_to_trimesh
+   * with slope_treshold): per vertex (i, j) of the heightfield, bits 0-3 = move code
+   * (dx + 1) * 3 + (dy + 1) of the corrected mesh (cells, each in {-1, 0, 1}), bit 4 = some vertex
+   * of rows i-1 .. i+2, cols j-1 .. j+2 moved (lgx_trimesh_build).  NULL: contact against the
+   * sampled heightfield itself (mesh_type heightfield, or no correction). */
+  const int8_t* hf_trimesh;
 } lgx_buffers;
 
 typedef struct lgx_sim lgx_sim;
@@ -212,6 +218,20 @@ int lgx_version(void);
  * sizeof(lgx_ppo_store_args), sizeof(lgx_gemm_args), sizeof(lgx_copy2d_job),
  * sizeof(lgx_gemm_tn_args), sizeof(lgx_mlp_x3_desc): lets bindings verify layout */
 void lgx_struct_sizes(int64_t out[12]);
+
+/* Trimesh terrain from the int16 heightfield on the device (isaacgym terrain_utils
+ * convert_heightfield_to_trimesh as called at terrain.py:70-73; legged_robot.py:629-643): with
+ * height_threshold >= 0 (= slope_treshold * (horizontal_scale / vertical_scale) in height units, the
+ * reference's own scaling of cfg.slope_treshold, computed by the caller in double) every vertex
+ * whose neighbour along x, y or the cell diagonal is higher by more than it moves one cell toward
+ * that neighbour; < 0: no correction.  Writes (each output optional, NULL to skip): vertices
+ * float32 [rows * cols, 3] (x = row, y = col on the reference's np.linspace grid in double, + the
+ * moves, then rounded to float; z = height * vertical_scale), triangles uint32
+ * [2 (rows - 1)(cols - 1), 3] ((v00, v11, v01), (v00, v10, v11) per cell), and the contact table
+ * of lgx_buffers.hf_trimesh. */
+int lgx_trimesh_build(const int16_t* height_samples, int32_t rows, int32_t cols, double horizontal_scale,
+                      double vertical_scale, double height_threshold, float* vertices, uint32_t* triangles,
+                      int8_t* contact_table, void* stream);
 
 /* Lanes per leg (1, 2, 4 or 8) of the physics launch at `num_envs` envs, i.e. which
  * lgx_physics_kernel<PP> instantiation lgx_step / lgx_simulate run: 4 below 8192 envs, 2 below

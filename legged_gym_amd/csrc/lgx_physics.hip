@@ -278,6 +278,116 @@ LGX_DEV float sea_lstm(const float* __restrict__ w, float* __restrict__ h, float
   return w[2] * t;
 }
 
+// ---- contact against the slope-corrected trimesh (terrain.py:70-73; the mesh of legged_robot.py:629-643)
+// closest point of triangle abc to p (Voronoi-region walk: Ericson, Real-Time Collision Detection 5.1.5)
+LGX_DEV f3 closest_on_tri(f3 p, f3 a, f3 b, f3 c) {
+  const f3 ab = b - a, ac = c - a, ap = p - a;
+  const float d1 = dot(ab, ap), d2 = dot(ac, ap);
+  if (d1 <= 0.f && d2 <= 0.f) return a;
+  const f3 bp = p - b;
+  const float d3 = dot(ab, bp), d4 = dot(ac, bp);
+  if (d3 >= 0.f && d4 <= d3) return b;
+  const float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + (d1 / (d1 - d3)) * ab;
+  const f3 cq = p - c;
+  const float d5 = dot(ab, cq), d6 = dot(ac, cq);
+  if (d6 >= 0.f && d5 <= d6) return c;
+  const float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + (d2 / (d2 - d6)) * ac;
+  const float va = d3 * d6 - d5 * d4;
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + ((d4 - d3) / ((d4 - d3) + (d5 - d6))) * (c - b);
+  const float den = 1.f / (va + vb + vc);
+  return a + (vb * den) * ab + (vc * den) * ac;
+}
+
+// one triangle of the query: nearest point so far (squared distance, point, face normal) and the
+// highest surface among the triangles whose xy projection holds p (height, face normal)
+struct TmQuery { float d2; f3 cp, cn; float top; f3 tn; };
+LGX_DEV void tm_tri(TmQuery& q, f3 p, f3 a, f3 b, f3 c) {
+  const f3 e1 = b - a, e2 = c - a;
+  f3 nf = cross(e1, e2);
+  const float nl = sqrtf(dot(nf, nf));
+  if (!(nl > 1e-12f)) return;                       // degenerate in 3D
+  nf = (nf.z < 0.f ? -1.f : 1.f) / nl * nf;         // oriented up
+  const f3 cp = closest_on_tri(p, a, b, c);
+  const f3 dv = p - cp;
+  const float d2 = dot(dv, dv);
+  if (d2 < q.d2) { q.d2 = d2; q.cp = cp; q.cn = nf; }
+  const float den = e1.x * e2.y - e1.y * e2.x;      // 2 x signed xy area (0 for vertical faces)
+  if (fabsf(den) > 1e-9f) {
+    const float px = p.x - a.x, py = p.y - a.y;
+    const float s = (px * e2.y - py * e2.x) / den, t = (e1.x * py - e1.y * px) / den;
+    if (s >= -1e-6f && t >= -1e-6f && s + t <= 1.f + 1e-6f) {
+      const float hz = a.z + s * e1.z + t * e2.z;
+      if (hz > q.top) { q.top = hz; q.tn = nf; }
+    }
+  }
+}
+
+// Signed contact depth of a sphere (radius r >= 0, centre p, world frame) against the corrected
+// mesh around cell (i, j): the nearest surface point over the two triangles of each cell of the
+// 3 x 3 cells around (i, j) (the moves are at most one cell, so every face within r < one cell of
+// p is among them), inside = p below the surface under it; depth = r -/+ distance, normal = from
+// the surface point toward p (outside) or from p toward it (inside).  Where p sits on the surface,
+// the face normal.
+LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
+                            f3* n, const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
+  const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
+  const int rows = B.hf_rows, cols = B.hf_cols;
+  TmQuery q;
+  q.d2 = 3.0e38f; q.cp = p; q.cn = mk3(0.f, 0.f, 1.f);
+  q.top = -3.0e38f; q.tn = mk3(0.f, 0.f, 1.f);
+  for (int ci = max(i - 1, 0); ci <= min(i + 1, rows - 2); ++ci)
+    for (int cj = max(j - 1, 0); cj <= min(j + 1, cols - 2); ++cj) {
+      f3 v[4];   // (ci, cj), (ci + 1, cj), (ci, cj + 1), (ci + 1, cj + 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int a = ci + (k & 1), b = cj + (k >> 1);
+        const int li = a - pi0, lj = b - pj0;
+        int h, code;
+        if (hpatch && (unsigned)li < LGX_HF_PATCH && (unsigned)lj < LGX_HF_PATCH) {
+          h = hpatch[li * LGX_HF_PATCH + lj];
+          code = tpatch[li * LGX_HF_PATCH + lj] & 15;
+        } else {
+          h = B.height_samples[(int64_t)a * cols + b];
+          code = B.hf_trimesh[(int64_t)a * cols + b] & 15;
+        }
+        const int dx = ((code * 11) >> 5) - 1, dy = code - 3 * (dx + 1) - 1;
+        v[k] = mk3((float)(a + dx) * hs - bo, (float)(b + dy) * hs - bo, (float)h * vs);
+      }
+      tm_tri(q, p, v[0], v[3], v[2]);   // reference triangle order (ind0, ind3, ind1), (ind0, ind2, ind3)
+      tm_tri(q, p, v[0], v[1], v[3]);
+    }
+  const bool inside = p.z < q.top;
+  const float d = sqrtf(q.d2);
+  if (d > 1e-7f) {
+    const float inv = 1.f / d;
+    *n = inside ? inv * (q.cp - p) : inv * (p - q.cp);
+  } else {
+    *n = q.top > -1e30f ? q.tn : q.cn;
+  }
+  return inside ? r + d : r - d;
+}
+
+// Ground contact of a sphere / point (radius r) centred at world p: the corrected trimesh where its
+// contact table flags the cell (near a moved vertex), else the triangulated heightfield under p
+// (identical there: no vertex of the neighbourhood moved) with depth along its face normal.
+LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, f3* n,
+                             const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
+  if (B.hf_trimesh && P->terrain_kind != 0 && B.height_samples) {
+    const float hs = P->horizontal_scale;
+    int i = (int)floorf((p.x + P->border_size) / hs), j = (int)floorf((p.y + P->border_size) / hs);
+    i = min(max(i, 0), B.hf_rows - 2);
+    j = min(max(j, 0), B.hf_cols - 2);
+    const int li = i - pi0, lj = j - pj0;
+    const int tm = (tpatch && (unsigned)li < LGX_HF_PATCH && (unsigned)lj < LGX_HF_PATCH)
+                       ? tpatch[li * LGX_HF_PATCH + lj] : B.hf_trimesh[(int64_t)i * B.hf_cols + j];
+    if (tm & 16) return trimesh_depth(P, B, p, r, i, j, n, hpatch, tpatch, pi0, pj0);
+  }
+  const float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, p.x, p.y, n, hpatch, pi0, pj0);
+  return (h - p.z) * n->z + r;
+}
+
 }  // namespace
 
 #define MAX_LANE_PTS 32
@@ -323,6 +433,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   __shared__ float leg_sys[ENVS * 4][36];           // contact-free leg system: B 18, D 6, rb 6, rl 3
   __shared__ float env_com[ENVS][40];               // base block 21, its rhs 6, base rotation 9
   __shared__ int16_t hf_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];  // terrain around each base
+  __shared__ int8_t tm_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];   // its trimesh contact table
   __shared__ int32_t hf_org[ENVS][2];
   {
     const int4* src = reinterpret_cast<const int4*>(DMg);
@@ -403,11 +514,14 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     for (int q = tid; q < ENVS * LGX_HF_PATCH * LGX_HF_PATCH; q += PHYS_BLOCK) {
       const int ee = q / (LGX_HF_PATCH * LGX_HF_PATCH), r = q % (LGX_HF_PATCH * LGX_HF_PATCH);
       const int li = r / LGX_HF_PATCH, lj = r % LGX_HF_PATCH;
-      hf_patch[ee][r] = B.height_samples[(int64_t)(hf_org[ee][0] + li) * B.hf_cols + hf_org[ee][1] + lj];
+      const int64_t gi = (int64_t)(hf_org[ee][0] + li) * B.hf_cols + hf_org[ee][1] + lj;
+      hf_patch[ee][r] = B.height_samples[gi];
+      if (B.hf_trimesh) tm_patch[ee][r] = B.hf_trimesh[gi];
     }
     __syncthreads();
   }
   const int16_t* patch = use_patch ? hf_patch[eb] : nullptr;
+  const int8_t* tpatch = use_patch ? tm_patch[eb] : nullptr;
   const int pi0 = use_patch ? hf_org[eb][0] : 0, pj0 = use_patch ? hf_org[eb][1] : 0;
   const int npts = DM->lane_npts[leg];
   const int maxpts = DM->max_lane_npts;
@@ -651,10 +765,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
           for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
           f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
           f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
-          float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, Pp.x + pos.x, Pp.y + pos.y, &n, patch,
-                                  pi0, pj0);
-          float rad = M->point_radius[pi];
-          depth = (h - (Pp.z + pos.z)) * n.z + rad;
+          const float rad = M->point_radius[pi];
+          depth = ground_contact(P, B, Pp + pos, rad, &n, patch, tpatch, pi0, pj0);
           st.x = depth > 0.f ? 1.f : 0.f;
           slot_state[sl][tid] = st;
           if (depth <= 0.f) continue;

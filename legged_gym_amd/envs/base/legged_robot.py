@@ -528,11 +528,39 @@ class LeggedRobot(BaseTask):
             self.height_samples = self.height_samples.contiguous()
             b.height_samples = _ptr(self.height_samples, abi.PI16)
             b.hf_rows, b.hf_cols = self.height_samples.shape
+            self.hf_trimesh = self._trimesh_contact_table()
+            if self.hf_trimesh is not None:
+                b.hf_trimesh = C.cast(C.c_void_p(self.hf_trimesh.data_ptr()), C.POINTER(C.c_int8))
         self._actuator_setup(p, b)
         self._lgx_params, self._lgx_bufs = p, b
         self._obs_bufs = [self.obs_buf, torch.zeros_like(self.obs_buf)]
         self._obs_slot = 0
         self._backend = self._make_backend(self._lgx_model, p, b)
+
+    def _trimesh_contact_table(self):
+        """mesh_type 'trimesh' with a slope threshold: the contact table of the slope-corrected mesh
+        (terrain.py:70-73) - built on the device by lgx_trimesh_build on the GPU path, from the
+        numpy restatement (utils/terrain.py) for CPU tensors (the oracle backend).  None: contact
+        against the heightfield itself (mesh_type 'heightfield': PhysX heightfield, no correction)."""
+        tcfg = self.cfg.terrain
+        if tcfg.mesh_type != "trimesh" or getattr(tcfg, "slope_treshold", None) is None:
+            return None
+        R, Cc = self.height_samples.shape
+        thr = tcfg.slope_treshold * (tcfg.horizontal_scale / tcfg.vertical_scale)   # (the library's scaling)
+        if self.height_samples.is_cuda:
+            from legged_gym_amd.sim import lib as lgxlib
+            lib = lgxlib.load()
+            table = torch.empty(R, Cc, dtype=torch.int8, device=self.device)
+            lgxlib.check(lib.lgx_trimesh_build(C.c_void_p(self.height_samples.data_ptr()), R, Cc, tcfg.horizontal_scale,
+                                               tcfg.vertical_scale, thr, None, None, C.c_void_p(table.data_ptr()),
+                                               C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                         "lgx_trimesh_build")
+            return table
+        from legged_gym_amd.utils.terrain import trimesh_contact_tables, trimesh_vertex_moves
+        dx, dy = trimesh_vertex_moves(self.height_samples.cpu().numpy(), tcfg.horizontal_scale, tcfg.vertical_scale,
+                                      tcfg.slope_treshold)
+        code, flag = trimesh_contact_tables(dx, dy)
+        return torch.from_numpy((code | (flag << 4)).astype(np.int8)).to(self.device)
 
     def _scratch_floats(self):
         blocks = (self.num_envs + abi.ENV_BLOCK - 1) // abi.ENV_BLOCK  # >= lgx_scratch_floats()

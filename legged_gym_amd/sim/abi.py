@@ -88,7 +88,7 @@ BUFFER_FIELDS = [
     ("body_mass_scale", PF), ("friction", PF), ("act_hist", PF), ("model_ins", PF),
     ("act_net_w", PF), ("act_net_scale", PF), ("act_dvel", PF),
     ("extras", PF), ("extras_time_outs", PU8), ("scratch", PF),
-    ("sea_w", PF), ("sea_h", PF), ("sea_c", PF),
+    ("sea_w", PF), ("sea_h", PF), ("sea_c", PF), ("hf_trimesh", C.POINTER(C.c_int8)),
 ]
 
 
@@ -184,6 +184,7 @@ def declare(lib, prefix="lgx"):
     if prefix == "lgx":  # PPO update entry points: product library only
         sigs.update({
             "physics_lane_split": (i32, [i32]),
+            "trimesh_build": (C.c_int, [vp, i32, i32, C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]),
             "step_from": (C.c_int, [vp, vp, i64, vp]),
             "drive_inputs": (C.c_int, [vp, vp, vp]),
             "sync_aux": (C.c_int, [vp, vp]),
@@ -228,7 +229,7 @@ def declare(lib, prefix="lgx"):
     return lib
 
 
-EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
+EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trimesh_build", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
             "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_step_from", "lgx_drive_inputs", "lgx_sync_aux",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",

@@ -127,6 +127,78 @@ def pit_terrain(t, depth, platform_size=1.0):  # terrain.py:180-187
     t.height_field_raw[x1:x2, y1:y2] = -d
 
 
+def trimesh_vertex_moves(height_field_raw, horizontal_scale, vertical_scale, slope_threshold):
+    """The slope correction of isaacgym.terrain_utils.convert_heightfield_to_trimesh (called at
+    terrain.py:70-73 with cfg.slope_treshold, legged_robot_config.py:68): a vertex whose neighbour
+    along x, y or the cell diagonal rises by more than slope_threshold * horizontal_scale moves one
+    cell toward it, so a steep one-cell ramp becomes a vertical wall.  Returns the per-vertex move
+    (dx, dy) in cells, int8 [rows, cols] each, in {-1, 0, 1} (restated from the published
+    algorithm; the library is absent: parity unpinned).  Heights are compared as int32 (the int16
+    differences of realistic terrains never wrap)."""
+    hf = np.asarray(height_field_raw).astype(np.int32)
+    R, Cc = hf.shape
+    thr = slope_threshold * (horizontal_scale / vertical_scale)   # (the library's `*=` order)
+    move_x = np.zeros((R, Cc), np.int32)
+    move_y = np.zeros((R, Cc), np.int32)
+    move_c = np.zeros((R, Cc), np.int32)
+    move_x[:R - 1, :] += hf[1:, :] - hf[:R - 1, :] > thr
+    move_x[1:, :] -= hf[:R - 1, :] - hf[1:, :] > thr
+    move_y[:, :Cc - 1] += hf[:, 1:] - hf[:, :Cc - 1] > thr
+    move_y[:, 1:] -= hf[:, :Cc - 1] - hf[:, 1:] > thr
+    move_c[:R - 1, :Cc - 1] += hf[1:, 1:] - hf[:R - 1, :Cc - 1] > thr
+    move_c[1:, 1:] -= hf[:R - 1, :Cc - 1] - hf[1:, 1:] > thr
+    dx = move_x + move_c * (move_x == 0)
+    dy = move_y + move_c * (move_y == 0)
+    return dx.astype(np.int8), dy.astype(np.int8)
+
+
+def convert_heightfield_to_trimesh(height_field_raw, horizontal_scale, vertical_scale, slope_threshold=None):
+    """isaacgym.terrain_utils.convert_heightfield_to_trimesh, vectorised (terrain.py:70-73): vertices
+    float32 [rows * cols, 3] (grid x = row * horizontal_scale, y = col * horizontal_scale, as
+    np.linspace, + the slope-correction moves; z = height * vertical_scale) and triangles uint32
+    [2 (rows - 1)(cols - 1), 3], two per cell: (v00, v11, v01), (v00, v10, v11).  Parity UNPINNED
+    (isaacgym absent); tests check the construction's invariants."""
+    hf = np.asarray(height_field_raw)
+    R, Cc = hf.shape
+    y = np.linspace(0, (Cc - 1) * horizontal_scale, Cc)
+    x = np.linspace(0, (R - 1) * horizontal_scale, R)
+    yy, xx = np.meshgrid(y, x)
+    if slope_threshold is not None:
+        dx, dy = trimesh_vertex_moves(hf, horizontal_scale, vertical_scale, slope_threshold)
+        xx = xx + dx * horizontal_scale
+        yy = yy + dy * horizontal_scale
+    vertices = np.zeros((R * Cc, 3), dtype=np.float32)
+    vertices[:, 0] = xx.flatten()
+    vertices[:, 1] = yy.flatten()
+    vertices[:, 2] = hf.flatten() * vertical_scale
+    i = np.arange(R - 1, dtype=np.int64)[:, None]
+    j = np.arange(Cc - 1, dtype=np.int64)[None, :]
+    ind0 = (i * Cc + j).ravel()
+    ind1, ind2 = ind0 + 1, ind0 + Cc
+    ind3 = ind2 + 1
+    triangles = np.empty((2 * ind0.size, 3), dtype=np.uint32)
+    triangles[0::2] = np.stack([ind0, ind3, ind1], 1)
+    triangles[1::2] = np.stack([ind0, ind2, ind3], 1)
+    return vertices, triangles
+
+
+def trimesh_contact_tables(dx, dy):
+    """The physics kernels' view of the corrected mesh: per-vertex move code (dx + 1) * 3 + (dy + 1)
+    (4 = unmoved) and a per-cell flag = some vertex of the 4 x 4 block around cell (i, j) (rows
+    i-1 .. i+2, cols j-1 .. j+2) moved, i.e. a query in that cell may be near a corrected (vertical)
+    face and takes the closest-point query over the neighbouring triangles."""
+    code = ((dx.astype(np.int16) + 1) * 3 + (dy.astype(np.int16) + 1)).astype(np.int8)
+    moved = (dx != 0) | (dy != 0)
+    R, Cc = moved.shape
+    pad = np.zeros((R + 3, Cc + 3), dtype=bool)
+    pad[1:R + 1, 1:Cc + 1] = moved
+    flag = np.zeros((R, Cc), dtype=bool)
+    for a in range(4):
+        for b in range(4):
+            flag |= pad[a:a + R, b:b + Cc]
+    return code, flag.astype(np.int8)
+
+
 class Terrain:
     """terrain.py:38-164."""
 
@@ -154,6 +226,13 @@ class Terrain:
         else:
             self._randomized()
         self.heightsamples = self.height_field_raw
+        if self.type == "trimesh":   # terrain.py:70-73
+            self.vertices, self.triangles = convert_heightfield_to_trimesh(
+                self.height_field_raw, cfg.horizontal_scale, cfg.vertical_scale, cfg.slope_treshold)
+            if cfg.slope_treshold is not None:
+                dx, dy = trimesh_vertex_moves(self.height_field_raw, cfg.horizontal_scale, cfg.vertical_scale,
+                                              cfg.slope_treshold)
+                self.vertex_moves, self.wall_flags = trimesh_contact_tables(dx, dy)
 
     def _randomized(self):
         for k in range(self.cfg.num_sub_terrains):

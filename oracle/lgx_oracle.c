@@ -174,6 +174,122 @@ static float ground(const ctx_t* cx, float x, float y, float* n) {
   return h;
 }
 
+/* ---- contact against the slope-corrected trimesh (terrain.py:70-73, legged_robot.py:629-643;
+ * lgx_buffers.hf_trimesh): same model as the kernel, restated on plain arrays.  Closest point of a
+ * triangle: Ericson, Real-Time Collision Detection 5.1.5. */
+static void v3(float* o, float x, float y, float z) { o[0] = x; o[1] = y; o[2] = z; }
+static void sub3(const float* a, const float* b, float* o) { v3(o, a[0] - b[0], a[1] - b[1], a[2] - b[2]); }
+static void axpy3(const float* a, float s, const float* d, float* o) { v3(o, a[0] + s * d[0], a[1] + s * d[1], a[2] + s * d[2]); }
+
+static void closest_on_tri(const float* p, const float* a, const float* b, const float* c, float* o) {
+  float ab[3], ac[3], ap[3], bp[3], cq[3], bc[3];
+  sub3(b, a, ab); sub3(c, a, ac); sub3(p, a, ap);
+  float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { memcpy(o, a, 12); return; }
+  sub3(p, b, bp);
+  float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { memcpy(o, b, 12); return; }
+  float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) { axpy3(a, d1 / (d1 - d3), ab, o); return; }
+  sub3(p, c, cq);
+  float d5 = dot3(ab, cq), d6 = dot3(ac, cq);
+  if (d6 >= 0 && d5 <= d6) { memcpy(o, c, 12); return; }
+  float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) { axpy3(a, d2 / (d2 - d6), ac, o); return; }
+  float va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    sub3(c, b, bc);
+    axpy3(b, (d4 - d3) / ((d4 - d3) + (d5 - d6)), bc, o);
+    return;
+  }
+  float den = 1.0f / (va + vb + vc);
+  float t[3];
+  axpy3(a, vb * den, ab, t);
+  axpy3(t, vc * den, ac, o);
+}
+
+typedef struct { float d2, cp[3], cn[3], top, tn[3]; } tmq_t;
+
+static void tm_tri(tmq_t* q, const float* p, const float* a, const float* b, const float* c) {
+  float e1[3], e2[3], nf[3];
+  sub3(b, a, e1); sub3(c, a, e2);
+  cross3(e1, e2, nf);
+  float nl = sqrtf(dot3(nf, nf));
+  if (!(nl > 1e-12f)) return;
+  float sgn = nf[2] < 0 ? -1.0f : 1.0f;
+  for (int k = 0; k < 3; ++k) nf[k] = sgn / nl * nf[k];
+  float cp[3], dv[3];
+  closest_on_tri(p, a, b, c, cp);
+  sub3(p, cp, dv);
+  float d2 = dot3(dv, dv);
+  if (d2 < q->d2) { q->d2 = d2; memcpy(q->cp, cp, 12); memcpy(q->cn, nf, 12); }
+  float den = e1[0] * e2[1] - e1[1] * e2[0];
+  if (fabsf(den) > 1e-9f) {
+    float px = p[0] - a[0], py = p[1] - a[1];
+    float s = (px * e2[1] - py * e2[0]) / den, t = (e1[0] * py - e1[1] * px) / den;
+    if (s >= -1e-6f && t >= -1e-6f && s + t <= 1.0f + 1e-6f) {
+      float hz = a[2] + s * e1[2] + t * e2[2];
+      if (hz > q->top) { q->top = hz; memcpy(q->tn, nf, 12); }
+    }
+  }
+}
+
+/* signed depth of a sphere (radius r, centre p world) against the corrected mesh of the 3 x 3
+ * cells around (i, j): nearest surface point, inside = below the surface under p */
+static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int j, float* n) {
+  const lgx_env_params* P = cx->p;
+  const lgx_buffers* b = cx->b;
+  const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
+  const int rows = b->hf_rows, cols = b->hf_cols;
+  tmq_t q;
+  q.d2 = 3.0e38f; memcpy(q.cp, p, 12); v3(q.cn, 0, 0, 1);
+  q.top = -3.0e38f; v3(q.tn, 0, 0, 1);
+  for (int ci = i - 1 < 0 ? 0 : i - 1; ci <= (i + 1 < rows - 2 ? i + 1 : rows - 2); ++ci)
+    for (int cj = j - 1 < 0 ? 0 : j - 1; cj <= (j + 1 < cols - 2 ? j + 1 : cols - 2); ++cj) {
+      float v[4][3];
+      for (int k = 0; k < 4; ++k) {
+        int a = ci + (k & 1), bb = cj + (k >> 1);
+        int h = b->height_samples[(int64_t)a * cols + bb];
+        int code = b->hf_trimesh[(int64_t)a * cols + bb] & 15;
+        int dx = code / 3 - 1, dy = code % 3 - 1;
+        v3(v[k], (float)(a + dx) * hs - bo, (float)(bb + dy) * hs - bo, (float)h * vs);
+      }
+      tm_tri(&q, p, v[0], v[3], v[2]);
+      tm_tri(&q, p, v[0], v[1], v[3]);
+    }
+  int inside = p[2] < q.top;
+  float d = sqrtf(q.d2);
+  if (d > 1e-7f) {
+    float inv = 1.0f / d;
+    for (int k = 0; k < 3; ++k) n[k] = inside ? inv * (q.cp[k] - p[k]) : inv * (p[k] - q.cp[k]);
+  } else {
+    memcpy(n, q.top > -1e30f ? q.tn : q.cn, 12);
+  }
+  return inside ? r + d : r - d;
+}
+
+/* ground contact depth of a sphere / point: the corrected trimesh where the contact table flags
+ * the cell, else the heightfield triangle under p with depth along its face normal */
+static float ground_contact(const ctx_t* cx, const float* p, float r, float* n) {
+  const lgx_env_params* P = cx->p;
+  const lgx_buffers* b = cx->b;
+  if (b->hf_trimesh && P->terrain_kind != 0 && b->height_samples) {
+    int i = (int)floorf((p[0] + P->border_size) / P->horizontal_scale);
+    int j = (int)floorf((p[1] + P->border_size) / P->horizontal_scale);
+    if (i < 0) i = 0; if (i > b->hf_rows - 2) i = b->hf_rows - 2;
+    if (j < 0) j = 0; if (j > b->hf_cols - 2) j = b->hf_cols - 2;
+    if (b->hf_trimesh[(int64_t)i * b->hf_cols + j] & 16) return trimesh_depth(cx, p, r, i, j, n);
+  }
+  float h = ground(cx, p[0], p[1], n);
+  return (h - p[2]) * n[2] + r;
+}
+
+/* test entry: ground_contact at world point p (radius r): depth, normal n[3] */
+float lgxo_ground_contact(const lgx_env_params* p, const lgx_buffers* b, const float* pt, float r, float* n) {
+  ctx_t cx = {NULL, p, b, NULL, 0};
+  return ground_contact(&cx, pt, r, n);
+}
+
 /* ------------------------------------------------------------------ physics substep */
 typedef struct {
   float R[LGX_NUM_DYN][9];  /* body rotation (world) */
@@ -405,8 +521,8 @@ static void physics_env(const ctx_t* cx, int e) {
     float P[3]; matvec3(K.R[b], m->point_pos[i], P);
     for (int k = 0; k < 3; ++k) P[k] += K.o[b][k];
     float n[3];
-    float h = ground(cx, P[0] + rs[0], P[1] + rs[1], n);
-    float depth = (h - (P[2] + rs[2])) * n[2] + m->point_radius[i];
+    const float Pw[3] = {P[0] + rs[0], P[1] + rs[1], P[2] + rs[2]};
+    float depth = ground_contact(cx, Pw, m->point_radius[i], n);
     if (depth <= 0.0f) continue;
     contact_t* c = &C[nc++];
     c->body = b; c->report = m->point_report[i];

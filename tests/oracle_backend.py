@@ -39,6 +39,7 @@ def load_oracle():
         "lgxo_actuator_lstm": (None, [vp, vp, vp, vp, i64, vp]),
         "lgxo_uniform": (C.c_float, [C.c_uint64, i32, i32, i64, C.c_uint32]),
         "lgxo_struct_sizes": (None, [C.POINTER(C.c_int64)]),
+        "lgxo_ground_contact": (C.c_float, [P, B, vp, C.c_float, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)

@@ -1,0 +1,101 @@
+"""GPU: the trimesh terrain on the device (lgx_trimesh_build: isaacgym terrain_utils
+convert_heightfield_to_trimesh with the slope correction, terrain.py:70-73) against the numpy
+restatement (utils/terrain.py, itself checked against the published algorithm in
+tests/test_terrain.py) bit for bit, and the physics on a slope-corrected stair (feet against
+vertical risers: the closest-point contact on the corrected mesh) against the oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from oracle_backend import make_env
+from test_gpu_parity import close, randomize_state, sync
+
+pytestmark = pytest.mark.gpu
+
+
+def test_trimesh_build_matches_numpy(gpu):
+    from legged_gym_amd.sim import lib as lgxlib
+    from legged_gym_amd.utils.terrain import (convert_heightfield_to_trimesh, trimesh_contact_tables,
+                                              trimesh_vertex_moves)
+    env = make_env("go1_rough", num_envs=16, device="cuda:0", backend="lgx")
+    tc = env.cfg.terrain
+    hf = env.height_samples
+    R, Cc = hf.shape
+    lib = lgxlib.load()
+    vert = torch.empty(R * Cc, 3, device=gpu)
+    tri = torch.empty(2 * (R - 1) * (Cc - 1), 3, dtype=torch.int32, device=gpu)
+    tab = torch.empty(R, Cc, dtype=torch.int8, device=gpu)
+    thr = tc.slope_treshold * (tc.horizontal_scale / tc.vertical_scale)
+    lgxlib.check(lib.lgx_trimesh_build(C.c_void_p(hf.data_ptr()), R, Cc, tc.horizontal_scale, tc.vertical_scale, thr,
+                                       C.c_void_p(vert.data_ptr()), C.c_void_p(tri.data_ptr()),
+                                       C.c_void_p(tab.data_ptr()), None), "trimesh_build")
+    torch.cuda.synchronize()
+    h = hf.cpu().numpy()
+    v_ref, t_ref = convert_heightfield_to_trimesh(h, tc.horizontal_scale, tc.vertical_scale, tc.slope_treshold)
+    np.testing.assert_array_equal(vert.cpu().numpy(), v_ref)
+    np.testing.assert_array_equal(tri.cpu().numpy().view(np.uint32), t_ref)
+    code, flag = trimesh_contact_tables(*trimesh_vertex_moves(h, tc.horizontal_scale, tc.vertical_scale, tc.slope_treshold))
+    np.testing.assert_array_equal(tab.cpu().numpy(), (code | (flag << 4)).astype(np.int8))
+    assert torch.equal(env.hf_trimesh.cpu(), tab.cpu())        # the table the env's physics reads
+    assert (flag == 1).mean() > 0.05                            # the curriculum's stairs are corrected
+
+
+def _stair_field(shape, seed):
+    """Stairs along x over the whole map (treads 2-4 cells, risers 0.08-0.2 m), plus random steps
+    along y every few metres: every foot is near a vertical face of the corrected mesh."""
+    rng = np.random.default_rng(seed)
+    R, Cc = shape
+    hf = np.zeros(shape, np.int16)
+    h, i = 0, 0
+    while i < R:
+        w = int(rng.integers(2, 5))
+        hf[i:i + w, :] = h
+        h += int(rng.integers(16, 40)) * (1 if rng.random() < 0.7 else -1)
+        i += w
+    for j in range(0, Cc, 37):
+        hf[:, j:j + 3] += int(rng.integers(16, 30))
+    return hf
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_physics_on_corrected_stairs_matches_oracle(gpu, seed):
+    ora = make_env("go1_rough", num_envs=64, device="cpu", backend="oracle")
+    dev = make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
+    hf = torch.from_numpy(_stair_field(tuple(ora.height_samples.shape), seed))
+    for e in (ora, dev):
+        e.height_samples.copy_(hf.to(e.device))
+        e.hf_trimesh.copy_(e._trimesh_contact_table())
+    assert torch.equal(ora.hf_trimesh, dev.hf_trimesh.cpu())
+    gen = torch.Generator().manual_seed(100 + seed)
+    randomize_state(ora, gen)
+    # stand the robots on the stair surface under their base
+    hs, bo = ora.cfg.terrain.horizontal_scale, ora.cfg.terrain.border_size
+    ij = ((ora.root_states[:, :2] + bo) / hs).long()
+    ground = hf[ij[:, 0].clamp(0, hf.shape[0] - 1), ij[:, 1].clamp(0, hf.shape[1] - 1)].float() * ora.cfg.terrain.vertical_scale
+    ora.root_states[:, 2] = ground + 0.26 + 0.08 * torch.rand(64, generator=gen)
+    sync(ora, dev)
+    dev.terrain_types.copy_(ora.terrain_types)
+    flagged = 0
+    for it in range(3):
+        ora.common_step_counter = dev.common_step_counter = 5 + it
+        a = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+        ora.step(a)
+        dev.step(a.cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf), it
+        keep = ~ora.reset_buf
+        ok, e = close(dev.root_states.cpu()[keep], ora.root_states[keep], 2e-3, 2e-3)
+        assert ok, f"step {it}: root max err {e}"
+        ok, e = close(dev.dof_state.view(64, 12, 2).cpu()[keep], ora.dof_state.view(64, 12, 2)[keep], 5e-3, 2e-3)
+        assert ok, f"step {it}: dof max err {e}"
+        ok, e = close(dev.contact_forces.cpu()[keep], ora.contact_forces[keep], 0.05, 5e-3)
+        assert ok, f"step {it}: contact force max err {e}"
+        ok, e = close(dev.obs_buf.cpu()[keep], ora.obs_buf[keep], 5e-3, 5e-3)
+        assert ok, f"step {it}: obs max err {e}"
+        # the feet really are on flagged (corrected-mesh) cells and in contact
+        feet_f = ora.contact_forces[:, ora.feet_indices].norm(dim=-1)
+        flagged += int((feet_f > 1.0).sum())
+        sync(ora, dev)
+    assert flagged > 64
