@@ -355,6 +355,12 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
         const int dx = ((code * 11) >> 5) - 1, dy = code - 3 * (dx + 1) - 1;
         v[k] = mk3((float)(a + dx) * hs - bo, (float)(b + dy) * hs - bo, (float)h * vs);
       }
+      // cull: p more than r above every vertex of the cell (no contact, not below its surface) or
+      // outside its xy box grown by r (farther than r, not over it): most queries keep one cell
+      const float zmax = fmaxf(fmaxf(v[0].z, v[1].z), fmaxf(v[2].z, v[3].z));
+      const float xmin = fminf(fminf(v[0].x, v[1].x), fminf(v[2].x, v[3].x)), xmax = fmaxf(fmaxf(v[0].x, v[1].x), fmaxf(v[2].x, v[3].x));
+      const float ymin = fminf(fminf(v[0].y, v[1].y), fminf(v[2].y, v[3].y)), ymax = fmaxf(fmaxf(v[0].y, v[1].y), fmaxf(v[2].y, v[3].y));
+      if (p.z - r > zmax || p.x < xmin - r || p.x > xmax + r || p.y < ymin - r || p.y > ymax + r) continue;
       tm_tri(q, p, v[0], v[3], v[2]);   // reference triangle order (ind0, ind3, ind1), (ind0, ind2, ind3)
       tm_tri(q, p, v[0], v[1], v[3]);
     }

@@ -254,6 +254,13 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
         int dx = code / 3 - 1, dy = code % 3 - 1;
         v3(v[k], (float)(a + dx) * hs - bo, (float)(bb + dy) * hs - bo, (float)h * vs);
       }
+      float zmax = v[0][2], xmin = v[0][0], xmax = v[0][0], ymin = v[0][1], ymax = v[0][1];
+      for (int k = 1; k < 4; ++k) {
+        zmax = fmaxf(zmax, v[k][2]);
+        xmin = fminf(xmin, v[k][0]); xmax = fmaxf(xmax, v[k][0]);
+        ymin = fminf(ymin, v[k][1]); ymax = fmaxf(ymax, v[k][1]);
+      }
+      if (p[2] - r > zmax || p[0] < xmin - r || p[0] > xmax + r || p[1] < ymin - r || p[1] > ymax + r) continue;
       tm_tri(&q, p, v[0], v[3], v[2]);
       tm_tri(&q, p, v[0], v[1], v[3]);
     }

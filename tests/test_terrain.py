@@ -133,8 +133,10 @@ def test_contact_on_the_corrected_stair():
     # the riser between rows 2 and 3 is the vertical face x = 0.3 from z = 0 to z = 0.15
     d, n = _contact(env, (0.29, 0.5, 0.05), r)            # beside the face, lower side, 1 cm away
     assert d == pytest.approx(r - 0.01, abs=1e-5) and n == pytest.approx([-1, 0, 0], abs=1e-5)
-    d, n = _contact(env, (0.25, 0.5, 0.05), r)            # 5 cm away: no contact
-    assert d == pytest.approx(r - 0.05, abs=1e-5) and d < 0
+    d, n = _contact(env, (0.25, 0.5, 0.05), r)            # 5 cm away: no contact (depth < 0; the
+    assert d < 0                                          # cells farther than r are culled)
+    d, n = _contact(env, (0.285, 0.5, 0.05), r)           # 1.5 cm away, still within r: contact
+    assert d == pytest.approx(r - 0.015, abs=1e-5) and n == pytest.approx([-1, 0, 0], abs=1e-5)
     d, n = _contact(env, (0.45, 0.5, 0.16), r)            # above the upper tread, 1 cm up
     assert d == pytest.approx(r - 0.01, abs=1e-5) and n == pytest.approx([0, 0, 1], abs=1e-5)
     d, n = _contact(env, (0.45, 0.5, 0.145), r)           # 5 mm into the tread
