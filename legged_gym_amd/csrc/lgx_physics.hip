@@ -334,6 +334,22 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
                             f3* n, const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
   const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
   const int rows = B.hf_rows, cols = B.hf_cols;
+  // early out: p more than r above every vertex of the 4 x 4 block (no face can be within r, and p
+  // is not below the surface) - the candidates off the ground leave after 16 LDS reads
+  const bool in_patch = hpatch && (unsigned)(i - 1 - pi0) < LGX_HF_PATCH - 3 && (unsigned)(j - 1 - pj0) < LGX_HF_PATCH - 3;
+  {
+    int hmax = -32768;
+#pragma unroll
+    for (int da = 0; da < 4; ++da)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int a = min(max(i - 1 + da, 0), rows - 1), b = min(max(j - 1 + db, 0), cols - 1);
+        const int h = in_patch ? hpatch[(i - 1 + da - pi0) * LGX_HF_PATCH + (j - 1 + db - pj0)]
+                               : B.height_samples[(int64_t)a * cols + b];
+        hmax = max(hmax, h);
+      }
+    if (p.z - r > (float)hmax * vs) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
+  }
   TmQuery q;
   q.d2 = 3.0e38f; q.cp = p; q.cn = mk3(0.f, 0.f, 1.f);
   q.top = -3.0e38f; q.tn = mk3(0.f, 0.f, 1.f);
@@ -343,11 +359,11 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int a = ci + (k & 1), b = cj + (k >> 1);
-        const int li = a - pi0, lj = b - pj0;
         int h, code;
-        if (hpatch && (unsigned)li < LGX_HF_PATCH && (unsigned)lj < LGX_HF_PATCH) {
-          h = hpatch[li * LGX_HF_PATCH + lj];
-          code = tpatch[li * LGX_HF_PATCH + lj] & 15;
+        if (in_patch) {   // (the whole 4 x 4 block is in the LDS patch)
+          const int o = (a - pi0) * LGX_HF_PATCH + (b - pj0);
+          h = hpatch[o];
+          code = tpatch[o] & 15;
         } else {
           h = B.height_samples[(int64_t)a * cols + b];
           code = B.hf_trimesh[(int64_t)a * cols + b] & 15;

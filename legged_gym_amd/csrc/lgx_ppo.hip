@@ -9,7 +9,9 @@
 //   - ELU backward fused with the bias-gradient column sums,
 //   - split-K / per-chunk partial reductions straight into the flat gradient buffer,
 //   - global-norm gradient clipping (clip_grad_norm_) fused into the Adam step.
-// The GEMMs between them stay on hipBLASLt through torch (mm / bmm).  All reductions are
+// The GEMMs between them are the hand-written split-bf16 kernels (lgx_gemm_x3p.hip forwards and
+// dA, lgx_gemm_tn.hip dW; lgx_gemm_split.hip / lgx_gemm.hip variants), with library GEMMs through
+// torch only for shapes they do not take or LGX_PPO_GEMM=lib (rl/fused_ppo.py).  All reductions are
 // two-stage in a fixed order (bitwise reproducible); the adaptive learning rate and the Adam
 // step counter live on the device so a whole update can be captured in one hipGraph.
 #include <hip/hip_runtime.h>

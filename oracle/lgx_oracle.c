@@ -241,6 +241,16 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
   const lgx_buffers* b = cx->b;
   const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
   const int rows = b->hf_rows, cols = b->hf_cols;
+  { /* early out: more than r above every vertex of the 4 x 4 block */
+    int hmax = -32768;
+    for (int a = i - 1; a <= i + 2; ++a)
+      for (int bb = j - 1; bb <= j + 2; ++bb) {
+        int aa = a < 0 ? 0 : (a > rows - 1 ? rows - 1 : a), bc = bb < 0 ? 0 : (bb > cols - 1 ? cols - 1 : bb);
+        int h = b->height_samples[(int64_t)aa * cols + bc];
+        if (h > hmax) hmax = h;
+      }
+    if (p[2] - r > (float)hmax * vs) { v3(n, 0, 0, 1); return -1.0f; }
+  }
   tmq_t q;
   q.d2 = 3.0e38f; memcpy(q.cp, p, 12); v3(q.cn, 0, 0, 1);
   q.top = -3.0e38f; v3(q.tn, 0, 0, 1);

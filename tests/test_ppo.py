@@ -296,3 +296,18 @@ def test_resume_learning_rate_follows_upstream(tmp_path, schedule):
         ratios = [np.log(lr / lr_cfg) / np.log(1.5) for lr in seen if 1e-5 < lr < 1e-2]
         assert seen and ratios and all(abs(r - round(r)) < 1e-6 for r in ratios), seen
         assert 3.3e-4 not in seen
+
+
+def test_play_logger(tmp_path):
+    """utils/logger.py (legged_gym/utils/logger.py:36-136): reward bookkeeping weighted by episode
+    counts, and the 3 x 3 state figure rendered headless."""
+    from legged_gym_amd.utils.logger import Logger
+    lg = Logger(0.02)
+    for t in range(50):
+        lg.log_states({"dof_pos": np.sin(t * 0.1), "dof_pos_target": 0.0, "dof_vel": 0.1 * t, "dof_torque": 1.0 - t,
+                       "base_vel_x": 0.5, "command_x": 0.5, "contact_forces_z": np.array([1.0, 2.0, 3.0, 4.0])})
+    lg.log_rewards({"rew_tracking": torch.tensor(2.0), "terrain_level": torch.tensor(3.0)}, 3)
+    lg.log_rewards({"rew_tracking": torch.tensor(1.0)}, 1)
+    assert lg.num_episodes == 4 and lg.average_rewards() == {"rew_tracking": (2.0 * 3 + 1.0) / 4}
+    path = lg.plot_states(str(tmp_path / "s.png"))
+    assert os.path.getsize(path) > 10000
