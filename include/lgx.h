@@ -287,6 +287,12 @@ int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
  * the golden replay).  Same device code as the physics launch's load stage. */
 int lgx_drive_inputs(lgx_sim* sim, const float* actions, void* stream);
 
+/* The physics launch's ground query for a batch of world points (tests, tools): points [n, 4] =
+ * (x, y, z, radius), out [n, 4] = (contact depth, normal xyz) against the bound terrain - the
+ * slope-corrected trimesh where lgx_buffers.hf_trimesh flags the cell, else the heightfield
+ * triangle under the point; depth <= 0: no contact (its magnitude is then unspecified). */
+int lgx_ground_contact(lgx_sim* sim, const float* points, int32_t n, float* out, void* stream);
+
 /* post_physics_step only (legged_robot.py:109-141) on the current state buffers. */
 int lgx_post_physics(lgx_sim* sim, int64_t common_step_counter, void* stream);
 

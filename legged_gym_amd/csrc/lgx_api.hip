@@ -258,6 +258,12 @@ int lgx_drive_inputs(lgx_sim* s, const float* actions, void* stream) {
                       "lgx_drive_inputs: launch");
 }
 
+int lgx_ground_contact(lgx_sim* s, const float* points, int32_t n, float* out, void* stream) {
+  if (!s || n < 0 || (n > 0 && (!points || !out))) return fail(LGX_EINVAL, "lgx_ground_contact: bad arguments");
+  return launch_check(lgx_launch_ground_contact(s->d_params, s->bufs, points, n, out, (hipStream_t)stream),
+                      "lgx_ground_contact: launch");
+}
+
 int lgx_post_physics(lgx_sim* s, int64_t step, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_post_physics: null sim");
   return launch_check(lgx_launch_post_physics(s->d_params, s->bufs, s->params.num_envs, s->params.num_obs, s->n_term_rows,

@@ -16,6 +16,8 @@ struct lgx_dev_model {
   int32_t lane_pts[4][LGX_MAX_LANE_PTS];
 };
 
+int lgx_launch_ground_contact(const lgx_env_params* dp, const lgx_buffers& b, const float* q, int32_t n, float* o,
+                              hipStream_t stream);
 int lgx_physics_pp(int32_t n_envs);   // lanes per leg of the physics launch at n_envs
 // frozen != 0: only the drive inputs of `nsub` substeps (clip, targets, actuator-net history and
 // model_ins rows) with the state held fixed (lgx_drive_inputs)

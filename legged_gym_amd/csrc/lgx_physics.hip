@@ -959,6 +959,26 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   LGX_CLK_PRINT("physics", 8)
 }
 
+// ground_contact for a batch of world points (test entry lgx_ground_contact): q[k] = (x, y, z, r)
+// -> o[k] = (depth, nx, ny, nz); heights / table read from global memory (no LDS patch)
+__global__ void lgx_ground_contact_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, const float4* __restrict__ q,
+                                          int32_t n, float4* __restrict__ o) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const float4 v = q[k];
+  f3 nn;
+  const float d = ground_contact(P, B, mk3(v.x, v.y, v.z), v.w, &nn, nullptr, nullptr, 0, 0);
+  o[k] = make_float4(d, nn.x, nn.y, nn.z);
+}
+
+int lgx_launch_ground_contact(const lgx_env_params* dp, const lgx_buffers& b, const float* q, int32_t n, float* o,
+                              hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(lgx_ground_contact_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, dp, b,
+                     reinterpret_cast<const float4*>(q), n, reinterpret_cast<float4*>(o));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 // lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches;
 // LGX_PHYS_PP (1, 2, 4, 8) overrides it for A/B runs and for the parity tests of every split
 int lgx_physics_pp(int32_t n_envs) {

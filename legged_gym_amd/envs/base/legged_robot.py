@@ -545,6 +545,8 @@ class LeggedRobot(BaseTask):
         tcfg = self.cfg.terrain
         if tcfg.mesh_type != "trimesh" or getattr(tcfg, "slope_treshold", None) is None:
             return None
+        if os.environ.get("LGX_TRIMESH", "1") == "0":   # A/B switch: contact on the raw heightfield
+            return None
         R, Cc = self.height_samples.shape
         thr = tcfg.slope_treshold * (tcfg.horizontal_scale / tcfg.vertical_scale)   # (the library's scaling)
         if self.height_samples.is_cuda:

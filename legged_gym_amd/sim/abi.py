@@ -187,6 +187,7 @@ def declare(lib, prefix="lgx"):
             "trimesh_build": (C.c_int, [vp, i32, i32, C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]),
             "step_from": (C.c_int, [vp, vp, i64, vp]),
             "drive_inputs": (C.c_int, [vp, vp, vp]),
+            "ground_contact": (C.c_int, [vp, vp, i32, vp, vp]),
             "sync_aux": (C.c_int, [vp, vp]),
             "rebind_extras": (C.c_int, [vp, vp]),
             "ppo_gather_rows": (C.c_int, [vp, vp, vp, i64, i32, vp]),
@@ -230,7 +231,7 @@ def declare(lib, prefix="lgx"):
 
 
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trimesh_build", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
-            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_step_from", "lgx_drive_inputs", "lgx_sync_aux",
+            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_step_from", "lgx_drive_inputs", "lgx_ground_contact", "lgx_sync_aux",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
