@@ -300,26 +300,24 @@ LGX_DEV f3 closest_on_tri(f3 p, f3 a, f3 b, f3 c) {
   return a + (vb * den) * ab + (vc * den) * ac;
 }
 
-// one triangle of the query: nearest point so far (squared distance, point, face normal) and the
-// highest surface among the triangles whose xy projection holds p (height, face normal)
+// one triangle of the query: nearest point so far (squared distance, point, the face's cross
+// product) and the highest surface among the triangles whose xy projection holds p (height, cross
+// product); face normals are normalised only for the rare on-surface case at the end
 struct TmQuery { float d2; f3 cp, cn; float top; f3 tn; };
 LGX_DEV void tm_tri(TmQuery& q, f3 p, f3 a, f3 b, f3 c) {
-  const f3 e1 = b - a, e2 = c - a;
-  f3 nf = cross(e1, e2);
-  const float nl = sqrtf(dot(nf, nf));
-  if (!(nl > 1e-12f)) return;                       // degenerate in 3D
-  nf = (nf.z < 0.f ? -1.f : 1.f) / nl * nf;         // oriented up
   const f3 cp = closest_on_tri(p, a, b, c);
   const f3 dv = p - cp;
   const float d2 = dot(dv, dv);
-  if (d2 < q.d2) { q.d2 = d2; q.cp = cp; q.cn = nf; }
+  const f3 e1 = b - a, e2 = c - a;
+  if (d2 < q.d2) { q.d2 = d2; q.cp = cp; q.cn = cross(e1, e2); }
   const float den = e1.x * e2.y - e1.y * e2.x;      // 2 x signed xy area (0 for vertical faces)
   if (fabsf(den) > 1e-9f) {
+    const float id = 1.f / den;
     const float px = p.x - a.x, py = p.y - a.y;
-    const float s = (px * e2.y - py * e2.x) / den, t = (e1.x * py - e1.y * px) / den;
+    const float s = (px * e2.y - py * e2.x) * id, t = (e1.x * py - e1.y * px) * id;
     if (s >= -1e-6f && t >= -1e-6f && s + t <= 1.f + 1e-6f) {
       const float hz = a.z + s * e1.z + t * e2.z;
-      if (hz > q.top) { q.top = hz; q.tn = nf; }
+      if (hz > q.top) { q.top = hz; q.tn = cross(e1, e2); }
     }
   }
 }
@@ -386,7 +384,9 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
     const float inv = 1.f / d;
     *n = inside ? inv * (q.cp - p) : inv * (p - q.cp);
   } else {
-    *n = q.top > -1e30f ? q.tn : q.cn;
+    f3 c = q.top > -1e30f ? q.tn : q.cn;
+    c = (c.z < 0.f ? -1.f : 1.f) / fmaxf(sqrtf(dot(c, c)), 1e-30f) * c;   // face normal, oriented up
+    *n = c;
   }
   return inside ? r + d : r - d;
 }

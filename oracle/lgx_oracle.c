@@ -211,25 +211,20 @@ static void closest_on_tri(const float* p, const float* a, const float* b, const
 typedef struct { float d2, cp[3], cn[3], top, tn[3]; } tmq_t;
 
 static void tm_tri(tmq_t* q, const float* p, const float* a, const float* b, const float* c) {
-  float e1[3], e2[3], nf[3];
+  float e1[3], e2[3], cp[3], dv[3];
   sub3(b, a, e1); sub3(c, a, e2);
-  cross3(e1, e2, nf);
-  float nl = sqrtf(dot3(nf, nf));
-  if (!(nl > 1e-12f)) return;
-  float sgn = nf[2] < 0 ? -1.0f : 1.0f;
-  for (int k = 0; k < 3; ++k) nf[k] = sgn / nl * nf[k];
-  float cp[3], dv[3];
   closest_on_tri(p, a, b, c, cp);
   sub3(p, cp, dv);
   float d2 = dot3(dv, dv);
-  if (d2 < q->d2) { q->d2 = d2; memcpy(q->cp, cp, 12); memcpy(q->cn, nf, 12); }
+  if (d2 < q->d2) { q->d2 = d2; memcpy(q->cp, cp, 12); cross3(e1, e2, q->cn); }
   float den = e1[0] * e2[1] - e1[1] * e2[0];
   if (fabsf(den) > 1e-9f) {
+    float id = 1.0f / den;
     float px = p[0] - a[0], py = p[1] - a[1];
-    float s = (px * e2[1] - py * e2[0]) / den, t = (e1[0] * py - e1[1] * px) / den;
+    float s = (px * e2[1] - py * e2[0]) * id, t = (e1[0] * py - e1[1] * px) * id;
     if (s >= -1e-6f && t >= -1e-6f && s + t <= 1.0f + 1e-6f) {
       float hz = a[2] + s * e1[2] + t * e2[2];
-      if (hz > q->top) { q->top = hz; memcpy(q->tn, nf, 12); }
+      if (hz > q->top) { q->top = hz; cross3(e1, e2, q->tn); }
     }
   }
 }
@@ -280,7 +275,10 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
     float inv = 1.0f / d;
     for (int k = 0; k < 3; ++k) n[k] = inside ? inv * (q.cp[k] - p[k]) : inv * (p[k] - q.cp[k]);
   } else {
-    memcpy(n, q.top > -1e30f ? q.tn : q.cn, 12);
+    const float* c = q.top > -1e30f ? q.tn : q.cn;
+    float l = sqrtf(dot3(c, c));
+    float s = (c[2] < 0 ? -1.0f : 1.0f) / (l > 1e-30f ? l : 1e-30f);
+    for (int k = 0; k < 3; ++k) n[k] = s * c[k];
   }
   return inside ? r + d : r - d;
 }
