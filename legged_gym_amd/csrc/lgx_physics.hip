@@ -348,6 +348,11 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
       }
     if (p.z - r > (float)hmax * vs) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
   }
+  // the geometry in a frame at raw vertex (i, j) (coordinates of a few cells: float precision of the
+  // nearest point and normal independent of how far the env is from the world origin); no fma
+  // contraction in the frame change, so the oracle's restatement rounds identically
+  const float ox = __fsub_rn(__fmul_rn((float)i, hs), bo), oy = __fsub_rn(__fmul_rn((float)j, hs), bo);
+  p = mk3(__fsub_rn(p.x, ox), __fsub_rn(p.y, oy), p.z);
   TmQuery q;
   q.d2 = 3.0e38f; q.cp = p; q.cn = mk3(0.f, 0.f, 1.f);
   q.top = -3.0e38f; q.tn = mk3(0.f, 0.f, 1.f);
@@ -367,7 +372,7 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
           code = B.hf_trimesh[(int64_t)a * cols + b] & 15;
         }
         const int dx = ((code * 11) >> 5) - 1, dy = code - 3 * (dx + 1) - 1;
-        v[k] = mk3((float)(a + dx) * hs - bo, (float)(b + dy) * hs - bo, (float)h * vs);
+        v[k] = mk3((float)(a + dx - i) * hs, (float)(b + dy - j) * hs, (float)h * vs);
       }
       // cull: p more than r above every vertex of the cell (no contact, not below its surface) or
       // outside its xy box grown by r (farther than r, not over it): most queries keep one cell

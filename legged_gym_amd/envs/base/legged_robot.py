@@ -545,7 +545,8 @@ class LeggedRobot(BaseTask):
         tcfg = self.cfg.terrain
         if tcfg.mesh_type != "trimesh" or getattr(tcfg, "slope_treshold", None) is None:
             return None
-        if os.environ.get("LGX_TRIMESH", "1") == "0":   # A/B switch: contact on the raw heightfield
+        mode = os.environ.get("LGX_TRIMESH", "1")       # A/B switches: 0 = contact on the raw heightfield,
+        if mode == "0":                                  # 2 = table bound but no cell flagged
             return None
         R, Cc = self.height_samples.shape
         thr = tcfg.slope_treshold * (tcfg.horizontal_scale / tcfg.vertical_scale)   # (the library's scaling)
@@ -557,6 +558,8 @@ class LeggedRobot(BaseTask):
                                                tcfg.vertical_scale, thr, None, None, C.c_void_p(table.data_ptr()),
                                                C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
                          "lgx_trimesh_build")
+            if mode == "2":
+                table &= 15
             return table
         from legged_gym_amd.utils.terrain import trimesh_contact_tables, trimesh_vertex_moves
         dx, dy = trimesh_vertex_moves(self.height_samples.cpu().numpy(), tcfg.horizontal_scale, tcfg.vertical_scale,

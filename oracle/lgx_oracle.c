@@ -246,6 +246,10 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
       }
     if (p[2] - r > (float)hmax * vs) { v3(n, 0, 0, 1); return -1.0f; }
   }
+  /* frame at raw vertex (i, j): small coordinates (see the kernel) */
+  const float ox = (float)i * hs - bo, oy = (float)j * hs - bo;
+  float pl[3] = {p[0] - ox, p[1] - oy, p[2]};
+  p = pl;
   tmq_t q;
   q.d2 = 3.0e38f; memcpy(q.cp, p, 12); v3(q.cn, 0, 0, 1);
   q.top = -3.0e38f; v3(q.tn, 0, 0, 1);
@@ -257,7 +261,7 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
         int h = b->height_samples[(int64_t)a * cols + bb];
         int code = b->hf_trimesh[(int64_t)a * cols + bb] & 15;
         int dx = code / 3 - 1, dy = code % 3 - 1;
-        v3(v[k], (float)(a + dx) * hs - bo, (float)(bb + dy) * hs - bo, (float)h * vs);
+        v3(v[k], (float)(a + dx - i) * hs, (float)(bb + dy - j) * hs, (float)h * vs);
       }
       float zmax = v[0][2], xmin = v[0][0], xmax = v[0][0], ymin = v[0][1], ymax = v[0][1];
       for (int k = 1; k < 4; ++k) {
