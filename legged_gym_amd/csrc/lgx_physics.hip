@@ -396,12 +396,15 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
   return inside ? r + d : r - d;
 }
 
-// Ground contact of a sphere / point (radius r) centred at world p: the corrected trimesh where its
-// contact table flags the cell (near a moved vertex), else the triangulated heightfield under p
-// (identical there: no vertex of the neighbourhood moved) with depth along its face normal.
+// Ground contact of a sphere / point (radius r) centred at world p: spheres (r > 0: feet, capsule
+// ends) against the corrected trimesh where its contact table flags the cell (near a moved vertex);
+// everything else against the triangulated heightfield under p (identical where no vertex of the
+// neighbourhood moved), depth along its face normal.  Box corners (r = 0) keep the heightfield query
+// everywhere: on a fallen robot dozens of them sit near the ground, and the full query per point
+// (up to 18 triangles, latency-bound at one wave per SIMD) cost 2x the whole physics launch.
 LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, f3* n,
                              const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
-  if (B.hf_trimesh && P->terrain_kind != 0 && B.height_samples) {
+  if (r > 0.f && B.hf_trimesh && P->terrain_kind != 0 && B.height_samples) {
     const float hs = P->horizontal_scale;
     int i = (int)floorf((p.x + P->border_size) / hs), j = (int)floorf((p.y + P->border_size) / hs);
     i = min(max(i, 0), B.hf_rows - 2);

@@ -287,12 +287,13 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
   return inside ? r + d : r - d;
 }
 
-/* ground contact depth of a sphere / point: the corrected trimesh where the contact table flags
- * the cell, else the heightfield triangle under p with depth along its face normal */
+/* ground contact depth of a sphere / point: spheres (r > 0) against the corrected trimesh where the
+ * contact table flags the cell; box corners (r = 0) and unflagged cells against the heightfield
+ * triangle under p, depth along its face normal (the kernel's split) */
 static float ground_contact(const ctx_t* cx, const float* p, float r, float* n) {
   const lgx_env_params* P = cx->p;
   const lgx_buffers* b = cx->b;
-  if (b->hf_trimesh && P->terrain_kind != 0 && b->height_samples) {
+  if (r > 0.0f && b->hf_trimesh && P->terrain_kind != 0 && b->height_samples) {
     int i = (int)floorf((p[0] + P->border_size) / P->horizontal_scale);
     int j = (int)floorf((p[1] + P->border_size) / P->horizontal_scale);
     if (i < 0) i = 0; if (i > b->hf_rows - 2) i = b->hf_rows - 2;

@@ -143,6 +143,10 @@ def test_contact_on_the_corrected_stair():
     assert d == pytest.approx(r + 0.005, abs=1e-5) and n == pytest.approx([0, 0, 1], abs=1e-5)
     d, n = _contact(env, (0.302, 0.5, 0.10), r)           # inside the step, 2 mm behind the face
     assert d == pytest.approx(r + 0.002, abs=1e-5) and n == pytest.approx([-1, 0, 0], abs=1e-5)
+    # box corners (radius 0) query the heightfield triangle under them, even beside the riser:
+    # 0.1 cm from the face, on the raw ramp of cell row 2 (0 -> 0.15 m over x 0.2 .. 0.3)
+    d, n = _contact(env, (0.299, 0.5, 0.05), 0.0)
+    assert d == pytest.approx((0.15 * 0.99 - 0.05) / np.sqrt(1 + 1.5 ** 2), abs=1e-5)
     # far from any moved vertex: the heightfield query (identical surface), e.g. the flat ground
     # beyond the stair
     d, n = _contact(env, (2.0, 2.5, 0.01), r)
