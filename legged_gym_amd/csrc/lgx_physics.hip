@@ -332,22 +332,29 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
                             f3* n, const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
   const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
   const int rows = B.hf_rows, cols = B.hf_cols;
-  // early out: p more than r above every vertex of the 4 x 4 block (no face can be within r, and p
-  // is not below the surface) - the candidates off the ground leave after 16 LDS reads
+  // the 4 x 4 vertex block (rows i-1 .. i+2, cols j-1 .. j+2; clamped at the map edge) read once,
+  // every load issued before the first use
   const bool in_patch = hpatch && (unsigned)(i - 1 - pi0) < LGX_HF_PATCH - 3 && (unsigned)(j - 1 - pj0) < LGX_HF_PATCH - 3;
-  {
-    int hmax = -32768;
+  int hv[16], cd[16];
 #pragma unroll
-    for (int da = 0; da < 4; ++da)
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const int a = min(max(i - 1 + da, 0), rows - 1), b = min(max(j - 1 + db, 0), cols - 1);
-        const int h = in_patch ? hpatch[(i - 1 + da - pi0) * LGX_HF_PATCH + (j - 1 + db - pj0)]
-                               : B.height_samples[(int64_t)a * cols + b];
-        hmax = max(hmax, h);
-      }
-    if (p.z - r > (float)hmax * vs) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
+  for (int k = 0; k < 16; ++k) {
+    const int da = k >> 2, db = k & 3;
+    if (in_patch) {
+      const int o = (i - 1 + da - pi0) * LGX_HF_PATCH + (j - 1 + db - pj0);
+      hv[k] = hpatch[o];
+      cd[k] = tpatch[o] & 15;
+    } else {
+      const int a = min(max(i - 1 + da, 0), rows - 1), b = min(max(j - 1 + db, 0), cols - 1);
+      hv[k] = B.height_samples[(int64_t)a * cols + b];
+      cd[k] = B.hf_trimesh[(int64_t)a * cols + b] & 15;
+    }
   }
+  // early out: p more than r above every vertex of the block (no face within r, not below the
+  // surface) - the spheres off the ground leave here
+  int hmax = hv[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) hmax = max(hmax, hv[k]);
+  if (p.z - r > (float)hmax * vs) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
   // the geometry in a frame at raw vertex (i, j) (coordinates of a few cells: float precision of the
   // nearest point and normal independent of how far the env is from the world origin); no fma
   // contraction in the frame change, so the oracle's restatement rounds identically
@@ -356,23 +363,19 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
   TmQuery q;
   q.d2 = 3.0e38f; q.cp = p; q.cn = mk3(0.f, 0.f, 1.f);
   q.top = -3.0e38f; q.tn = mk3(0.f, 0.f, 1.f);
-  for (int ci = max(i - 1, 0); ci <= min(i + 1, rows - 2); ++ci)
-    for (int cj = max(j - 1, 0); cj <= min(j + 1, cols - 2); ++cj) {
+#pragma unroll
+  for (int ca = 0; ca < 3; ++ca)
+#pragma unroll
+    for (int cb = 0; cb < 3; ++cb) {
+      const int ci = i - 1 + ca, cj = j - 1 + cb;
+      if (ci < 0 || ci > rows - 2 || cj < 0 || cj > cols - 2) continue;
       f3 v[4];   // (ci, cj), (ci + 1, cj), (ci, cj + 1), (ci + 1, cj + 1)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int a = ci + (k & 1), b = cj + (k >> 1);
-        int h, code;
-        if (in_patch) {   // (the whole 4 x 4 block is in the LDS patch)
-          const int o = (a - pi0) * LGX_HF_PATCH + (b - pj0);
-          h = hpatch[o];
-          code = tpatch[o] & 15;
-        } else {
-          h = B.height_samples[(int64_t)a * cols + b];
-          code = B.hf_trimesh[(int64_t)a * cols + b] & 15;
-        }
+        const int da = ca + (k & 1), db = cb + (k >> 1);
+        const int code = cd[da * 4 + db];
         const int dx = ((code * 11) >> 5) - 1, dy = code - 3 * (dx + 1) - 1;
-        v[k] = mk3((float)(a + dx - i) * hs, (float)(b + dy - j) * hs, (float)h * vs);
+        v[k] = mk3((float)(da - 1 + dx) * hs, (float)(db - 1 + dy) * hs, (float)hv[da * 4 + db] * vs);
       }
       // cull: p more than r above every vertex of the cell (no contact, not below its surface) or
       // outside its xy box grown by r (farther than r, not over it): most queries keep one cell
