@@ -11,14 +11,35 @@
 // EXTRA=-DLGX_PHASE_CLOCK (tools/phase_clock.sh); compiled out of the product library.
 #ifdef LGX_PHASE_CLOCK
 #include <stdio.h>
-#define LGX_CLK_DECL(n) uint64_t lgx_clk_acc[n] = {}; uint64_t lgx_clk_t = clock64();
+#define LGX_CLK_DECL(n) LGX_CLK_START uint64_t lgx_clk_acc[n] = {}; uint64_t lgx_clk_t = clock64();
 #define LGX_CLK(i) do { const uint64_t _t = clock64(); lgx_clk_acc[i] += _t - lgx_clk_t; lgx_clk_t = _t; } while (0)
+#ifdef LGX_PHASE_CLOCK_ALL   // every workgroup's thread 0 (load-balance studies)
+#define LGX_CLK_WHO (threadIdx.x == 0)
+#else
+#define LGX_CLK_WHO (blockIdx.x == 0 && threadIdx.x == 0)
+#endif
+#ifdef LGX_PHASE_CLOCK_BUF   // per-workgroup record of the last launch in a device table (no printf):
+                             // [start, end] (s_memrealtime, 100 MHz) + the phase sums; read by
+                             // lgx_debug_clock (lgx_physics.hip)
+#define LGX_CLK_MAXB 4096
+static __device__ unsigned long long lgx_clk_buf[LGX_CLK_MAXB][10];
+#define LGX_CLK_START const unsigned long long lgx_clk_t0 = __builtin_amdgcn_s_memrealtime();
 #define LGX_CLK_PRINT(name, n)                                                                        \
-  if (blockIdx.x == 0 && threadIdx.x == 0) {                                                          \
-    printf("%s cycles:", name);                                                                       \
-    for (int _i = 0; _i < n; ++_i) printf(" %d=%llu", _i, (unsigned long long)lgx_clk_acc[_i]);        \
-    printf("\n");                                                                                     \
+  if (threadIdx.x == 0 && blockIdx.x < LGX_CLK_MAXB) {                                                \
+    lgx_clk_buf[blockIdx.x][0] = lgx_clk_t0;                                                          \
+    lgx_clk_buf[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                                    \
+    for (int _i = 0; _i < n && _i < 8; ++_i) lgx_clk_buf[blockIdx.x][2 + _i] = lgx_clk_acc[_i];       \
   }
+#else
+#define LGX_CLK_START
+#define LGX_CLK_PRINT(name, n)                                                                        \
+  if (LGX_CLK_WHO) {   /* one printf per line (lines of concurrent workgroups do not interleave) */   \
+    unsigned long long _v[8] = {};                                                                    \
+    for (int _i = 0; _i < n && _i < 8; ++_i) _v[_i] = lgx_clk_acc[_i];                                \
+    printf("%s cycles: b=%d 0=%llu 1=%llu 2=%llu 3=%llu 4=%llu 5=%llu 6=%llu 7=%llu\n", name,         \
+           (int)blockIdx.x, _v[0], _v[1], _v[2], _v[3], _v[4], _v[5], _v[6], _v[7]);                  \
+  }
+#endif
 #else
 #define LGX_CLK_DECL(n)
 #define LGX_CLK(i) do { } while (0)

@@ -5,7 +5,7 @@
 
 #include "../../include/lgx.h"
 
-#define LGX_MAX_LANE_PTS 32
+#define LGX_MAX_LANE_PTS 24   // contact candidates per leg lane (Go1: 23)
 
 // device-resident model: the ABI model + the per-lane (per-leg) contact candidate tables
 struct lgx_dev_model {

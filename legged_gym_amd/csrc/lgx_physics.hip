@@ -329,7 +329,7 @@ LGX_DEV void tm_tri(TmQuery& q, f3 p, f3 a, f3 b, f3 c) {
 // the surface point toward p (outside) or from p toward it (inside).  Where p sits on the surface,
 // the face normal.
 LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
-                            f3* n, const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
+                            f3* n, const int32_t* hpatch, int pi0, int pj0) {
   const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
   const int rows = B.hf_rows, cols = B.hf_cols;
   // the 4 x 4 vertex block (rows i-1 .. i+2, cols j-1 .. j+2; clamped at the map edge) read once,
@@ -340,9 +340,9 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
   for (int k = 0; k < 16; ++k) {
     const int da = k >> 2, db = k & 3;
     if (in_patch) {
-      const int o = (i - 1 + da - pi0) * LGX_HF_PATCH + (j - 1 + db - pj0);
-      hv[k] = hpatch[o];
-      cd[k] = tpatch[o] & 15;
+      const int v = hpatch[(i - 1 + da - pi0) * LGX_HF_PATCH + (j - 1 + db - pj0)];
+      hv[k] = v >> 8;
+      cd[k] = v & 15;
     } else {
       const int a = min(max(i - 1 + da, 0), rows - 1), b = min(max(j - 1 + db, 0), cols - 1);
       hv[k] = B.height_samples[(int64_t)a * cols + b];
@@ -406,24 +406,39 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
 // everywhere: on a fallen robot dozens of them sit near the ground, and the full query per point
 // (up to 18 triangles, latency-bound at one wave per SIMD) cost 2x the whole physics launch.
 LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, f3* n,
-                             const int16_t* hpatch, const int8_t* tpatch, int pi0, int pj0) {
-  if (r > 0.f && B.hf_trimesh && P->terrain_kind != 0 && B.height_samples) {
-    const float hs = P->horizontal_scale;
-    int i = (int)floorf((p.x + P->border_size) / hs), j = (int)floorf((p.y + P->border_size) / hs);
-    i = min(max(i, 0), B.hf_rows - 2);
-    j = min(max(j, 0), B.hf_cols - 2);
-    const int li = i - pi0, lj = j - pj0;
-    const int tm = (tpatch && (unsigned)li < LGX_HF_PATCH && (unsigned)lj < LGX_HF_PATCH)
-                       ? tpatch[li * LGX_HF_PATCH + lj] : B.hf_trimesh[(int64_t)i * B.hf_cols + j];
-    if (tm & 16) return trimesh_depth(P, B, p, r, i, j, n, hpatch, tpatch, pi0, pj0);
+                             const int32_t* patch, int pi0, int pj0) {
+  if (P->terrain_kind == 0 || B.height_samples == nullptr) { *n = mk3(0.f, 0.f, 1.f); return r - p.z; }
+  const float hs = P->horizontal_scale, vs = P->vertical_scale;
+  const float u = (p.x + P->border_size) / hs, v = (p.y + P->border_size) / hs;
+  const int i = min(max((int)floorf(u), 0), B.hf_rows - 2), j = min(max((int)floorf(v), 0), B.hf_cols - 2);
+  // the cell's 4 samples (height << 8 | contact-table byte in the LDS patch) in one round trip
+  int q00, q10, q01, q11;
+  const int li = i - pi0, lj = j - pj0;
+  if (patch && (unsigned)li < LGX_HF_PATCH - 1 && (unsigned)lj < LGX_HF_PATCH - 1) {
+    const int32_t* q = patch + li * LGX_HF_PATCH + lj;
+    q00 = q[0]; q10 = q[LGX_HF_PATCH]; q01 = q[1]; q11 = q[LGX_HF_PATCH + 1];
+  } else {
+    const int16_t* H = B.height_samples;
+    const int64_t o = (int64_t)i * B.hf_cols + j;
+    const int tb = B.hf_trimesh ? B.hf_trimesh[o] & 0xff : 4;
+    q00 = (H[o] << 8) | tb; q10 = H[o + B.hf_cols] << 8; q01 = H[o + 1] << 8; q11 = H[o + B.hf_cols + 1] << 8;
   }
-  const float h = ground_height(P, B.height_samples, B.hf_rows, B.hf_cols, p.x, p.y, n, hpatch, pi0, pj0);
+  if (r > 0.f && B.hf_trimesh && (q00 & 16)) return trimesh_depth(P, B, p, r, i, j, n, patch, pi0, pj0);
+  // triangulated heightfield (diagonal (i, j)-(i+1, j+1)), depth along the face normal
+  const float h00 = (float)(q00 >> 8) * vs, h10 = (float)(q10 >> 8) * vs, h01 = (float)(q01 >> 8) * vs,
+              h11 = (float)(q11 >> 8) * vs;
+  const float fu = clampf(u - (float)i, 0.f, 1.f), fv = clampf(v - (float)j, 0.f, 1.f);
+  float gx, gy, h;
+  if (fu >= fv) { gx = (h10 - h00) / hs; gy = (h11 - h10) / hs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
+  else          { gx = (h11 - h01) / hs; gy = (h01 - h00) / hs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
+  const float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
+  *n = mk3(-gx * inv, -gy * inv, inv);
   return (h - p.z) * n->z + r;
 }
 
 }  // namespace
 
-#define MAX_LANE_PTS 32
+#define MAX_LANE_PTS LGX_MAX_LANE_PTS
 #ifndef LGX_PHYS_WAVES_PER_SIMD
 #define LGX_PHYS_WAVES_PER_SIMD 1
 #endif
@@ -465,8 +480,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   __shared__ float leg_kin[ENVS * 4][3][12];        // body frames of the leg: R (9), origin (3)
   __shared__ float leg_sys[ENVS * 4][36];           // contact-free leg system: B 18, D 6, rb 6, rl 3
   __shared__ float env_com[ENVS][40];               // base block 21, its rhs 6, base rotation 9
-  __shared__ int16_t hf_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];  // terrain around each base
-  __shared__ int8_t tm_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];   // its trimesh contact table
+  // terrain around each base: height << 8 | trimesh contact-table byte (4 = unmoved, unflagged)
+  __shared__ int32_t hf_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];
   __shared__ int32_t hf_org[ENVS][2];
   {
     const int4* src = reinterpret_cast<const int4*>(DMg);
@@ -544,17 +559,32 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       hf_org[eb][1] = min(max(cj - LGX_HF_PATCH / 2, 0), B.hf_cols - LGX_HF_PATCH);
     }
     __syncthreads();
-    for (int q = tid; q < ENVS * LGX_HF_PATCH * LGX_HF_PATCH; q += PHYS_BLOCK) {
-      const int ee = q / (LGX_HF_PATCH * LGX_HF_PATCH), r = q % (LGX_HF_PATCH * LGX_HF_PATCH);
-      const int li = r / LGX_HF_PATCH, lj = r % LGX_HF_PATCH;
-      const int64_t gi = (int64_t)(hf_org[ee][0] + li) * B.hf_cols + hf_org[ee][1] + lj;
-      hf_patch[ee][r] = B.height_samples[gi];
-      if (B.hf_trimesh) tm_patch[ee][r] = B.hf_trimesh[gi];
+    // every thread copies PER samples, in batches of up to 12 whose global loads are all issued
+    // before the first LDS store (the copy is latency-bound otherwise: one HBM round trip per sample)
+    constexpr int AREA = LGX_HF_PATCH * LGX_HF_PATCH, PER = ENVS * AREA / PHYS_BLOCK;
+    constexpr int BATCH = PER % 12 == 0 ? 12 : (PER % 9 == 0 ? 9 : 6);
+    static_assert(ENVS * AREA % PHYS_BLOCK == 0 && PER % BATCH == 0, "patch copy layout");
+    const int8_t* T = B.hf_trimesh;
+    for (int q0 = 0; q0 < PER; q0 += BATCH) {
+      int16_t hv[BATCH];
+      int8_t tv[BATCH];
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const int q = tid + (q0 + b) * PHYS_BLOCK;
+        const int ee = q / AREA, r = q % AREA;
+        const int64_t gi = (int64_t)(hf_org[ee][0] + r / LGX_HF_PATCH) * B.hf_cols + hf_org[ee][1] + r % LGX_HF_PATCH;
+        hv[b] = B.height_samples[gi];
+        tv[b] = T ? T[gi] : (int8_t)4;
+      }
+#pragma unroll
+      for (int b = 0; b < BATCH; ++b) {
+        const int q = tid + (q0 + b) * PHYS_BLOCK;
+        hf_patch[q / AREA][q % AREA] = ((int32_t)hv[b] << 8) | (tv[b] & 0xff);
+      }
     }
     __syncthreads();
   }
-  const int16_t* patch = use_patch ? hf_patch[eb] : nullptr;
-  const int8_t* tpatch = use_patch ? tm_patch[eb] : nullptr;
+  const int32_t* patch = use_patch ? hf_patch[eb] : nullptr;
   const int pi0 = use_patch ? hf_org[eb][0] : 0, pj0 = use_patch ? hf_org[eb][1] : 0;
   const int npts = DM->lane_npts[leg];
   const int maxpts = DM->max_lane_npts;
@@ -799,7 +829,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
           f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
           f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
           const float rad = M->point_radius[pi];
-          depth = ground_contact(P, B, Pp + pos, rad, &n, patch, tpatch, pi0, pj0);
+          depth = ground_contact(P, B, Pp + pos, rad, &n, patch, pi0, pj0);
           st.x = depth > 0.f ? 1.f : 0.f;
           slot_state[sl][tid] = st;
           if (depth <= 0.f) continue;
@@ -832,7 +862,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       }
 #pragma unroll
       for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + lsys[30 + k];
-      LGX_CLK(3);
+      if (pass == 0) LGX_CLK(3); else LGX_CLK(7);
       arrow_solve(L, ecom, ecom + 21, lane0, xb, xl);
       LGX_CLK(4);
       // contact status (after pass 0) / reported forces (after pass 1, last substep)
@@ -978,7 +1008,7 @@ __global__ void lgx_ground_contact_kernel(const lgx_env_params* __restrict__ P, 
   if (k >= n) return;
   const float4 v = q[k];
   f3 nn;
-  const float d = ground_contact(P, B, mk3(v.x, v.y, v.z), v.w, &nn, nullptr, nullptr, 0, 0);
+  const float d = ground_contact(P, B, mk3(v.x, v.y, v.z), v.w, &nn, nullptr, 0, 0);
   o[k] = make_float4(d, nn.x, nn.y, nn.z);
 }
 
@@ -1015,3 +1045,11 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+
+#ifdef LGX_PHASE_CLOCK_BUF
+// instrumented builds only (tools/phase_clock.sh): the per-workgroup clock table of the last physics launch
+extern "C" int lgx_debug_clock(unsigned long long* out, int32_t nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(lgx_clk_buf), (size_t)min(nblocks, LGX_CLK_MAXB) * 10 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -247,7 +247,7 @@ def tn_bench(M=24576, iters=20):
                   f"{f/t2/1e9:.1f} TF/s", flush=True)
 
 
-def phys_run(task="go1_rough", n=4096, steps=10):
+def phys_run(task="go1_rough", n=4096, steps=int(os.environ.get("KB_STEPS", "10"))):
     """Short env-step loop for PMC collection (rocprofv3 --pmc): 10 env steps after reset."""
     from oracle_backend import make_env
     env = make_env(task, num_envs=n, device="cuda:0", backend="lgx")
@@ -256,6 +256,16 @@ def phys_run(task="go1_rough", n=4096, steps=10):
     for _ in range(steps):
         env.step(torch.randn(n, 12, device="cuda:0", generator=g) * 0.5)
     torch.cuda.synchronize()
+    from legged_gym_amd.sim import lib as lgxlib
+    L = lgxlib.load()
+    if hasattr(L, "lgx_debug_clock"):   # LGX_PHASE_CLOCK_BUF build: per-workgroup clocks of the last launch
+        import ctypes as C
+        import numpy as np
+        nb = (n + 15) // 16
+        buf = np.zeros((nb, 10), dtype=np.uint64)
+        L.lgx_debug_clock(buf.ctypes.data_as(C.c_void_p), C.c_int32(nb))
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.save(os.environ.get("KB_CLK_OUT", "gpurun_out/clk.npy"), buf)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/clock
 for f in legged_gym_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DLGX_PHASE_CLOCK -c $f -o build/clock/$(basename $f .hip).o &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DLGX_PHASE_CLOCK ${CLK_EXTRA:-} -c $f -o build/clock/$(basename $f .hip).o &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/clock/liblgx.so build/clock/*.o
