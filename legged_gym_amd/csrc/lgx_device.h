@@ -22,13 +22,13 @@
                              // [start, end] (s_memrealtime, 100 MHz) + the phase sums; read by
                              // lgx_debug_clock (lgx_physics.hip)
 #define LGX_CLK_MAXB 4096
-static __device__ unsigned long long lgx_clk_buf[LGX_CLK_MAXB][10];
+static __device__ unsigned long long lgx_clk_buf[LGX_CLK_MAXB][14];
 #define LGX_CLK_START const unsigned long long lgx_clk_t0 = __builtin_amdgcn_s_memrealtime();
 #define LGX_CLK_PRINT(name, n)                                                                        \
   if (threadIdx.x == 0 && blockIdx.x < LGX_CLK_MAXB) {                                                \
     lgx_clk_buf[blockIdx.x][0] = lgx_clk_t0;                                                          \
     lgx_clk_buf[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();                                    \
-    for (int _i = 0; _i < n && _i < 8; ++_i) lgx_clk_buf[blockIdx.x][2 + _i] = lgx_clk_acc[_i];       \
+    for (int _i = 0; _i < n && _i < 12; ++_i) lgx_clk_buf[blockIdx.x][2 + _i] = lgx_clk_acc[_i];      \
   }
 #else
 #define LGX_CLK_START

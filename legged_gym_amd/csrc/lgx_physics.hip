@@ -322,70 +322,112 @@ LGX_DEV void tm_tri(TmQuery& q, f3 p, f3 a, f3 b, f3 c) {
   }
 }
 
-// Signed contact depth of a sphere (radius r >= 0, centre p, world frame) against the corrected
-// mesh around cell (i, j): the nearest surface point over the two triangles of each cell of the
-// 3 x 3 cells around (i, j) (the moves are at most one cell, so every face within r < one cell of
-// p is among them), inside = p below the surface under it; depth = r -/+ distance, normal = from
-// the surface point toward p (outside) or from p toward it (inside).  Where p sits on the surface,
-// the face normal.
-LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
-                            f3* n, const int32_t* hpatch, int pi0, int pj0) {
-  const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
+// the 4 x 4 vertex block around cell (i, j) (rows i-1 .. i+2, cols j-1 .. j+2; clamped at the map
+// edge): heights and move codes.  One branch around each source's 16 loads (a per-load condition
+// compiles to a branch and a full wait after every load: 16 serial round trips)
+LGX_DEV void tm_block(const lgx_buffers& B, int i, int j, const int32_t* hpatch, int pi0, int pj0, int* hv, int* cd) {
   const int rows = B.hf_rows, cols = B.hf_cols;
-  // the 4 x 4 vertex block (rows i-1 .. i+2, cols j-1 .. j+2; clamped at the map edge) read once,
-  // every load issued before the first use
   const bool in_patch = hpatch && (unsigned)(i - 1 - pi0) < LGX_HF_PATCH - 3 && (unsigned)(j - 1 - pj0) < LGX_HF_PATCH - 3;
-  int hv[16], cd[16];
+  if (in_patch) {
+    const int32_t* q = hpatch + (i - 1 - pi0) * LGX_HF_PATCH + (j - 1 - pj0);
+    int w[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int da = k >> 2, db = k & 3;
-    if (in_patch) {
-      const int v = hpatch[(i - 1 + da - pi0) * LGX_HF_PATCH + (j - 1 + db - pj0)];
-      hv[k] = v >> 8;
-      cd[k] = v & 15;
-    } else {
-      const int a = min(max(i - 1 + da, 0), rows - 1), b = min(max(j - 1 + db, 0), cols - 1);
+    for (int k = 0; k < 16; ++k) w[k] = q[(k >> 2) * LGX_HF_PATCH + (k & 3)];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { hv[k] = w[k] >> 8; cd[k] = w[k] & 15; }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int a = min(max(i - 1 + (k >> 2), 0), rows - 1), b = min(max(j - 1 + (k & 3), 0), cols - 1);
       hv[k] = B.height_samples[(int64_t)a * cols + b];
-      cd[k] = B.hf_trimesh[(int64_t)a * cols + b] & 15;
+      cd[k] = B.hf_trimesh[(int64_t)a * cols + b];
     }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) cd[k] &= 15;
   }
-  // early out: p more than r above every vertex of the block (no face within r, not below the
-  // surface) - the spheres off the ground leave here
+}
+
+// the cell (i, j) under world point p (clamped to the map)
+LGX_DEV void tm_cell(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, int* i, int* j) {
+  const float hs = P->horizontal_scale;
+  const float u = (p.x + P->border_size) / hs, v = (p.y + P->border_size) / hs;
+  *i = min(max((int)floorf(u), 0), B.hf_rows - 2);
+  *j = min(max((int)floorf(v), 0), B.hf_cols - 2);
+}
+
+// false when the sphere is more than r above every vertex of the 4 x 4 block around its cell (no
+// face within r, not below the surface): the query's early out
+LGX_DEV bool tm_near(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, const int32_t* hpatch,
+                     int pi0, int pj0) {
+  int i, j, hv[16], cd[16];
+  tm_cell(P, B, p, &i, &j);
+  tm_block(B, i, j, hpatch, pi0, pj0, hv, cd);
   int hmax = hv[0];
 #pragma unroll
   for (int k = 1; k < 16; ++k) hmax = max(hmax, hv[k]);
-  if (p.z - r > (float)hmax * vs) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
-  // the geometry in a frame at raw vertex (i, j) (coordinates of a few cells: float precision of the
-  // nearest point and normal independent of how far the env is from the world origin); no fma
-  // contraction in the frame change, so the oracle's restatement rounds identically
+  return !(p.z - r > (float)hmax * P->vertical_scale);
+}
+
+// The corrected-mesh query is built from three pieces shared by the one-lane form (trimesh_depth) and
+// the 16-lanes-per-query form of the physics kernel, so both round identically:
+// tm_local: the geometry in a frame at raw vertex (i, j) (coordinates of a few cells: float precision
+// of the nearest point and normal independent of how far the env is from the world origin); no fma
+// contraction in the frame change, so the oracle's restatement rounds identically
+LGX_DEV f3 tm_local(const lgx_env_params* __restrict__ P, f3 p, int i, int j) {
+  const float hs = P->horizontal_scale, bo = P->border_size;
   const float ox = __fsub_rn(__fmul_rn((float)i, hs), bo), oy = __fsub_rn(__fmul_rn((float)j, hs), bo);
-  p = mk3(__fsub_rn(p.x, ox), __fsub_rn(p.y, oy), p.z);
-  TmQuery q;
+  return mk3(__fsub_rn(p.x, ox), __fsub_rn(p.y, oy), p.z);
+}
+
+// tm_cell_tris: cell (ca, cb) of the 3 x 3 around (i, j) (ca, cb in 0..2) against local point p: its 4
+// samples (LDS patch or global), moved vertices, cull (off the map; p more than r above every vertex
+// of the cell - no contact, not below its surface; or outside its xy box grown by r - farther than r,
+// not over it), then its two triangles into q in the reference order
+LGX_DEV void tm_cell_tris(TmQuery& q, const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i,
+                          int j, int ca, int cb, const int32_t* hpatch, int pi0, int pj0) {
+  const float hs = P->horizontal_scale, vs = P->vertical_scale;
+  const int rows = B.hf_rows, cols = B.hf_cols;
+  const int ci = i - 1 + ca, cj = j - 1 + cb;
+  if (ci < 0 || ci > rows - 2 || cj < 0 || cj > cols - 2) return;
+  int h[4], code[4];   // samples (ci + (k & 1), cj + (k >> 1))
+  if (hpatch && (unsigned)(ci - pi0) < LGX_HF_PATCH - 1 && (unsigned)(cj - pj0) < LGX_HF_PATCH - 1) {
+    const int32_t* w = hpatch + (ci - pi0) * LGX_HF_PATCH + (cj - pj0);
+    const int w0 = w[0], w1 = w[LGX_HF_PATCH], w2 = w[1], w3 = w[LGX_HF_PATCH + 1];
+    h[0] = w0 >> 8; h[1] = w1 >> 8; h[2] = w2 >> 8; h[3] = w3 >> 8;
+    code[0] = w0 & 15; code[1] = w1 & 15; code[2] = w2 & 15; code[3] = w3 & 15;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t o = (int64_t)(ci + (k & 1)) * cols + cj + (k >> 1);
+      h[k] = B.height_samples[o];
+      code[k] = B.hf_trimesh[o];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) code[k] &= 15;
+  }
+  f3 v[4];   // (ci, cj), (ci + 1, cj), (ci, cj + 1), (ci + 1, cj + 1)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int da = ca + (k & 1), db = cb + (k >> 1);
+    const int dx = ((code[k] * 11) >> 5) - 1, dy = code[k] - 3 * (dx + 1) - 1;
+    v[k] = mk3((float)(da - 1 + dx) * hs, (float)(db - 1 + dy) * hs, (float)h[k] * vs);
+  }
+  const float zmax = fmaxf(fmaxf(v[0].z, v[1].z), fmaxf(v[2].z, v[3].z));
+  const float xmin = fminf(fminf(v[0].x, v[1].x), fminf(v[2].x, v[3].x)), xmax = fmaxf(fmaxf(v[0].x, v[1].x), fmaxf(v[2].x, v[3].x));
+  const float ymin = fminf(fminf(v[0].y, v[1].y), fminf(v[2].y, v[3].y)), ymax = fmaxf(fmaxf(v[0].y, v[1].y), fmaxf(v[2].y, v[3].y));
+  if (p.z - r > zmax || p.x < xmin - r || p.x > xmax + r || p.y < ymin - r || p.y > ymax + r) return;
+  tm_tri(q, p, v[0], v[3], v[2]);   // reference triangle order (ind0, ind3, ind1), (ind0, ind2, ind3)
+  tm_tri(q, p, v[0], v[1], v[3]);
+}
+
+LGX_DEV void tm_init(TmQuery& q, f3 p) {
   q.d2 = 3.0e38f; q.cp = p; q.cn = mk3(0.f, 0.f, 1.f);
   q.top = -3.0e38f; q.tn = mk3(0.f, 0.f, 1.f);
-#pragma unroll
-  for (int ca = 0; ca < 3; ++ca)
-#pragma unroll
-    for (int cb = 0; cb < 3; ++cb) {
-      const int ci = i - 1 + ca, cj = j - 1 + cb;
-      if (ci < 0 || ci > rows - 2 || cj < 0 || cj > cols - 2) continue;
-      f3 v[4];   // (ci, cj), (ci + 1, cj), (ci, cj + 1), (ci + 1, cj + 1)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int da = ca + (k & 1), db = cb + (k >> 1);
-        const int code = cd[da * 4 + db];
-        const int dx = ((code * 11) >> 5) - 1, dy = code - 3 * (dx + 1) - 1;
-        v[k] = mk3((float)(da - 1 + dx) * hs, (float)(db - 1 + dy) * hs, (float)hv[da * 4 + db] * vs);
-      }
-      // cull: p more than r above every vertex of the cell (no contact, not below its surface) or
-      // outside its xy box grown by r (farther than r, not over it): most queries keep one cell
-      const float zmax = fmaxf(fmaxf(v[0].z, v[1].z), fmaxf(v[2].z, v[3].z));
-      const float xmin = fminf(fminf(v[0].x, v[1].x), fminf(v[2].x, v[3].x)), xmax = fmaxf(fmaxf(v[0].x, v[1].x), fmaxf(v[2].x, v[3].x));
-      const float ymin = fminf(fminf(v[0].y, v[1].y), fminf(v[2].y, v[3].y)), ymax = fmaxf(fmaxf(v[0].y, v[1].y), fmaxf(v[2].y, v[3].y));
-      if (p.z - r > zmax || p.x < xmin - r || p.x > xmax + r || p.y < ymin - r || p.y > ymax + r) continue;
-      tm_tri(q, p, v[0], v[3], v[2]);   // reference triangle order (ind0, ind3, ind1), (ind0, ind2, ind3)
-      tm_tri(q, p, v[0], v[1], v[3]);
-    }
+}
+
+// tm_finish: inside = p below the surface under it; depth = r -/+ distance, normal = from the surface
+// point toward p (outside) or from p toward it (inside); where p sits on the surface, the face normal
+LGX_DEV float tm_finish(const TmQuery& q, f3 p, float r, f3* n) {
   const bool inside = p.z < q.top;
   const float d = sqrtf(q.d2);
   if (d > 1e-7f) {
@@ -399,14 +441,51 @@ LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buff
   return inside ? r + d : r - d;
 }
 
-// Ground contact of a sphere / point (radius r) centred at world p: spheres (r > 0: feet, capsule
-// ends) against the corrected trimesh where its contact table flags the cell (near a moved vertex);
-// everything else against the triangulated heightfield under p (identical where no vertex of the
-// neighbourhood moved), depth along its face normal.  Box corners (r = 0) keep the heightfield query
-// everywhere: on a fallen robot dozens of them sit near the ground, and the full query per point
-// (up to 18 triangles, latency-bound at one wave per SIMD) cost 2x the whole physics launch.
-LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, f3* n,
-                             const int32_t* patch, int pi0, int pj0) {
+// Signed contact depth of a sphere (radius r >= 0, centre p, world frame) against the corrected
+// mesh around cell (i, j): the nearest surface point over the two triangles of each cell of the
+// 3 x 3 cells around (i, j) (the moves are at most one cell, so every face within r < one cell of
+// p is among them), in cell order, after the block-height early out (the spheres off the ground).
+LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
+                            f3* n, const int32_t* hpatch, int pi0, int pj0) {
+  if (!tm_near(P, B, p, r, hpatch, pi0, pj0)) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
+  p = tm_local(P, p, i, j);
+  TmQuery q;
+  tm_init(q, p);
+#pragma unroll
+  for (int c = 0; c < 9; ++c) tm_cell_tris(q, P, B, p, r, i, j, c / 3, c % 3, hpatch, pi0, pj0);
+  return tm_finish(q, p, r, n);
+}
+
+// the query state of the lane 16 - `m` lanes away in a 16-lane row (xor m, DPP), as floats
+template <int M>
+LGX_DEV float row_xor(float v) {
+  return M == 1 ? lane_xor1(v) : M == 2 ? lane_xor2(v) : M == 4 ? lane_xor4(v) : lane_xor8(v);
+}
+// combine the per-cell query states of a 16-lane row (lane g holds cell g, g < 9): the smallest
+// distance and the highest covering surface, ties to the lower cell - the order of the sequential
+// scan (strict comparisons, first triangle kept), so the result equals trimesh_depth's
+template <int M>
+LGX_DEV void tm_combine_step(TmQuery& q, int& cd2, int& ctop) {
+  const float od2 = row_xor<M>(q.d2), otop = row_xor<M>(q.top);
+  const int ocd2 = __builtin_bit_cast(int, row_xor<M>(__builtin_bit_cast(float, cd2)));
+  const int octop = __builtin_bit_cast(int, row_xor<M>(__builtin_bit_cast(float, ctop)));
+  const f3 ocp = mk3(row_xor<M>(q.cp.x), row_xor<M>(q.cp.y), row_xor<M>(q.cp.z));
+  const f3 ocn = mk3(row_xor<M>(q.cn.x), row_xor<M>(q.cn.y), row_xor<M>(q.cn.z));
+  const f3 otn = mk3(row_xor<M>(q.tn.x), row_xor<M>(q.tn.y), row_xor<M>(q.tn.z));
+  if (od2 < q.d2 || (od2 == q.d2 && ocd2 < cd2)) { q.d2 = od2; q.cp = ocp; q.cn = ocn; cd2 = ocd2; }
+  if (otop > q.top || (otop == q.top && octop < ctop)) { q.top = otop; q.tn = otn; ctop = octop; }
+}
+
+// Ground contact of a sphere / point (radius r) centred at world p, first stage: spheres (r > 0: feet,
+// capsule ends) on a cell its contact table flags (near a moved vertex) need the corrected-trimesh
+// query (`*defer` = true, depth not computed); everything else is answered here against the
+// triangulated heightfield under p (identical where no vertex of the neighbourhood moved), depth
+// along its face normal.  Box corners (r = 0) keep the heightfield query everywhere: on a fallen
+// robot dozens of them sit near the ground, and the full query per point (up to 18 triangles,
+// latency-bound at one wave per SIMD) cost 2x the whole physics launch.
+LGX_DEV float ground_cell(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, f3* n,
+                          const int32_t* patch, int pi0, int pj0, bool* defer) {
+  *defer = false;
   if (P->terrain_kind == 0 || B.height_samples == nullptr) { *n = mk3(0.f, 0.f, 1.f); return r - p.z; }
   const float hs = P->horizontal_scale, vs = P->vertical_scale;
   const float u = (p.x + P->border_size) / hs, v = (p.y + P->border_size) / hs;
@@ -423,7 +502,7 @@ LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buf
     const int tb = B.hf_trimesh ? B.hf_trimesh[o] & 0xff : 4;
     q00 = (H[o] << 8) | tb; q10 = H[o + B.hf_cols] << 8; q01 = H[o + 1] << 8; q11 = H[o + B.hf_cols + 1] << 8;
   }
-  if (r > 0.f && B.hf_trimesh && (q00 & 16)) return trimesh_depth(P, B, p, r, i, j, n, patch, pi0, pj0);
+  if (r > 0.f && B.hf_trimesh && (q00 & 16)) { *defer = true; return 0.f; }
   // triangulated heightfield (diagonal (i, j)-(i+1, j+1)), depth along the face normal
   const float h00 = (float)(q00 >> 8) * vs, h10 = (float)(q10 >> 8) * vs, h01 = (float)(q01 >> 8) * vs,
               h11 = (float)(q11 >> 8) * vs;
@@ -434,6 +513,25 @@ LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buf
   const float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
   *n = mk3(-gx * inv, -gy * inv, inv);
   return (h - p.z) * n->z + r;
+}
+
+// both stages for one point (the lgx_ground_contact test entry)
+LGX_DEV float ground_contact(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, f3* n,
+                             const int32_t* patch, int pi0, int pj0) {
+  bool defer;
+  const float d = ground_cell(P, B, p, r, n, patch, pi0, pj0, &defer);
+  if (!defer) return d;
+  int i, j;
+  tm_cell(P, B, p, &i, &j);
+  return trimesh_depth(P, B, p, r, i, j, n, patch, pi0, pj0);
+}
+
+// LDS written by some lanes of a wave and read by others of the same wave: order the accesses
+// (wave-scope fences; no workgroup barrier - every queue below is wave-private)
+LGX_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace
@@ -483,6 +581,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   // terrain around each base: height << 8 | trimesh contact-table byte (4 = unmoved, unflagged)
   __shared__ int32_t hf_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];
   __shared__ int32_t hf_org[ENVS][2];
+  // per-wave queue of the candidates that need the corrected-trimesh query: (slot << 6 | lane)
+  __shared__ uint16_t tm_q[PP][64 * SLOTS];
   {
     const int4* src = reinterpret_cast<const int4*>(DMg);
     int4* dst = reinterpret_cast<int4*>(&smodel);
@@ -504,7 +604,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   const bool valid = e < N;
   const int ec = valid ? e : N - 1;  // inactive lanes compute on a clamped env, never store
 
-  LGX_CLK_DECL(8)
+  LGX_CLK_DECL(12)
   const float dt = M->sim_dt;
   // ---- load state
   const float* rs = B.root_states + (int64_t)ec * 13;
@@ -588,6 +688,15 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   const int pi0 = use_patch ? hf_org[eb][0] : 0, pj0 = use_patch ? hf_org[eb][1] : 0;
   const int npts = DM->lane_npts[leg];
   const int maxpts = DM->max_lane_npts;
+  // this lane's candidates (point index, dynamic body) per slot, fixed for the launch: the geometry
+  // loop's model reads then no longer wait on one another
+  int slot_pt[SLOTS], slot_db[SLOTS];
+#pragma unroll
+  for (int sl = 0; sl < SLOTS; ++sl) {
+    const int c = pl + PP * sl;
+    slot_pt[sl] = DM->lane_pts[leg][c < npts ? c : 0];
+    slot_db[sl] = M->point_dyn[slot_pt[sl]];
+  }
   f3 cf_leg[4] = {mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0), mk3(0, 0, 0)};
   f3 cf_base = mk3(0, 0, 0);
   float tq[3] = {0.f, 0.f, 0.f};
@@ -667,6 +776,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     sv S[3];
 #pragma unroll
     for (int i = 0; i < 9; ++i) ecom[27 + i] = R0.a[i];
+    ecom[36] = pos.x; ecom[37] = pos.y; ecom[38] = pos.z;
     {
       m33 Rp = R0;
       f3 op = mk3(0, 0, 0);
@@ -801,6 +911,116 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     // ---- contacts: two passes (pass 0 implicit stick, pass 1 with slide / drop decisions)
     const float kn = M->contact_k, cn = M->contact_c, ct = M->friction_c;
     const float wn = dt * (cn + dt * kn);
+    // contact geometry of every candidate (positions do not change within the substep): contact
+    // point, depth and normal of the penetrating ones into LDS, before any contact term is formed
+    // (the terrain queries run without the 54 accumulator registers live).  The corrected-trimesh
+    // query is rare and long: a wave would run it once for every slot in which any of its lanes
+    // needs it, so those candidates are queued (wave-private, ballot-compacted) and answered
+    // afterwards 64 at a time - first the block-height test that dismisses the spheres high above
+    // the ground, then the full query for the near ones.  Same arithmetic per candidate.
+    {
+      const int ln = tid & 63, wv = tid >> 6;
+      const uint64_t below = (1ull << ln) - 1;
+      const int nslots = (maxpts + PP - 1) / PP;    // wave-uniform slot count
+      int qn = 0;
+#pragma unroll
+      for (int sl = 0; sl < SLOTS; ++sl) {
+        if (sl >= nslots) break;
+        const bool act = pl + PP * sl < npts;
+        const int pi = slot_pt[sl];
+        const int db = slot_db[sl];
+        const int k = db == 0 ? -1 : (db - 1) % 3;
+        const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;   // body rotation (+ origin) in LDS
+        m33 R;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
+        f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
+        f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
+        const float rad = M->point_radius[pi];
+        f3 n;
+        bool defer;
+        const float depth = ground_cell(P, B, Pp + pos, rad, &n, patch, pi0, pj0, &defer);
+        defer = defer && act;
+        const uint64_t m = __ballot(defer);
+        if (defer) {
+          tm_q[wv][qn + __popcll(m & below)] = (uint16_t)(sl << 6 | ln);
+          geo_p[sl][tid] = make_float4(Pp.x, Pp.y, Pp.z, rad);
+          geo_n[sl][tid] = make_float4(0.f, 0.f, 1.f, (float)pi);
+        } else if (act) {
+          slot_state[sl][tid] = make_float4(depth > 0.f ? 1.f : 0.f, 0.f, 0.f, 0.f);
+          if (depth > 0.f) {
+            const f3 Pc = Pp - rad * n;
+            geo_p[sl][tid] = make_float4(Pc.x, Pc.y, Pc.z, depth);
+            geo_n[sl][tid] = make_float4(n.x, n.y, n.z, (float)pi);
+          }
+        }
+        qn += __popcll(m);
+      }
+      LGX_CLK(8);
+      if (qn > 0) {
+        wave_lds_sync();
+        // stage 1: block-height test, survivors compacted in place (a round reads all its entries
+        // before it writes any, and writes only positions below the ones it read)
+        int qn2 = 0;
+        for (int q0 = 0; q0 < qn; q0 += 64) {
+          const int q = q0 + ln;
+          int ent = 0;
+          bool near = false;
+          if (q < qn) {
+            ent = tm_q[wv][q];
+            const int sl2 = ent >> 6, t = (wv << 6) | (ent & 63), e2 = t / LPE;
+            const float4 g = geo_p[sl2][t];
+            const f3 pw = mk3(g.x, g.y, g.z) + mk3(env_com[e2][36], env_com[e2][37], env_com[e2][38]);
+            near = tm_near(P, B, pw, g.w, use_patch ? hf_patch[e2] : nullptr, use_patch ? hf_org[e2][0] : 0, use_patch ? hf_org[e2][1] : 0);
+            if (!near) slot_state[sl2][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          const uint64_t m = __ballot(near);
+          if (near) tm_q[wv][qn2 + __popcll(m & below)] = (uint16_t)ent;
+          qn2 += __popcll(m);
+        }
+        wave_lds_sync();
+        LGX_CLK(9);
+#ifdef LGX_PHASE_CLOCK
+        lgx_clk_acc[11] += (uint64_t)qn * 1000 + qn2;   // queue lengths (tuning builds)
+#endif
+        // stage 2: the full query for the spheres near the ground, 16 lanes per sphere (lane g < 9 of
+        // the row takes cell g of the 3 x 3), combined across the row in the sequential scan's order
+        const int grp = ln >> 4, g = ln & 15;
+        for (int q0 = 0; q0 < qn2; q0 += 4) {
+          const int q = min(q0 + grp, qn2 - 1);
+          const int ent = tm_q[wv][q];
+          const int sl2 = ent >> 6, t = (wv << 6) | (ent & 63), e2 = t / LPE;
+          const float4 gp = geo_p[sl2][t];
+          const f3 Pp = mk3(gp.x, gp.y, gp.z);
+          const f3 pw = Pp + mk3(env_com[e2][36], env_com[e2][37], env_com[e2][38]);
+          const int32_t* hp = use_patch ? hf_patch[e2] : nullptr;
+          const int o0 = use_patch ? hf_org[e2][0] : 0, o1 = use_patch ? hf_org[e2][1] : 0;
+          int i, j;
+          tm_cell(P, B, pw, &i, &j);
+          const f3 pl3 = tm_local(P, pw, i, j);
+          TmQuery tq;
+          tm_init(tq, pl3);
+          if (g < 9) tm_cell_tris(tq, P, B, pl3, gp.w, i, j, (g * 11) >> 5, g - 3 * ((g * 11) >> 5), hp, o0, o1);
+          int cd2 = g, ctop = g;
+          tm_combine_step<1>(tq, cd2, ctop);
+          tm_combine_step<2>(tq, cd2, ctop);
+          tm_combine_step<4>(tq, cd2, ctop);
+          tm_combine_step<8>(tq, cd2, ctop);
+          if (g == 0 && q0 + grp < qn2) {
+            f3 n;
+            const float depth = tm_finish(tq, pl3, gp.w, &n);
+            slot_state[sl2][t] = make_float4(depth > 0.f ? 1.f : 0.f, 0.f, 0.f, 0.f);
+            if (depth > 0.f) {
+              const f3 Pc = Pp - gp.w * n;
+              geo_p[sl2][t] = make_float4(Pc.x, Pc.y, Pc.z, depth);
+              geo_n[sl2][t] = make_float4(n.x, n.y, n.z, geo_n[sl2][t].w);
+            }
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+    LGX_CLK(10);
     float xb[6];
     f3 xl;
     for (int pass = 0; pass < 2; ++pass) {
@@ -814,37 +1034,14 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       L.rl[0] = L.rl[1] = L.rl[2] = 0.f;
       for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
         if (c >= npts) break;
-        float4 st = slot_state[sl][tid];
-        f3 Pc, n;
-        float depth;
-        int k;
-        if (pass == 0) {
-          const int pi = DM->lane_pts[leg][c];
-          const int db = M->point_dyn[pi];
-          k = db == 0 ? -1 : (db - 1) % 3;
-          const float* fr = db == 0 ? ecom + 27 : kin + 12 * k;   // body rotation (+ origin) in LDS
-          m33 R;
-#pragma unroll
-          for (int i = 0; i < 9; ++i) R.a[i] = fr[i];
-          f3 ol = db == 0 ? mk3(0, 0, 0) : mk3(fr[9], fr[10], fr[11]);
-          f3 Pp = ol + mul(R, mk3(M->point_pos[pi][0], M->point_pos[pi][1], M->point_pos[pi][2]));
-          const float rad = M->point_radius[pi];
-          depth = ground_contact(P, B, Pp + pos, rad, &n, patch, pi0, pj0);
-          st.x = depth > 0.f ? 1.f : 0.f;
-          slot_state[sl][tid] = st;
-          if (depth <= 0.f) continue;
-          Pc = Pp - rad * n;
-          geo_p[sl][tid] = make_float4(Pc.x, Pc.y, Pc.z, depth);
-          geo_n[sl][tid] = make_float4(n.x, n.y, n.z, (float)pi);
-        } else {
-          if (st.x == 0.f) continue;  // separated in pass 0: same geometry, no contact
-          const float4 gp = geo_p[sl][tid], gn = geo_n[sl][tid];
-          Pc = mk3(gp.x, gp.y, gp.z);
-          depth = gp.w;
-          n = mk3(gn.x, gn.y, gn.z);
-          const int db = M->point_dyn[(int)gn.w];
-          k = db == 0 ? -1 : (db - 1) % 3;
-        }
+        const float4 st = slot_state[sl][tid];
+        if (st.x == 0.f) continue;  // separated (pass 1: in pass 0's classification)
+        const float4 gp = geo_p[sl][tid], gn = geo_n[sl][tid];
+        const f3 Pc = mk3(gp.x, gp.y, gp.z);
+        const float depth = gp.w;
+        const f3 n = mk3(gn.x, gn.y, gn.z);
+        const int db = M->point_dyn[(int)gn.w];
+        const int k = db == 0 ? -1 : (db - 1) % 3;
         float wt = (pass == 0 || st.x == 1.f) ? dt * ct : 0.f;
         f3 f = (dt * kn * depth) * n;
         if (pass == 1 && st.x == 2.f) f = f + dt * mk3(st.y, st.z, st.w);
@@ -997,7 +1194,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     ro[10] = wang.x; ro[11] = wang.y; ro[12] = wang.z;
   }
   LGX_CLK(7);
-  LGX_CLK_PRINT("physics", 8)
+  LGX_CLK_PRINT("physics", 12)
 }
 
 // ground_contact for a batch of world points (test entry lgx_ground_contact): q[k] = (x, y, z, r)
@@ -1049,7 +1246,7 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
 #ifdef LGX_PHASE_CLOCK_BUF
 // instrumented builds only (tools/phase_clock.sh): the per-workgroup clock table of the last physics launch
 extern "C" int lgx_debug_clock(unsigned long long* out, int32_t nblocks) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(lgx_clk_buf), (size_t)min(nblocks, LGX_CLK_MAXB) * 10 * 8, 0,
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(lgx_clk_buf), (size_t)min(nblocks, LGX_CLK_MAXB) * 14 * 8, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

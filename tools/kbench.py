@@ -262,7 +262,7 @@ def phys_run(task="go1_rough", n=4096, steps=int(os.environ.get("KB_STEPS", "10"
         import ctypes as C
         import numpy as np
         nb = (n + 15) // 16
-        buf = np.zeros((nb, 10), dtype=np.uint64)
+        buf = np.zeros((nb, 14), dtype=np.uint64)
         L.lgx_debug_clock(buf.ctypes.data_as(C.c_void_p), C.c_int32(nb))
         os.makedirs("gpurun_out", exist_ok=True)
         np.save(os.environ.get("KB_CLK_OUT", "gpurun_out/clk.npy"), buf)
