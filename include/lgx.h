@@ -234,8 +234,8 @@ int lgx_trimesh_build(const int16_t* height_samples, int32_t rows, int32_t cols,
                       int8_t* contact_table, void* stream);
 
 /* Lanes per leg (1, 2, 4 or 8) of the physics launch at `num_envs` envs, i.e. which
- * lgx_physics_kernel<PP> instantiation lgx_step / lgx_simulate run: 4 below 8192 envs, 2 below
- * 16384, 1 above (env LGX_PHYS_PP overrides); LGX_EINVAL for num_envs <= 0. */
+ * lgx_physics_kernel<PP> instantiation lgx_step / lgx_simulate run: 4 at every size (env
+ * LGX_PHYS_PP overrides); LGX_EINVAL for num_envs <= 0. */
 int32_t lgx_physics_lane_split(int32_t num_envs);
 
 /* Bytes of scratch the caller must bind in lgx_buffers.scratch. */

@@ -84,8 +84,10 @@ LGX_DEV float sv_get(const sv& v, int i) {
 }
 
 // 6x6 SPD solve (packed sym), in registers
+// (the substitutions multiply by the factorisation's reciprocal diagonal: 12 of the 18 correctly
+// rounded divisions of the textbook form, ~10 instructions each, on the per-substep critical path)
 LGX_DEV void chol6_solve(float* A, float* b) {
-  float L[21];
+  float L[21], Li[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     float s = A[sidx(j, j)];
@@ -93,7 +95,8 @@ LGX_DEV void chol6_solve(float* A, float* b) {
     for (int k = 0; k < j; ++k) s -= L[sidx(j, k)] * L[sidx(j, k)];
     float d = sqrtf(fmaxf(s, 1e-20f));
     L[sidx(j, j)] = d;
-    float inv = 1.0f / d;
+    const float inv = 1.0f / d;
+    Li[j] = inv;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       float t = A[sidx(i, j)];
@@ -107,14 +110,14 @@ LGX_DEV void chol6_solve(float* A, float* b) {
     float t = b[i];
 #pragma unroll
     for (int k = 0; k < i; ++k) t -= L[sidx(i, k)] * b[k];
-    b[i] = t / L[sidx(i, i)];
+    b[i] = t * Li[i];
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
     float t = b[i];
 #pragma unroll
     for (int k = i + 1; k < 6; ++k) t -= L[sidx(k, i)] * b[k];
-    b[i] = t / L[sidx(i, i)];
+    b[i] = t * Li[i];
   }
 }
 
@@ -355,19 +358,6 @@ LGX_DEV void tm_cell(const lgx_env_params* __restrict__ P, const lgx_buffers& B,
   *j = min(max((int)floorf(v), 0), B.hf_cols - 2);
 }
 
-// false when the sphere is more than r above every vertex of the 4 x 4 block around its cell (no
-// face within r, not below the surface): the query's early out
-LGX_DEV bool tm_near(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, const int32_t* hpatch,
-                     int pi0, int pj0) {
-  int i, j, hv[16], cd[16];
-  tm_cell(P, B, p, &i, &j);
-  tm_block(B, i, j, hpatch, pi0, pj0, hv, cd);
-  int hmax = hv[0];
-#pragma unroll
-  for (int k = 1; k < 16; ++k) hmax = max(hmax, hv[k]);
-  return !(p.z - r > (float)hmax * P->vertical_scale);
-}
-
 // The corrected-mesh query is built from three pieces shared by the one-lane form (trimesh_depth) and
 // the 16-lanes-per-query form of the physics kernel, so both round identically:
 // tm_local: the geometry in a frame at raw vertex (i, j) (coordinates of a few cells: float precision
@@ -441,19 +431,82 @@ LGX_DEV float tm_finish(const TmQuery& q, f3 p, float r, f3* n) {
   return inside ? r + d : r - d;
 }
 
+// false when the sphere is more than r above every vertex of the 4 x 4 block around its cell (i, j)
+// (no face within r, not below the surface): the query's early out on its own
+LGX_DEV bool tm_near(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
+                     const int32_t* hpatch, int pi0, int pj0) {
+  int hv[16], cd[16];
+  tm_block(B, i, j, hpatch, pi0, pj0, hv, cd);
+  int hmax = hv[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) hmax = max(hmax, hv[k]);
+  return !(p.z - r > (float)hmax * P->vertical_scale);
+}
+
+// tm_keep: the cells of the 3 x 3 around p's cell (i, j) the query has to visit (bit ca * 3 + cb):
+// 0 when p is more than r above every vertex of the 4 x 4 block (the spheres off the ground) or every
+// cell is culled (tm_cell_tris' tests, here on the block decoded once in registers) - no face within
+// r and p not below the surface: no contact.  `pl` returns p in the local frame.
+LGX_DEV unsigned tm_keep(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
+                         const int32_t* hpatch, int pi0, int pj0, f3* pl) {
+  const float hs = P->horizontal_scale, vs = P->vertical_scale;
+  const int rows = B.hf_rows, cols = B.hf_cols;
+  int hv[16], cd[16];
+  tm_block(B, i, j, hpatch, pi0, pj0, hv, cd);
+  int hmax = hv[0];
+#pragma unroll
+  for (int k = 1; k < 16; ++k) hmax = max(hmax, hv[k]);
+  p = tm_local(P, p, i, j);
+  *pl = p;
+  if (p.z - r > (float)hmax * vs) return 0u;
+  unsigned keep = 0;
+#pragma unroll
+  for (int ca = 0; ca < 3; ++ca)
+#pragma unroll
+    for (int cb = 0; cb < 3; ++cb) {
+      const int ci = i - 1 + ca, cj = j - 1 + cb;
+      f3 v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int da = ca + (k & 1), db = cb + (k >> 1);
+        const int code = cd[da * 4 + db];
+        const int dx = ((code * 11) >> 5) - 1, dy = code - 3 * (dx + 1) - 1;
+        v[k] = mk3((float)(da - 1 + dx) * hs, (float)(db - 1 + dy) * hs, (float)hv[da * 4 + db] * vs);
+      }
+      const float zmax = fmaxf(fmaxf(v[0].z, v[1].z), fmaxf(v[2].z, v[3].z));
+      const float xmin = fminf(fminf(v[0].x, v[1].x), fminf(v[2].x, v[3].x)), xmax = fmaxf(fmaxf(v[0].x, v[1].x), fmaxf(v[2].x, v[3].x));
+      const float ymin = fminf(fminf(v[0].y, v[1].y), fminf(v[2].y, v[3].y)), ymax = fmaxf(fmaxf(v[0].y, v[1].y), fmaxf(v[2].y, v[3].y));
+      const bool on_map = ci >= 0 && ci <= rows - 2 && cj >= 0 && cj <= cols - 2;
+      const bool cull = p.z - r > zmax || p.x < xmin - r || p.x > xmax + r || p.y < ymin - r || p.y > ymax + r;
+      if (on_map && !cull) keep |= 1u << (ca * 3 + cb);
+    }
+  return keep;
+}
+
+// the kept cells of a query in cell order (the sequential scan: strict comparisons, first triangle kept)
+LGX_DEV float tm_visit(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 pl, float r, int i, int j,
+                       unsigned keep, f3* n, const int32_t* hpatch, int pi0, int pj0) {
+  TmQuery q;
+  tm_init(q, pl);
+  while (keep) {
+    const int c = __builtin_ctz(keep);
+    keep &= keep - 1;
+    const int ca = (c * 11) >> 5;   // c / 3 for c < 9
+    tm_cell_tris(q, P, B, pl, r, i, j, ca, c - 3 * ca, hpatch, pi0, pj0);
+  }
+  return tm_finish(q, pl, r, n);
+}
+
 // Signed contact depth of a sphere (radius r >= 0, centre p, world frame) against the corrected
 // mesh around cell (i, j): the nearest surface point over the two triangles of each cell of the
 // 3 x 3 cells around (i, j) (the moves are at most one cell, so every face within r < one cell of
-// p is among them), in cell order, after the block-height early out (the spheres off the ground).
+// p is among them) that the culls keep, in cell order; -1 (normal up) when no cell is kept.
 LGX_DEV float trimesh_depth(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, float r, int i, int j,
                             f3* n, const int32_t* hpatch, int pi0, int pj0) {
-  if (!tm_near(P, B, p, r, hpatch, pi0, pj0)) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
-  p = tm_local(P, p, i, j);
-  TmQuery q;
-  tm_init(q, p);
-#pragma unroll
-  for (int c = 0; c < 9; ++c) tm_cell_tris(q, P, B, p, r, i, j, c / 3, c % 3, hpatch, pi0, pj0);
-  return tm_finish(q, p, r, n);
+  f3 pl;
+  const unsigned keep = tm_keep(P, B, p, r, i, j, hpatch, pi0, pj0, &pl);
+  if (!keep) { *n = mk3(0.f, 0.f, 1.f); return -1.f; }
+  return tm_visit(P, B, pl, r, i, j, keep, n, hpatch, pi0, pj0);
 }
 
 // the query state of the lane 16 - `m` lanes away in a 16-lane row (xor m, DPP), as floats
@@ -581,8 +634,8 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   // terrain around each base: height << 8 | trimesh contact-table byte (4 = unmoved, unflagged)
   __shared__ int32_t hf_patch[ENVS][LGX_HF_PATCH * LGX_HF_PATCH];
   __shared__ int32_t hf_org[ENVS][2];
-  // per-wave queue of the candidates that need the corrected-trimesh query: (slot << 6 | lane)
-  __shared__ uint16_t tm_q[PP][64 * SLOTS];
+  // per-wave queue of the candidates that need the corrected-trimesh query: (cells << 16 | slot << 6 | lane)
+  __shared__ uint32_t tm_q[PP][64 * SLOTS];
   {
     const int4* src = reinterpret_cast<const int4*>(DMg);
     int4* dst = reinterpret_cast<int4*>(&smodel);
@@ -943,7 +996,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         defer = defer && act;
         const uint64_t m = __ballot(defer);
         if (defer) {
-          tm_q[wv][qn + __popcll(m & below)] = (uint16_t)(sl << 6 | ln);
+          tm_q[wv][qn + __popcll(m & below)] = (uint32_t)(sl << 6 | ln);
           geo_p[sl][tid] = make_float4(Pp.x, Pp.y, Pp.z, rad);
           geo_n[sl][tid] = make_float4(0.f, 0.f, 1.f, (float)pi);
         } else if (act) {
@@ -959,23 +1012,37 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       LGX_CLK(8);
       if (qn > 0) {
         wave_lds_sync();
-        // stage 1: block-height test, survivors compacted in place (a round reads all its entries
-        // before it writes any, and writes only positions below the ones it read)
+        // stage 1: which cells of the 3 x 3 each sphere has to visit, survivors compacted in place with
+        // their cell set (a round reads all its entries before it writes any, and writes only
+        // positions below the ones it read).  Short queues (a Go1's feet): the block-height test
+        // alone (the spheres well above the ground leave), every cell kept - stage 2 culls them per
+        // lane; long queues (a capsule-covered robot like ANYmal on stairs): the cell culls too, so
+        // fewer spheres reach stage 2 and each visits only its kept cells
+        const bool cull1 = qn > 16;
         int qn2 = 0;
         for (int q0 = 0; q0 < qn; q0 += 64) {
           const int q = q0 + ln;
-          int ent = 0;
-          bool near = false;
+          uint32_t ent = 0;
+          unsigned keep = 0;
           if (q < qn) {
             ent = tm_q[wv][q];
-            const int sl2 = ent >> 6, t = (wv << 6) | (ent & 63), e2 = t / LPE;
+            const int sl2 = (ent >> 6) & 1023, t = (wv << 6) | (ent & 63), e2 = t / LPE;
             const float4 g = geo_p[sl2][t];
             const f3 pw = mk3(g.x, g.y, g.z) + mk3(env_com[e2][36], env_com[e2][37], env_com[e2][38]);
-            near = tm_near(P, B, pw, g.w, use_patch ? hf_patch[e2] : nullptr, use_patch ? hf_org[e2][0] : 0, use_patch ? hf_org[e2][1] : 0);
-            if (!near) slot_state[sl2][t] = make_float4(0.f, 0.f, 0.f, 0.f);
+            const int32_t* hp = use_patch ? hf_patch[e2] : nullptr;
+            const int o0 = use_patch ? hf_org[e2][0] : 0, o1 = use_patch ? hf_org[e2][1] : 0;
+            int i, j;
+            tm_cell(P, B, pw, &i, &j);
+            if (cull1) {
+              f3 pl3;
+              keep = tm_keep(P, B, pw, g.w, i, j, hp, o0, o1, &pl3);
+            } else {
+              keep = tm_near(P, B, pw, g.w, i, j, hp, o0, o1) ? 0x1ffu : 0u;
+            }
+            if (!keep) slot_state[sl2][t] = make_float4(0.f, 0.f, 0.f, 0.f);
           }
-          const uint64_t m = __ballot(near);
-          if (near) tm_q[wv][qn2 + __popcll(m & below)] = (uint16_t)ent;
+          const uint64_t m = __ballot(keep != 0);
+          if (keep) tm_q[wv][qn2 + __popcll(m & below)] = ent | keep << 16;
           qn2 += __popcll(m);
         }
         wave_lds_sync();
@@ -983,37 +1050,66 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 #ifdef LGX_PHASE_CLOCK
         lgx_clk_acc[11] += (uint64_t)qn * 1000 + qn2;   // queue lengths (tuning builds)
 #endif
-        // stage 2: the full query for the spheres near the ground, 16 lanes per sphere (lane g < 9 of
-        // the row takes cell g of the 3 x 3), combined across the row in the sequential scan's order
-        const int grp = ln >> 4, g = ln & 15;
-        for (int q0 = 0; q0 < qn2; q0 += 4) {
-          const int q = min(q0 + grp, qn2 - 1);
-          const int ent = tm_q[wv][q];
-          const int sl2 = ent >> 6, t = (wv << 6) | (ent & 63), e2 = t / LPE;
-          const float4 gp = geo_p[sl2][t];
-          const f3 Pp = mk3(gp.x, gp.y, gp.z);
-          const f3 pw = Pp + mk3(env_com[e2][36], env_com[e2][37], env_com[e2][38]);
-          const int32_t* hp = use_patch ? hf_patch[e2] : nullptr;
-          const int o0 = use_patch ? hf_org[e2][0] : 0, o1 = use_patch ? hf_org[e2][1] : 0;
-          int i, j;
-          tm_cell(P, B, pw, &i, &j);
-          const f3 pl3 = tm_local(P, pw, i, j);
-          TmQuery tq;
-          tm_init(tq, pl3);
-          if (g < 9) tm_cell_tris(tq, P, B, pl3, gp.w, i, j, (g * 11) >> 5, g - 3 * ((g * 11) >> 5), hp, o0, o1);
-          int cd2 = g, ctop = g;
-          tm_combine_step<1>(tq, cd2, ctop);
-          tm_combine_step<2>(tq, cd2, ctop);
-          tm_combine_step<4>(tq, cd2, ctop);
-          tm_combine_step<8>(tq, cd2, ctop);
-          if (g == 0 && q0 + grp < qn2) {
-            f3 n;
-            const float depth = tm_finish(tq, pl3, gp.w, &n);
-            slot_state[sl2][t] = make_float4(depth > 0.f ? 1.f : 0.f, 0.f, 0.f, 0.f);
-            if (depth > 0.f) {
-              const f3 Pc = Pp - gp.w * n;
-              geo_p[sl2][t] = make_float4(Pc.x, Pc.y, Pc.z, depth);
-              geo_n[sl2][t] = make_float4(n.x, n.y, n.z, geo_n[sl2][t].w);
+        // stage 2: the kept cells of each near sphere.  Few spheres (the common case: a robot's feet on
+        // a riser): 16 lanes per sphere, lane g < 9 of the row visits cell g if kept, the row combines
+        // in the sequential scan's order.  Many (a capsule-covered robot like ANYmal on stairs): one
+        // lane per sphere visiting its kept cells in order (a round costs its lane with the most
+        // cells, typically 1 - 3 of the 9)
+        if (qn2 <= 8) {
+          const int grp = ln >> 4, g = ln & 15;
+          for (int q0 = 0; q0 < qn2; q0 += 4) {
+            const int q = min(q0 + grp, qn2 - 1);
+            const uint32_t ent = tm_q[wv][q];
+            const int sl2 = (ent >> 6) & 1023, t = (wv << 6) | (ent & 63), e2 = t / LPE;
+            const float4 gp = geo_p[sl2][t];
+            const f3 Pp = mk3(gp.x, gp.y, gp.z);
+            const f3 pw = Pp + mk3(env_com[e2][36], env_com[e2][37], env_com[e2][38]);
+            const int32_t* hp = use_patch ? hf_patch[e2] : nullptr;
+            const int o0 = use_patch ? hf_org[e2][0] : 0, o1 = use_patch ? hf_org[e2][1] : 0;
+            int i, j;
+            tm_cell(P, B, pw, &i, &j);
+            const f3 pl3 = tm_local(P, pw, i, j);
+            TmQuery tq;
+            tm_init(tq, pl3);
+            if (g < 9 && ((ent >> (16 + g)) & 1u))
+              tm_cell_tris(tq, P, B, pl3, gp.w, i, j, (g * 11) >> 5, g - 3 * ((g * 11) >> 5), hp, o0, o1);
+            int cd2 = g, ctop = g;
+            tm_combine_step<1>(tq, cd2, ctop);
+            tm_combine_step<2>(tq, cd2, ctop);
+            tm_combine_step<4>(tq, cd2, ctop);
+            tm_combine_step<8>(tq, cd2, ctop);
+            if (g == 0 && q0 + grp < qn2) {
+              f3 n;
+              const float depth = tm_finish(tq, pl3, gp.w, &n);
+              slot_state[sl2][t] = make_float4(depth > 0.f ? 1.f : 0.f, 0.f, 0.f, 0.f);
+              if (depth > 0.f) {
+                const f3 Pc = Pp - gp.w * n;
+                geo_p[sl2][t] = make_float4(Pc.x, Pc.y, Pc.z, depth);
+                geo_n[sl2][t] = make_float4(n.x, n.y, n.z, geo_n[sl2][t].w);
+              }
+            }
+          }
+        } else {
+          for (int q0 = 0; q0 < qn2; q0 += 64) {
+            const int q = q0 + ln;
+            if (q < qn2) {
+              const uint32_t ent = tm_q[wv][q];
+              const int sl2 = (ent >> 6) & 1023, t = (wv << 6) | (ent & 63), e2 = t / LPE;
+              const float4 gp = geo_p[sl2][t];
+              const f3 Pp = mk3(gp.x, gp.y, gp.z);
+              const f3 pw = Pp + mk3(env_com[e2][36], env_com[e2][37], env_com[e2][38]);
+              int i, j;
+              tm_cell(P, B, pw, &i, &j);
+              f3 n;
+              const float depth = tm_visit(P, B, tm_local(P, pw, i, j), gp.w, i, j, ent >> 16, &n,
+                                           use_patch ? hf_patch[e2] : nullptr, use_patch ? hf_org[e2][0] : 0,
+                                           use_patch ? hf_org[e2][1] : 0);
+              slot_state[sl2][t] = make_float4(depth > 0.f ? 1.f : 0.f, 0.f, 0.f, 0.f);
+              if (depth > 0.f) {
+                const f3 Pc = Pp - gp.w * n;
+                geo_p[sl2][t] = make_float4(Pc.x, Pc.y, Pc.z, depth);
+                geo_n[sl2][t] = make_float4(n.x, n.y, n.z, geo_n[sl2][t].w);
+              }
             }
           }
         }
@@ -1217,13 +1313,16 @@ int lgx_launch_ground_contact(const lgx_env_params* dp, const lgx_buffers& b, co
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-// lanes per leg: enough waves to cover the 1024 SIMDs of the chip, 1 for huge batches;
-// LGX_PHYS_PP (1, 2, 4, 8) overrides it for A/B runs and for the parity tests of every split
+// lanes per leg: 4 at every size (4096 envs x 16 lanes = 1024 waves = one per SIMD; larger batches run
+// in rounds of one 16-env workgroup per CU - the 148 KB of LDS per workgroup admit one, so a 2- or
+// 1-lane split would leave 2 or 3 SIMDs of each CU idle: measured C5 8192 envs 355 -> 283 us,
+// 16384 envs 670 -> 568 us for 2 -> 4 lanes); LGX_PHYS_PP (1, 2, 4, 8) overrides it for A/B runs
+// and for the parity tests of every split
 int lgx_physics_pp(int32_t n_envs) {
-  const int pp = n_envs >= 16384 ? 1 : (n_envs >= 8192 ? 2 : 4);
+  (void)n_envs;
   const char* force = getenv("LGX_PHYS_PP");
   const int f = force ? atoi(force) : 0;
-  return (f == 1 || f == 2 || f == 4 || f == 8) ? f : pp;
+  return (f == 1 || f == 2 || f == 4 || f == 8) ? f : 4;
 }
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,

@@ -1,6 +1,6 @@
-"""GPU at the benchmark sizes: C3 (go1_rough, 4096 envs/GPU: lgx_physics_kernel<4>), C5
-(anymal_c_rough with friction / base-mass / push randomisation, 8192 envs/GPU: <2>) and 16384
-envs (<1>): size-independent properties of a rollout, oracle parity of a strided 64-env subset
+"""GPU at the benchmark sizes: C3 (go1_rough, 4096 envs/GPU: one round of lgx_physics_kernel<4>
+workgroups), C5 (anymal_c_rough with friction / base-mass / push randomisation, 8192 envs/GPU: two
+rounds) and 16384 envs (four rounds): size-independent properties of a rollout, oracle parity of a strided 64-env subset
 taken from the full-size run, and the every-env-resets-at-once edge case.
 
 Tolerances as test_gpu_parity.py (physics model identical, algorithms differ: dense vs Schur).
@@ -64,12 +64,13 @@ def test_full_size_rollout_properties(big):
 def test_full_size_subset_matches_oracle(gpu, task, n):
     """Envs 0, n/64, 2n/64, ... of the n-env device state, stepped by the 64-env oracle.  Draws
     are keyed by env index, so observation noise is off (both envs) and only non-resetting envs
-    are compared in full.  The physics launch at n envs picks its lane split from n (PP = 4 / 2 /
-    1 at 4096 / 8192 / 16384), so each size runs its own kernel instantiation."""
+    are compared in full.  The physics launch runs 4 lanes per leg at every size (1, 2 and 4
+    rounds of one workgroup per CU at 4096 / 8192 / 16384; the other splits are covered at 64 envs
+    by test_gpu_parity.py)."""
     from legged_gym_amd.sim import lib as lgxlib
     dev = _big(task, n)
     N = n
-    assert lgxlib.load().lgx_physics_lane_split(N) == {4096: 4, 8192: 2, 16384: 1}[N]
+    assert lgxlib.load().lgx_physics_lane_split(N) == 4
     idx = torch.arange(0, N, N // 64)
     ora = make_env(task, num_envs=64, device="cpu", backend="oracle", overrides=_no_noise)
     if not torch.equal(ora.height_samples, dev.height_samples.cpu()):

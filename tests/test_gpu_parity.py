@@ -468,7 +468,7 @@ def test_anymal_c_rough_dr_step_matches_oracle(gpu, monkeypatch, pp):
     full domain randomisation - friction buckets U[0.5, 1.25] (legged_robot.py:259-282), base mass
     +U[-5, 5] kg (anymal_c_rough_config.py:80-81, legged_robot.py:312-335) and the push at step
     751 (legged_robot.py:436-441) - two env steps, HIP path vs oracle.  pp = LGX_PHYS_PP: every
-    lane split of lgx_physics_kernel (4 below 8192 envs, 2 at 8192 = C5's size, 1 from 16384)."""
+    lane split of lgx_physics_kernel (4 = the default at every size; 2 and 1 as A/B variants)."""
     monkeypatch.setenv("LGX_PHYS_PP", pp)
     ora = make_env("anymal_c_rough", num_envs=64, device="cpu", backend="oracle")
     dev = make_env("anymal_c_rough", num_envs=64, device="cuda:0", backend="lgx")
