@@ -352,8 +352,8 @@ LGX_DEV void tm_block(const lgx_buffers& B, int i, int j, const int32_t* hpatch,
 
 // the cell (i, j) under world point p (clamped to the map)
 LGX_DEV void tm_cell(const lgx_env_params* __restrict__ P, const lgx_buffers& B, f3 p, int* i, int* j) {
-  const float hs = P->horizontal_scale;
-  const float u = (p.x + P->border_size) / hs, v = (p.y + P->border_size) / hs;
+  const float ihs = 1.0f / P->horizontal_scale;
+  const float u = (p.x + P->border_size) * ihs, v = (p.y + P->border_size) * ihs;
   *i = min(max((int)floorf(u), 0), B.hf_rows - 2);
   *j = min(max((int)floorf(v), 0), B.hf_cols - 2);
 }
@@ -540,8 +540,10 @@ LGX_DEV float ground_cell(const lgx_env_params* __restrict__ P, const lgx_buffer
                           const int32_t* patch, int pi0, int pj0, bool* defer) {
   *defer = false;
   if (P->terrain_kind == 0 || B.height_samples == nullptr) { *n = mk3(0.f, 0.f, 1.f); return r - p.z; }
-  const float hs = P->horizontal_scale, vs = P->vertical_scale;
-  const float u = (p.x + P->border_size) / hs, v = (p.y + P->border_size) / hs;
+  // cell and slopes on the reciprocal of the horizontal scale (uniform: one division per launch, not
+  // four correctly rounded ones per query; the oracle rounds the same way)
+  const float ihs = 1.0f / P->horizontal_scale, vs = P->vertical_scale;
+  const float u = (p.x + P->border_size) * ihs, v = (p.y + P->border_size) * ihs;
   const int i = min(max((int)floorf(u), 0), B.hf_rows - 2), j = min(max((int)floorf(v), 0), B.hf_cols - 2);
   // the cell's 4 samples (height << 8 | contact-table byte in the LDS patch) in one round trip
   int q00, q10, q01, q11;
@@ -561,8 +563,8 @@ LGX_DEV float ground_cell(const lgx_env_params* __restrict__ P, const lgx_buffer
               h11 = (float)(q11 >> 8) * vs;
   const float fu = clampf(u - (float)i, 0.f, 1.f), fv = clampf(v - (float)j, 0.f, 1.f);
   float gx, gy, h;
-  if (fu >= fv) { gx = (h10 - h00) / hs; gy = (h11 - h10) / hs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
-  else          { gx = (h11 - h01) / hs; gy = (h01 - h00) / hs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
+  if (fu >= fv) { gx = (h10 - h00) * ihs; gy = (h11 - h10) * ihs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
+  else          { gx = (h11 - h01) * ihs; gy = (h01 - h00) * ihs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
   const float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
   *n = mk3(-gx * inv, -gy * inv, inv);
   return (h - p.z) * n->z + r;

@@ -156,8 +156,8 @@ static float ground(const ctx_t* cx, float x, float y, float* n) {
   const lgx_env_params* p = cx->p;
   const lgx_buffers* b = cx->b;
   if (p->terrain_kind == 0 || !b->height_samples) { n[0] = 0; n[1] = 0; n[2] = 1; return 0.0f; }
-  float hs = p->horizontal_scale, vs = p->vertical_scale;
-  float u = (x + p->border_size) / hs, v = (y + p->border_size) / hs;
+  float ihs = 1.0f / p->horizontal_scale, vs = p->vertical_scale;   /* reciprocal scale, as the kernel */
+  float u = (x + p->border_size) * ihs, v = (y + p->border_size) * ihs;
   int i = (int)floorf(u), j = (int)floorf(v);
   if (i < 0) i = 0; if (i > b->hf_rows - 2) i = b->hf_rows - 2;
   if (j < 0) j = 0; if (j > b->hf_cols - 2) j = b->hf_cols - 2;
@@ -167,8 +167,8 @@ static float ground(const ctx_t* cx, float x, float y, float* n) {
   float h00 = H[i * b->hf_cols + j] * vs, h10 = H[(i + 1) * b->hf_cols + j] * vs;
   float h01 = H[i * b->hf_cols + j + 1] * vs, h11 = H[(i + 1) * b->hf_cols + j + 1] * vs;
   float gx, gy, h;
-  if (fu >= fv) { gx = (h10 - h00) / hs; gy = (h11 - h10) / hs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
-  else          { gx = (h11 - h01) / hs; gy = (h01 - h00) / hs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
+  if (fu >= fv) { gx = (h10 - h00) * ihs; gy = (h11 - h10) * ihs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
+  else          { gx = (h11 - h01) * ihs; gy = (h01 - h00) * ihs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
   float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
   n[0] = -gx * inv; n[1] = -gy * inv; n[2] = inv;
   return h;
@@ -294,8 +294,9 @@ static float ground_contact(const ctx_t* cx, const float* p, float r, float* n) 
   const lgx_env_params* P = cx->p;
   const lgx_buffers* b = cx->b;
   if (r > 0.0f && b->hf_trimesh && P->terrain_kind != 0 && b->height_samples) {
-    int i = (int)floorf((p[0] + P->border_size) / P->horizontal_scale);
-    int j = (int)floorf((p[1] + P->border_size) / P->horizontal_scale);
+    const float ihs = 1.0f / P->horizontal_scale;
+    int i = (int)floorf((p[0] + P->border_size) * ihs);
+    int j = (int)floorf((p[1] + P->border_size) * ihs);
     if (i < 0) i = 0; if (i > b->hf_rows - 2) i = b->hf_rows - 2;
     if (j < 0) j = 0; if (j > b->hf_cols - 2) j = b->hf_cols - 2;
     if (b->hf_trimesh[(int64_t)i * b->hf_cols + j] & 16) return trimesh_depth(cx, p, r, i, j, n);
