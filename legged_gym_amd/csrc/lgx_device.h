@@ -150,11 +150,30 @@ LGX_DEV float lane_xor8(float v) {
   return (threadIdx.x & 8) ? dn : up;
 }
 
-// sum over the 4 lanes of a quad; every lane gets the bitwise-identical ((a+b)+(c+d)) order
+// DPP source operand meant to fold into the consuming VALU op (bound_ctrl with full masks: the
+// compiler's DPP combine turns `v + dpp_src(v)` into one v_add_f32_dpp)
+template <int CTRL>
+LGX_DEV float dpp_src(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// sum over the 4 lanes of a quad; every lane gets the bitwise-identical ((a+b)+(c+d)) value
+// (float addition is commutative)
 LGX_DEV float quad_sum(float v) {
-  v += lane_xor1(v);
-  v += lane_xor2(v);
+  v += dpp_src<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_src<0x4E>(v);   // quad_perm [2,3,0,1]
   return v;
+}
+
+// sum over the 4 quads of a 16-lane row (lanes r, r^4, r^8, r^12) in lane_xor4 / lane_xor8's order
+// ((v_p + v_p^1) + (v_p^2 + v_p^3)) for quad index p, on DPP adds: row_ror:4 brings quad p-1, row_ror:12
+// quad p+1 - the partner p^1 for odd / even p - then row_ror:8 brings p^2.  Every lane of the row gets
+// the same value (float addition is commutative), and the same as the shuffle form.
+LGX_DEV float row_quads_sum(float v) {
+  const float b = v + dpp_src<0x124>(v);   // row_ror:4  : v_p + v_(p-1)
+  const float c = v + dpp_src<0x12C>(v);   // row_ror:12 : v_p + v_(p+1)
+  const float a = (threadIdx.x & 4) ? b : c;
+  return a + dpp_src<0x128>(a);            // row_ror:8  : + a_(p^2)
 }
 
 // triangulated heightfield (diagonal (i,j)-(i+1,j+1), isaacgym terrain_utils trimesh).

@@ -600,6 +600,7 @@ LGX_DEV void wave_lds_sync() {
 // sum over the PP lanes that share a leg (lane bits 2..): contact terms were split across them
 template <int PP>
 LGX_DEV float psum(float v) {
+  if (PP == 4) return row_quads_sum(v);   // an env is one 16-lane DPP row: two rotates
   if (PP >= 2) v += lane_xor4(v);
   if (PP >= 4) v += lane_xor8(v);
   if (PP >= 8) v += __shfl_xor(v, 16);
