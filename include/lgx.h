@@ -375,6 +375,15 @@ int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
 int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_values, float* returns,
             float* advantages, int32_t T, int32_t N, float gamma, float lam, void* stream);
 
+/* lgx_gae followed by rsl_rl's advantage normalisation (single process: rl/storage.py
+ * compute_returns, `(adv - adv.mean()) / (adv.std() + 1e-8)`, unbiased std) in place - two
+ * launches instead of the GAE kernel + the torch mean / std / elementwise chain.  scratch:
+ * lgx_gae_norm_scratch(N) doubles of device memory (per-workgroup sums, fixed order). */
+int64_t lgx_gae_norm_scratch(int32_t N);
+int lgx_gae_norm(const float* rewards, const float* values, const uint8_t* dones, const float* last_values,
+                 float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam, double* scratch,
+                 void* stream);
+
 /* ---- PPO update (rsl_rl PPO.update, legged_robot_config.py:226-239): the non-GEMM work of a
  * minibatch step.  Activations are net-major [2 (actor, critic), M, H]; the GEMMs between
  * these calls are library GEMMs issued by the host.  All pointers are device pointers. */

@@ -46,6 +46,8 @@ int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, c
 int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t stream);
 int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream);
+int lgx_launch_gae_norm(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
+                        float* adv, int32_t T, int32_t N, float gamma, float lam, double* scratch, hipStream_t stream);
 
 // Kernel-tight timing for lgx_profile_*: when the caller arms a (start, stop) event pair, the
 // next LGX_LAUNCH on this thread is dispatched with hipExtLaunchKernelGGL, which records the

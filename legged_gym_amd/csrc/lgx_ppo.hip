@@ -761,7 +761,12 @@ struct Mirror {
   int64_t off, dst_ld, dst_bs;  // off: first flat index of the block in p
   float* dst;
   int32_t count, rows, cols, transpose;   // count = batch * rows * cols
-};
+  uint64_t inv_rc, inv_cols;    // ceil(2^40 / (rows * cols)), ceil(2^40 / cols): exact quotients
+};                              // for every index < count (host-checked: count * rows * cols < 2^40)
+
+// floor(l / d) for l < 2^20-ish ranges as one 64-bit multiply-shift (inv = ceil(2^40 / d), exact
+// while l * d < 2^40) instead of the ~40-instruction 32-bit integer division, three per element
+__device__ __forceinline__ int32_t mdiv(int32_t l, uint64_t inv) { return (int32_t)(((uint64_t)l * inv) >> 40); }
 constexpr int MAX_MIRRORS = LGX_MAX_REDUCE_JOBS;
 struct Mirrors {
   Mirror mj[MAX_MIRRORS];
@@ -830,7 +835,7 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
       const uint64_t li = (uint64_t)(i - J.off);
       if (li < (uint64_t)J.count) {
         const int32_t l = (int32_t)li, rc = J.rows * J.cols;
-        const int32_t b = l / rc, rem = l - b * rc, rr = rem / J.cols, cc = rem - rr * J.cols;
+        const int32_t b = mdiv(l, J.inv_rc), rem = l - b * rc, rr = mdiv(rem, J.inv_cols), cc = rem - rr * J.cols;
         mirror_store(J, b, rr, cc, pi);
       }
     }
@@ -1084,7 +1089,11 @@ extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int6
       return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: mirror source must be a contiguous block of p");
     if ((j.transpose & 2) && (((j.transpose & 1) ? j.cols : j.rows) % 128))   // x3_limb_off: N % 128
       return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: a limb mirror needs output rows % 128 == 0");
-    M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose};
+    const uint64_t rc = (uint64_t)j.rows * j.cols;
+    if ((uint64_t)count * rc >= (1ULL << 40))
+      return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: mirror block too large for the index arithmetic");
+    M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose,
+                     ((1ULL << 40) + rc - 1) / rc, ((1ULL << 40) + (uint64_t)j.cols - 1) / (uint64_t)j.cols};
   }
   hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
   int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);

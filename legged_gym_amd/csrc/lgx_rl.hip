@@ -4,31 +4,92 @@
 #include "lgx_device.h"
 #include "lgx_internal.h"
 
-__global__ void lgx_gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
-                               const uint8_t* __restrict__ dones, const float* __restrict__ last_val,
-                               float* __restrict__ ret, float* __restrict__ adv, int32_t T, int32_t N, float gamma,
-                               float lam) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= N) return;
-  float next_v = last_val[e];
-  float a = 0.f;
-  for (int t = T - 1; t >= 0; --t) {
-    int64_t i = (int64_t)t * N + e;
-    float v = val[i];
-    float nt = 1.0f - (float)dones[i];
-    float delta = rew[i] + nt * gamma * next_v - v;
-    a = delta + nt * gamma * lam * a;
-    float r = a + v;
-    ret[i] = r;
-    adv[i] = r - v;
-    next_v = v;
+#include <algorithm>
+
+// part != nullptr: each workgroup also writes the sum and the sum of squares of its advantages
+// (double, fixed reduction order) to part[2 * blockIdx.x ...] for lgx_adv_norm_kernel
+__global__ void __launch_bounds__(256) lgx_gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
+                                                      const uint8_t* __restrict__ dones,
+                                                      const float* __restrict__ last_val, float* __restrict__ ret,
+                                                      float* __restrict__ adv, int32_t T, int32_t N, float gamma,
+                                                      float lam, double* __restrict__ part) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  double s = 0.0, q = 0.0;
+  if (e < N) {
+    float next_v = last_val[e];
+    float a = 0.f;
+    for (int t = T - 1; t >= 0; --t) {
+      int64_t i = (int64_t)t * N + e;
+      float v = val[i];
+      float nt = 1.0f - (float)dones[i];
+      float delta = rew[i] + nt * gamma * next_v - v;
+      a = delta + nt * gamma * lam * a;
+      float r = a + v;
+      ret[i] = r;
+      const float d = r - v;
+      adv[i] = d;
+      s += d;
+      q += (double)d * d;
+      next_v = v;
+    }
   }
+  if (!part) return;
+  __shared__ double rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      rs[threadIdx.x] += rs[threadIdx.x + w];
+      rq[threadIdx.x] += rq[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = rs[0];
+    part[2 * blockIdx.x + 1] = rq[0];
+  }
+}
+
+// rsl_rl's advantage normalisation, (adv - adv.mean()) / (adv.std() + 1e-8) with the unbiased
+// std, in place: every workgroup re-reduces the GAE partials in the same order (double), then
+// normalises its slice in f32 as torch does from the f32 mean / std
+__global__ void __launch_bounds__(256) lgx_adv_norm_kernel(float* __restrict__ adv, int64_t n,
+                                                           const double* __restrict__ part, int32_t nparts) {
+  __shared__ float ms[2];
+  if (threadIdx.x == 0) {
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < nparts; ++i) {
+      s += part[2 * i];
+      q += part[2 * i + 1];
+    }
+    const double mean = s / (double)n;
+    const double var = n > 1 ? fmax((q - (double)n * mean * mean) / (double)(n - 1), 0.0) : 0.0;
+    ms[0] = (float)mean;
+    ms[1] = (float)sqrt(var) + 1e-8f;
+  }
+  __syncthreads();
+  const float mean = ms[0], den = ms[1];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    adv[i] = (adv[i] - mean) / den;
 }
 
 int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream) {
   if (T <= 0 || N <= 0) return -1;
   hipLaunchKernelGGL(lgx_gae_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, rew, val, dones, last_val, ret, adv, T,
-                     N, gamma, lam);
+                     N, gamma, lam, (double*)nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int lgx_launch_gae_norm(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
+                        float* adv, int32_t T, int32_t N, float gamma, float lam, double* scratch, hipStream_t stream) {
+  if (T <= 0 || N <= 0) return -1;
+  const int nparts = (N + 255) / 256;
+  hipLaunchKernelGGL(lgx_gae_kernel, dim3(nparts), dim3(256), 0, stream, rew, val, dones, last_val, ret, adv, T, N,
+                     gamma, lam, scratch);
+  const int64_t n = (int64_t)T * N;
+  const int blocks = (int)std::min<int64_t>((n + 1023) / 1024, 256);
+  hipLaunchKernelGGL(lgx_adv_norm_kernel, dim3(blocks), dim3(256), 0, stream, adv, n, (const double*)scratch, nparts);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

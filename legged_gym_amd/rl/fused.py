@@ -18,3 +18,22 @@ def gae(rewards, values, dones, last_values, returns, advantages, gamma, lam):
     stream = C.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
     lgxlib.check(lib.lgx_gae(_vp(rewards), _vp(values), _vp(dones), _vp(last_values), _vp(returns), _vp(advantages),
                              T, N, float(gamma), float(lam), stream), "lgx_gae")
+
+
+_scratch = {}
+
+
+def gae_norm(rewards, values, dones, last_values, returns, advantages, gamma, lam):
+    """gae() + rsl_rl's advantage normalisation in place (single process): lgx_gae_norm."""
+    from legged_gym_amd.sim import lib as lgxlib
+    lib = lgxlib.load()
+    T, N = rewards.shape[0], rewards.shape[1]
+    for t in (rewards, values, dones, returns, advantages, last_values):
+        assert t.is_cuda and t.is_contiguous()
+    key = (rewards.device, N)
+    if key not in _scratch:
+        _scratch[key] = torch.empty(int(lib.lgx_gae_norm_scratch(N)), dtype=torch.float64, device=rewards.device)
+    stream = C.c_void_p(torch.cuda.current_stream(rewards.device).cuda_stream)
+    lgxlib.check(lib.lgx_gae_norm(_vp(rewards), _vp(values), _vp(dones), _vp(last_values), _vp(returns),
+                                  _vp(advantages), T, N, float(gamma), float(lam), _vp(_scratch[key]), stream),
+                 "lgx_gae_norm")

@@ -196,7 +196,8 @@ class PPO:
 
     def compute_returns(self, last_critic_obs):
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
-        self.storage.compute_returns(last_values, self.gamma, self.lam, reduce_stats=self._adv_stats)
+        self.storage.compute_returns(last_values, self.gamma, self.lam,
+                                     reduce_stats=self._adv_stats if self.dist is not None else None)
 
     # ---------------------------------------------------------------- update
     def _allreduce_grads(self):
@@ -210,9 +211,11 @@ class PPO:
             p.grad.copy_(flat[off:off + n].view_as(p.grad))
             off += n
 
-    def update(self):
+    def update(self, defer=False):
+        """rsl_rl PPO.update -> (mean value loss, mean surrogate loss).  defer=True (fused path only)
+        issues the update and returns None; resolve() returns the losses later (FusedPPOUpdate)."""
         if self._fused is not None:
-            out = self._fused.update()
+            out = self._fused.update(defer=defer)
             self.storage.clear()
             if hasattr(self.actor_critic, "invalidate_fused"):
                 self.actor_critic.invalidate_fused()
@@ -268,4 +271,15 @@ class PPO:
         mean_value_loss = (mean_value_loss / n).item()
         mean_surrogate_loss = (mean_surrogate_loss / n).item()
         self.storage.clear()
+        if defer:
+            self._deferred = (mean_value_loss, mean_surrogate_loss)
+            return None
         return mean_value_loss, mean_surrogate_loss
+
+    def resolve(self):
+        """The losses of an update(defer=True) (applying the fused path's learning-rate readback),
+        or None when none is pending."""
+        if self._fused is not None:
+            return self._fused.resolve()
+        out, self._deferred = getattr(self, "_deferred", None), None
+        return out

@@ -372,9 +372,11 @@ def test_mlp_forward_batch_actor_critic(gpu):
     assert ac._fused_actor.last_x3 and ac._fused_critic.last_x3   # the split-bf16 kernel ran
 
 
-def test_gae_kernel_matches_torch_loop(gpu):
+@pytest.mark.parametrize("N", [1000, 4096, 3])
+def test_gae_kernel_matches_torch_loop(gpu, N):
+    """lgx_gae_norm (GAE + rsl_rl's advantage normalisation, unbiased std) vs the torch loop."""
     from legged_gym_amd.rl.storage import RolloutStorage
-    T, N = 24, 1000
+    T = 24
     gen = torch.Generator().manual_seed(1)
     st_c = RolloutStorage(N, T, [4], [None], [2], "cpu")
     st_c.rewards.copy_(torch.randn(T, N, 1, generator=gen))

@@ -148,3 +148,36 @@ def test_runner_iteration_matches_reference_semantics(gpu, tmp_path):
     assert set(ck) == {"model_state_dict", "optimizer_state_dict", "iter", "infos"} and ck["iter"] == 1
     for k, p in alg.actor_critic.state_dict().items():
         assert torch.equal(ck["model_state_dict"][k], p), k
+
+
+def test_deferred_readback_matches_synchronous_runner(gpu, tmp_path):
+    """learn() without a log directory issues each update with a deferred readback (the
+    statistics are taken after the next rollout is issued); with one it reads them back at once.
+    Same seeds, 3 iterations each: identical parameters, Adam moments, learning rate and final
+    iteration statistics (bitwise: the same kernels in the same order)."""
+    from legged_gym_amd.envs.go1.go1_config import Go1RoughCfgPPO
+    from legged_gym_amd.rl.runner import OnPolicyRunner
+    from legged_gym_amd.utils.helpers import class_to_dict
+    out = []
+    for log_dir in (None, str(tmp_path)):
+        env = make_env("go1_rough", num_envs=256, device="cuda:0", backend="lgx")
+        cfg = class_to_dict(Go1RoughCfgPPO())
+        cfg["runner"]["save_interval"] = 100
+        torch.manual_seed(0)
+        runner = OnPolicyRunner(env, cfg, log_dir, device="cuda:0")
+        deferred = []
+        orig = runner.alg.update
+        runner.alg.update = lambda defer=False: (deferred.append(defer), orig(defer=defer))[1]
+        torch.manual_seed(7)
+        runner.learn(3, init_at_random_ep_len=True)
+        torch.cuda.synchronize()
+        assert deferred == [log_dir is None] * 3
+        assert runner.alg._fused._pending is None
+        o = runner.alg.optimizer
+        out.append(([p.detach().clone() for p in runner.alg.actor_critic.parameters()],
+                    o.m.clone(), o.v.clone(), runner.alg.learning_rate, o.param_groups[0]["lr"],
+                    {k: v for k, v in runner.last_iteration_stats.items() if k.endswith("loss") or k == "learning_rate"}))
+    (pa, ma, va, lra, pga, sa), (pb, mb, vb, lrb, pgb, sb) = out
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    assert torch.equal(ma, mb) and torch.equal(va, vb)
+    assert lra == lrb and pga == pgb and sa == sb, (lra, lrb, sa, sb)
