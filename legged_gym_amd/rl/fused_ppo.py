@@ -501,7 +501,6 @@ class FusedPPOUpdate:
         job(self.head_parts, self.Wg[self.L], (A + 1) * h[-1], 1, 0, hchunks, nh, 0)  # dW head (actor | critic)
         hp_b = self.head_parts[(A + 1) * h[-1]:]
         job(hp_b, self.bo[self.L - 1], 2 * h[-1], 1, 0, hchunks, nh, 0)              # db of the last hidden layer
-        self.db0_job = len(jobs) if self.L > 1 else None                            # (db of hidden layer 1)
         for k in range(self.L - 1):
             cchunks = self.col_parts[k].numel() // (2 * h[k])
             job(self.col_parts[k], self.bo[k], 2 * h[k], 1, 0, cchunks, 2 * h[k], 0)  # db_k
@@ -511,11 +510,6 @@ class FusedPPOUpdate:
         self.njobs = len(jobs)
         self.jobs_dw1 = (abi.LgxReduceJob * n_dw1)(*jobs[:n_dw1])
         self.jobs_rest = (abi.LgxReduceJob * (len(jobs) - n_dw1))(*jobs[n_dw1:])
-        if self.db0_job is not None:   # _backward_two_syncs: db_1 joins dW_1 on the main stream
-            main2 = jobs[:n_dw1] + [jobs[self.db0_job]]
-            side2 = [j for i, j in enumerate(jobs) if i >= n_dw1 and i != self.db0_job]
-            self.jobs_main2 = (abi.LgxReduceJob * len(main2))(*main2)
-            self.jobs_side2 = (abi.LgxReduceJob * len(side2))(*side2)
 
     # ------------------------------------------------------------------ update
     @torch.no_grad()
@@ -715,134 +709,6 @@ class FusedPPOUpdate:
         return out
 
     @torch.no_grad()
-    def _backward(self, M, S, h, L, X, Xc, xs, xp, xcp, args, stream, apply, fused):
-        """Hidden-layer backward of one minibatch (dA with ELU' + bias column sums, dW split-K, the
-        reductions into the flat gradient).  Returns whether the gradient went out in two DDP buckets."""
-        lib, chk, ppo = self.lib, self.check, self.ppo
-        side_on = self.tn and os.environ.get("LGX_PPO_DW_SIDE", "1") != "0"
-        if (side_on and fused and self.loss_bwd and L == 3 and ppo.dist is None and self.db0_job is not None
-                and all(k in self.gemm_dw for k in range(L)) and os.environ.get("LGX_PPO_SCHED", "0") == "2"):
-            self._backward_two_syncs(xp, xcp, args, stream)
-            self.bucketed = False
-            return False
-        dZ = self.Y[L - 1]                           # dZ of the last hidden layer (in place)
-        # dW_k (lgx_gemm_tn) of the hidden layers on a second stream, concurrent with dA_k on this
-        # one (both only read dZ_k and Y_{k-1}): the weight-gradient tiles fill the CUs that the
-        # dA launch's last round leaves idle (measured 19.3 -> 19.0 ms per iteration);
-        # LGX_PPO_DW_SIDE=0 keeps every launch on one stream
-        side_used = False
-        for k in range(L - 1, 0, -1):
-            # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
-            Sl = self.Sk[k]
-            if k in self.gemm_dw and side_on:
-                if getattr(self, "_side", None) is None:
-                    self._side = torch.cuda.Stream(self.dev)
-                    self._ev_in = [torch.cuda.Event() for _ in range(L)]
-                    self._ev_out = torch.cuda.Event()
-                main = torch.cuda.current_stream(self.dev)
-                self._ev_in[k].record(main)
-                self._side.wait_event(self._ev_in[k])
-                for t in self.gemm_dw[k]:
-                    self._gemm_tn(t, C.c_void_p(self._side.cuda_stream), self._side)
-                side_used = True
-            elif k in self.gemm_dw:
-                for t in self.gemm_dw[k]:
-                    self._gemm_tn(t, stream)
-            else:
-                torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2),
-                          self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]), out=self.P[k])
-            if fused:
-                self._gemm(self.gemm_bwd[k], stream)
-            else:
-                torch.bmm(dZ, self.W[k], out=self.D[k - 1])
-                chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
-                                           _vp(self.col_parts[k - 1]), stream), "elu_bwd")
-            dZ = self.D[k - 1]
-        early = (side_used and self.loss_bwd and len(self.jobs_rest) > 0
-                 and os.environ.get("LGX_PPO_EARLY_REDUCE", "1") != "0")
-        if early:
-            # every gradient block but dW1's is complete once dA_1 (this stream) and the side
-            # stream's dW GEMMs are: reduce them (+ the loss finalize) on the side stream while dW1
-            # runs here - the memory-bound reduction next to the MFMA-bound GEMM
-            self._ev_in[0].record(torch.cuda.current_stream(self.dev))
-            self._side.wait_event(self._ev_in[0])
-            chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
-                                               C.c_void_p(self._side.cuda_stream)), "reduce")
-        bucketed = early and apply and ppo.dist is not None
-        self.bucketed = bucketed
-        if bucketed:
-            # data-parallel: the first gradient bucket (every block after dW1's in the layer-major
-            # flat layout + the KL slot) is all-reduced from the side stream as soon as it is
-            # reduced, concurrent with dW1's GEMM here; dW1's bucket follows below (one
-            # communicator: the collectives run in issue order on every rank)
-            with torch.cuda.stream(self._side):
-                self.g_comm[self.n:].copy_(self.stats[0:1])
-                ppo.dist.all_reduce(self.g_comm[self.nW1:])
-        if 0 in self.gemm_dw and fused:     # lgx_gemm_tn over the minibatch's padded input rows
-            t = self.gemm_dw[0]
-            t[0].B = xp.data_ptr()
-            if len(t) > 1:
-                t[1].B = (xcp if xcp is not None else xp).data_ptr()
-            for tk in t:
-                self._gemm_tn(tk, stream)
-        elif xs is not None and len(xs) > 2:    # one batched GEMM: 2 networks x S row slices
-            x2 = xs[2].view(2 * S, M // S, self.Kp)[:, :, :self.num_obs]
-            torch.bmm(dZ.view(2 * S, M // S, h[0]).transpose(1, 2), x2, out=self.P[0].view(2 * S, h[0], self.num_obs))
-        else:
-            torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
-            torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
-        if side_used and not early:   # the weight gradients are complete before the reduction reads them
-            self._ev_out.record(self._side)
-            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
-        if early:   # (dW1's partials come from this stream; the side stream's blocks are joined below)
-            chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
-            if bucketed:
-                ppo.dist.all_reduce(self.g_comm[:self.nW1])
-            self._ev_out.record(self._side)
-            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
-        elif self.loss_bwd:
-            chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
-        else:
-            chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
-        return bucketed
-
-    def _side_stream(self):
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.dev)
-            self._ev_in = [torch.cuda.Event() for _ in range(self.L)]
-            self._ev_out = torch.cuda.Event()
-        return self._side
-
-    def _backward_two_syncs(self, xp, xcp, args, stream):
-        """Single-process backward of the 3-hidden-layer networks with two cross-stream syncs per
-        minibatch instead of four (on ROCm every event record between two launches of a stream
-        costs ~6.5 us of idle GPU there, measured in the kernel trace):
-          this stream:  dA_3 -> [record] -> dA_2 -> dW_1 -> reduce(dW_1 + db_1) -> [wait] -> Adam
-          side stream:  [wait] -> dW_3 -> dW_2 -> reduce(the rest) + loss finalize -> [record]
-        dW_3 needs dZ_3 (the loss launch) and dW_2 needs dZ_2 (dA_3): both precede the one record;
-        db_1's column sums come from dA_2, so its reduction job moves to this stream."""
-        lib, chk = self.lib, self.check
-        side = self._side_stream()
-        side_p = C.c_void_p(side.cuda_stream)
-        main = torch.cuda.current_stream(self.dev)
-        self._gemm(self.gemm_bwd[2], stream)                 # dZ_2 = (dZ_3 W_3) * ELU'(Y_2), db_2 sums
-        self._ev_in[1].record(main)
-        side.wait_event(self._ev_in[1])
-        for k in (2, 1):
-            for t in self.gemm_dw[k]:
-                self._gemm_tn(t, side_p, side)
-        chk(lib.lgx_reduce_slices_finalize(self.jobs_side2, len(self.jobs_side2), C.byref(args), side_p), "reduce")
-        self._ev_out.record(side)
-        self._gemm(self.gemm_bwd[1], stream)                 # dZ_1, db_1 sums
-        t = self.gemm_dw[0]
-        t[0].B = xp.data_ptr()
-        if len(t) > 1:
-            t[1].B = (xcp if xcp is not None else xp).data_ptr()
-        for tk in t:
-            self._gemm_tn(tk, stream)
-        chk(lib.lgx_reduce_slices(self.jobs_main2, len(self.jobs_main2), stream), "reduce")
-        main.wait_event(self._ev_out)
-
     def _minibatch(self, idx, obs, cobs, args, stream, apply=True, xs=None):
         with self.tuned:     # TunableOp table on for the library GEMMs of this minibatch only
             self._minibatch_body(idx, obs, cobs, args, stream, apply, xs)
@@ -926,7 +792,86 @@ class FusedPPOUpdate:
             # ---- backward (+ the loss finalize on one extra workgroup of the same launch)
             chk(lib.lgx_head_bwd_finalize(C.byref(args), _vp(self.dMU), _vp(self.dV), _vp(wha), _vp(whc),
                                           _vp(self.Y[L - 1]), M, A, h[-1], _vp(self.head_parts), stream), "head_bwd")
-        bucketed = self._backward(M, S, h, L, X, Xc, xs, xp, xcp, args, stream, apply, fused)
+        dZ = self.Y[L - 1]                           # dZ of the last hidden layer (in place)
+        # dW_k (lgx_gemm_tn) of the hidden layers on a second stream, concurrent with dA_k on this
+        # one (both only read dZ_k and Y_{k-1}): the weight-gradient tiles fill the CUs that the
+        # dA launch's last round leaves idle (measured 19.3 -> 19.0 ms per iteration);
+        # LGX_PPO_DW_SIDE=0 keeps every launch on one stream
+        side_on = self.tn and os.environ.get("LGX_PPO_DW_SIDE", "1") != "0"
+        side_used = False
+        for k in range(L - 1, 0, -1):
+            # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below)
+            Sl = self.Sk[k]
+            if k in self.gemm_dw and side_on:
+                if getattr(self, "_side", None) is None:
+                    self._side = torch.cuda.Stream(self.dev)
+                    self._ev_in = [torch.cuda.Event() for _ in range(L)]
+                    self._ev_out = torch.cuda.Event()
+                main = torch.cuda.current_stream(self.dev)
+                self._ev_in[k].record(main)
+                self._side.wait_event(self._ev_in[k])
+                for t in self.gemm_dw[k]:
+                    self._gemm_tn(t, C.c_void_p(self._side.cuda_stream), self._side)
+                side_used = True
+            elif k in self.gemm_dw:
+                for t in self.gemm_dw[k]:
+                    self._gemm_tn(t, stream)
+            else:
+                torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2),
+                          self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]), out=self.P[k])
+            if fused:
+                self._gemm(self.gemm_bwd[k], stream)
+            else:
+                torch.bmm(dZ, self.W[k], out=self.D[k - 1])
+                chk(lib.lgx_elu_bwd_colsum(_vp(self.D[k - 1]), _vp(self.Y[k - 1]), M, h[k - 1], 2,
+                                           _vp(self.col_parts[k - 1]), stream), "elu_bwd")
+            dZ = self.D[k - 1]
+        early = (side_used and self.loss_bwd and len(self.jobs_rest) > 0
+                 and os.environ.get("LGX_PPO_EARLY_REDUCE", "1") != "0")
+        if early:
+            # every gradient block but dW1's is complete once dA_1 (this stream) and the side
+            # stream's dW GEMMs are: reduce them (+ the loss finalize) on the side stream while dW1
+            # runs here - the memory-bound reduction next to the MFMA-bound GEMM
+            self._ev_in[0].record(torch.cuda.current_stream(self.dev))
+            self._side.wait_event(self._ev_in[0])
+            chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
+                                               C.c_void_p(self._side.cuda_stream)), "reduce")
+        bucketed = early and apply and ppo.dist is not None
+        self.bucketed = bucketed
+        if bucketed:
+            # data-parallel: the first gradient bucket (every block after dW1's in the layer-major
+            # flat layout + the KL slot) is all-reduced from the side stream as soon as it is
+            # reduced, concurrent with dW1's GEMM here; dW1's bucket follows below (one
+            # communicator: the collectives run in issue order on every rank)
+            with torch.cuda.stream(self._side):
+                self.g_comm[self.n:].copy_(self.stats[0:1])
+                ppo.dist.all_reduce(self.g_comm[self.nW1:])
+        if 0 in self.gemm_dw and fused:     # lgx_gemm_tn over the minibatch's padded input rows
+            t = self.gemm_dw[0]
+            t[0].B = xp.data_ptr()
+            if len(t) > 1:
+                t[1].B = (xcp if xcp is not None else xp).data_ptr()
+            for tk in t:
+                self._gemm_tn(tk, stream)
+        elif xs is not None and len(xs) > 2:    # one batched GEMM: 2 networks x S row slices
+            x2 = xs[2].view(2 * S, M // S, self.Kp)[:, :, :self.num_obs]
+            torch.bmm(dZ.view(2 * S, M // S, h[0]).transpose(1, 2), x2, out=self.P[0].view(2 * S, h[0], self.num_obs))
+        else:
+            torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
+            torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
+        if side_used and not early:   # the weight gradients are complete before the reduction reads them
+            self._ev_out.record(self._side)
+            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
+        if early:   # (dW1's partials come from this stream; the side stream's blocks are joined below)
+            chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
+            if bucketed:
+                ppo.dist.all_reduce(self.g_comm[:self.nW1])
+            self._ev_out.record(self._side)
+            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
+        elif self.loss_bwd:
+            chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
+        else:
+            chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
         if not apply:
             return
         grad_scale = 1.0

@@ -334,10 +334,9 @@ def test_fused_update_matches_numpy_oracle(gpu, schedule):
     assert big <= 1e-3 * total, (big, total, dmax)
 
 
-@pytest.mark.parametrize("schedule,cobs,algo,sched", [("adaptive", None, "split", "2"), ("fixed", None, "split", "2"),
-                                                      ("adaptive", 252, "split", "2"), ("adaptive", None, "f32", "2"),
-                                                      ("adaptive", None, "split", "0")])
-def test_fused_update_every_step_is_exact(gpu, monkeypatch, schedule, cobs, algo, sched):
+@pytest.mark.parametrize("schedule,cobs,algo", [("adaptive", None, "split"), ("fixed", None, "split"),
+                                                ("adaptive", 252, "split"), ("adaptive", None, "f32")])
+def test_fused_update_every_step_is_exact(gpu, monkeypatch, schedule, cobs, algo):
     """Every coordinate of every optimizer step of a full fused update (2 epochs x 4 minibatches),
     recorded as it runs (tests/ppo_trace.py):
       * the flat gradient the step consumed == the autograd gradient (rl/ppo.py's loss, pinned
@@ -346,11 +345,9 @@ def test_fused_update_every_step_is_exact(gpu, monkeypatch, schedule, cobs, algo
       * the parameters / moments after the step == float64 clip_grad_norm_ + torch Adam applied
         to that gradient from the recorded state: |d| <= 1e-6 + 1e-3 lr (p), 1e-5 relative (m, v:
         the f32 global norm);
-      * the learning rate the step used == the adaptive schedule's (same sequence as autograd);
-    both single-process backward stream schedules (LGX_PPO_SCHED 2 / 0)."""
+      * the learning rate the step used == the adaptive schedule's (same sequence as autograd)."""
     from ppo_trace import StepTrace, adam64, flat_view
     monkeypatch.setenv("LGX_GEMM_ALGO", algo)
-    monkeypatch.setenv("LGX_PPO_SCHED", sched)   # 2: two-sync backward schedule (default), 0: four syncs
     ref, fus = make_pair(schedule, cobs)
     tr = StepTrace(fus._fused)
     torch.manual_seed(11)
