@@ -86,6 +86,33 @@ def env_bench(task="go1_rough", n=4096):
     print(f"{task} env.step N={n}: {ms*1e3:.1f} us/step  {n/ms*1e3/1e6:.2f} M env-steps/s (env only)")
 
 
+def env_env_ab(task=os.environ.get("KB_TASK", "go1_rough"), n=int(os.environ.get("KB_N", "4096")),
+               var=os.environ.get("KB_VAR", "LGX_ACT_FIRST"), modes=tuple(os.environ.get("KB_VALUES", "0,1").split(",")),
+               rounds=int(os.environ.get("KB_ROUNDS", "10")), steps=24):
+    """A/B of a per-launch env-step switch (env var `var`), interleaved in ONE process: every round
+    times `steps` env steps per value (HIP events); prints median / min us per step."""
+    from oracle_backend import make_env
+    env = make_env(task, num_envs=n, device="cuda:0", backend="lgx")
+    env.reset()
+    a = torch.randn(n, 12, device="cuda:0")
+    res = {m: [] for m in modes}
+    for r in range(rounds + 1):
+        for m in modes:
+            os.environ[var] = m
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                env.step(a)
+            e1.record()
+            e1.synchronize()
+            if r:
+                res[m].append(e0.elapsed_time(e1) * 1e3 / steps)
+    for m in modes:
+        v = sorted(res[m])
+        print(f"{task} N={n} {var}={m}: env.step median {v[len(v) // 2]:.1f} us, min {v[0]:.1f} us", flush=True)
+
+
 def phys_ab():
     """A/B the physics kernel lanes-per-leg variants in one process."""
     import ctypes as C
@@ -340,5 +367,7 @@ if __name__ == "__main__":
         tn_bench()
     if "update_env" in what:
         update_env_ab()
+    if "env_env" in what:
+        env_env_ab()
 
 
