@@ -425,6 +425,9 @@ typedef struct lgx_ppo_store_args {
   uint8_t* st_dones;
 } lgx_ppo_store_args;
 int lgx_ppo_store(const lgx_ppo_store_args* args, void* stream);
+/* lgx_ppo_act of step t+1 and the deferred lgx_ppo_store of step t in ONE launch (the store reads
+ * only step t's env outputs and storage row t, which the act does not touch); same envs. */
+int lgx_ppo_act_store(const lgx_ppo_act_args* args, const lgx_ppo_store_args* prev, void* stream);
 
 /* dst[r, :] = src[idx[r], :] for r < rows (minibatch gather of storage rows) */
 int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width, void* stream);

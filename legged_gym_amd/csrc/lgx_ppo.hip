@@ -73,10 +73,20 @@ __device__ __forceinline__ void copy_rows(const float* __restrict__ src, float* 
     for (int64_t i = threadIdx.x; i < cnt; i += TPB) dst[i] = src[i];
   }
 }
+// STORE: also the previous step's lgx_ppo_store rows (env n0 + threadIdx.x), which read only that
+// step's env outputs and storage row: one launch per env step instead of two
+template <bool STORE>
 __global__ void __launch_bounds__(TPB)
-ppo_act_kernel(lgx_ppo_act_args a) {
+ppo_act_kernel(lgx_ppo_act_args a, lgx_ppo_store_args ps) {
   const int64_t n0 = (int64_t)blockIdx.x * ACT_ENVS;
   const int64_t nn = min((int64_t)ACT_ENVS, a.num_envs - n0);
+  if (STORE && threadIdx.x < nn) {
+    const int64_t n = n0 + threadIdx.x;
+    float r = ps.rew[n];
+    if (ps.time_outs) r += ps.gamma * (ps.st_values[n] * (ps.time_outs[n] ? 1.f : 0.f));
+    ps.st_rew[n] = r;
+    ps.st_dones[n] = ps.reset[n] ? 1 : 0;
+  }
   copy_rows(a.obs + n0 * a.num_obs, a.st_obs + n0 * a.num_obs, nn * a.num_obs);
   if (a.cobs && a.st_cobs) copy_rows(a.cobs + n0 * a.num_cobs, a.st_cobs + n0 * a.num_cobs, nn * a.num_cobs);
   const int A = a.num_actions;
@@ -856,23 +866,38 @@ extern "C" int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* 
   return lgx_hip_status("lgx_ppo_gather_rows");
 }
 
+static bool act_args_ok(const lgx_ppo_act_args& a) {
+  return !(a.num_envs <= 0 || a.num_actions <= 0 || a.num_obs <= 0 || !a.mu || !a.std || !a.noise || !a.obs ||
+           !a.actions_out || !a.st_obs || !a.st_actions || (a.value && !a.st_values) || !a.st_logp || !a.st_mu ||
+           !a.st_sigma || ((a.cobs != nullptr) != (a.st_cobs != nullptr)));
+}
+static bool store_args_ok(const lgx_ppo_store_args& a) {
+  return !(a.num_envs <= 0 || !a.rew || !a.reset || !a.st_values || !a.st_rew || !a.st_dones);
+}
+
 extern "C" int lgx_ppo_act(const lgx_ppo_act_args* args, void* stream) {
   if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_act: null args");
   const lgx_ppo_act_args& a = *args;
-  if (a.num_envs <= 0 || a.num_actions <= 0 || a.num_obs <= 0 || !a.mu || !a.std || !a.noise || !a.obs ||
-      !a.actions_out || !a.st_obs || !a.st_actions || (a.value && !a.st_values) || !a.st_logp || !a.st_mu || !a.st_sigma ||
-      ((a.cobs != nullptr) != (a.st_cobs != nullptr)))
-    return lgx_fail(LGX_EINVAL, "lgx_ppo_act: bad args");
-  hipLaunchKernelGGL(ppo_act_kernel, dim3((unsigned)((a.num_envs + ACT_ENVS - 1) / ACT_ENVS)), dim3(TPB), 0,
-                     LGX_STREAM(stream), a);
+  if (!act_args_ok(a)) return lgx_fail(LGX_EINVAL, "lgx_ppo_act: bad args");
+  hipLaunchKernelGGL(ppo_act_kernel<false>, dim3((unsigned)((a.num_envs + ACT_ENVS - 1) / ACT_ENVS)), dim3(TPB), 0,
+                     LGX_STREAM(stream), a, lgx_ppo_store_args{});
   return lgx_hip_status("lgx_ppo_act");
+}
+
+extern "C" int lgx_ppo_act_store(const lgx_ppo_act_args* args, const lgx_ppo_store_args* prev, void* stream) {
+  if (!args || !prev) return lgx_fail(LGX_EINVAL, "lgx_ppo_act_store: null args");
+  const lgx_ppo_act_args& a = *args;
+  if (!act_args_ok(a) || !store_args_ok(*prev) || prev->num_envs != a.num_envs)
+    return lgx_fail(LGX_EINVAL, "lgx_ppo_act_store: bad args (the store must cover the same envs)");
+  hipLaunchKernelGGL(ppo_act_kernel<true>, dim3((unsigned)((a.num_envs + ACT_ENVS - 1) / ACT_ENVS)), dim3(TPB), 0,
+                     LGX_STREAM(stream), a, *prev);
+  return lgx_hip_status("lgx_ppo_act_store");
 }
 
 extern "C" int lgx_ppo_store(const lgx_ppo_store_args* args, void* stream) {
   if (!args) return lgx_fail(LGX_EINVAL, "lgx_ppo_store: null args");
   const lgx_ppo_store_args& a = *args;
-  if (a.num_envs <= 0 || !a.rew || !a.reset || !a.st_values || !a.st_rew || !a.st_dones)
-    return lgx_fail(LGX_EINVAL, "lgx_ppo_store: bad args");
+  if (!store_args_ok(a)) return lgx_fail(LGX_EINVAL, "lgx_ppo_store: bad args");
   hipLaunchKernelGGL(ppo_store_kernel, dim3((unsigned)((a.num_envs + TPB - 1) / TPB)), dim3(TPB), 0,
                      LGX_STREAM(stream), a);
   return lgx_hip_status("lgx_ppo_store");

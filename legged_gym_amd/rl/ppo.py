@@ -54,6 +54,10 @@ class PPO:
         self.use_clipped_value_loss = use_clipped_value_loss
         self.dist = _dist()
         self._fused = None
+        # process_env_step leaves its storage-row launch to the next act (one launch per step);
+        # set by OnPolicyRunner, whose loop always calls act between env.step calls
+        self.defer_store = False
+        self._pending_store = None
         if fused and use_fused_update and FusedPPOUpdate.supported(self.actor_critic):
             self._fused = FusedPPOUpdate(self)       # parameters become views of its flat buffer
             self.optimizer = self._fused.optimizer
@@ -127,8 +131,14 @@ class PPO:
             st.values[s].data_ptr()
         a.st_logp, a.st_mu, a.st_sigma = st.actions_log_prob[s].data_ptr(), st.mu[s].data_ptr(), st.sigma[s].data_ptr()
         lib = self._fused.lib
-        self._fused.check(lib.lgx_ppo_act(C.byref(a), C.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)),
-                          "lgx_ppo_act")
+        stream = C.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
+        pend = getattr(self, "_pending_store", None)
+        if pend is not None and pend[0].num_envs == a.num_envs:   # the previous step's store rides along
+            self._pending_store = None
+            self._fused.check(lib.lgx_ppo_act_store(C.byref(a), C.byref(pend[0]), stream), "lgx_ppo_act_store")
+        else:
+            self.flush_store()
+            self._fused.check(lib.lgx_ppo_act(C.byref(a), stream), "lgx_ppo_act")
         t = self.transition
         t.actions, t.values = self._act_out, st.values[s]
         t.actions_log_prob, t.action_mean, t.action_sigma = st.actions_log_prob[s], st.mu[s], st.sigma[s]
@@ -170,8 +180,15 @@ class PPO:
                 a.time_outs = to.data_ptr()
             a.st_values, a.st_rew, a.st_dones = st.values[st.step].data_ptr(), st.rewards[st.step].data_ptr(), \
                 st.dones[st.step].data_ptr()
-            self._fused.check(self._fused.lib.lgx_ppo_store(C.byref(a), C.c_void_p(
-                torch.cuda.current_stream(rewards.device).cuda_stream)), "lgx_ppo_store")
+            if self.defer_store:
+                # launched with the next act (lgx_ppo_act_store) or by flush_store(): the env's
+                # reward / reset / time-out buffers hold this step's values until the next env.step,
+                # which the runner issues only after that act
+                self.flush_store()
+                self._pending_store = (a, rewards, dones, to)
+            else:
+                self._fused.check(self._fused.lib.lgx_ppo_store(C.byref(a), C.c_void_p(
+                    torch.cuda.current_stream(rewards.device).cuda_stream)), "lgx_ppo_store")
             st.step += 1
             t.clear()
             self.actor_critic.reset(dones)
@@ -184,6 +201,15 @@ class PPO:
         t.clear()
         self.actor_critic.reset(dones)
 
+    def flush_store(self):
+        """Launch a deferred lgx_ppo_store (defer_store) on its own."""
+        pend = getattr(self, "_pending_store", None)
+        if pend is None:
+            return
+        self._pending_store = None
+        self._fused.check(self._fused.lib.lgx_ppo_store(C.byref(pend[0]), C.c_void_p(
+            torch.cuda.current_stream(pend[1].device).cuda_stream)), "lgx_ppo_store")
+
     def _adv_stats(self, adv):
         if self.dist is None:
             return adv.mean(), adv.std()
@@ -195,6 +221,7 @@ class PPO:
         return mean, var.clamp(min=0).sqrt()
 
     def compute_returns(self, last_critic_obs):
+        self.flush_store()
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         self.storage.compute_returns(last_values, self.gamma, self.lam,
                                      reduce_stats=self._adv_stats if self.dist is not None else None)
@@ -214,6 +241,7 @@ class PPO:
     def update(self, defer=False):
         """rsl_rl PPO.update -> (mean value loss, mean surrogate loss).  defer=True (fused path only)
         issues the update and returns None; resolve() returns the losses later (FusedPPOUpdate)."""
+        self.flush_store()
         if self._fused is not None:
             out = self._fused.update(defer=defer)
             self.storage.clear()

@@ -77,6 +77,9 @@ class OnPolicyRunner:
         # synchronisation and issues again).  Same computation, same results.
         defer = cuda and self.log_dir is None
         pending = None
+        # act -> env.step -> process_env_step: each step's storage-row store rides on the next act's
+        # launch (LGX_DEFER_STORE=0: its own launch, as before)
+        self.alg.defer_store = os.environ.get("LGX_DEFER_STORE", "1") != "0"
         tot_iter = self.current_learning_iteration + num_learning_iterations
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
@@ -106,6 +109,7 @@ class OnPolicyRunner:
                 stop = time.time()
                 collection_time = stop - start
                 start = stop
+                self.alg.flush_store()           # (the last step's storage row: no act follows it)
                 self.alg.compute_returns(critic_obs)
             if pending is not None:
                 self._finish_deferred(pending)
@@ -134,6 +138,7 @@ class OnPolicyRunner:
             ep_infos.clear()
         if pending is not None:
             self._finish_deferred(pending)
+        self.alg.defer_store = False
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))

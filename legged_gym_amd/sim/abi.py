@@ -195,6 +195,7 @@ def declare(lib, prefix="lgx"):
             "ppo_gather_rows": (C.c_int, [vp, vp, vp, i64, i32, vp]),
             "ppo_act": (C.c_int, [C.POINTER(LgxPpoActArgs), vp]),
             "ppo_store": (C.c_int, [C.POINTER(LgxPpoStoreArgs), vp]),
+            "ppo_act_store": (C.c_int, [C.POINTER(LgxPpoActArgs), C.POINTER(LgxPpoStoreArgs), vp]),
             "bias_act": (C.c_int, [vp, vp, i64, i32, i32, i32, vp]),
             "ppo_loss_partials_floats": (i64, [i64, i32]),
             "ppo_loss": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp]),
@@ -238,7 +239,7 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trim
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
-            "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store",
+            "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store", "lgx_ppo_act_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
             "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward"]

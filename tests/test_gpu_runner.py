@@ -150,16 +150,20 @@ def test_runner_iteration_matches_reference_semantics(gpu, tmp_path):
         assert torch.equal(ck["model_state_dict"][k], p), k
 
 
-def test_deferred_readback_matches_synchronous_runner(gpu, tmp_path):
+@pytest.mark.parametrize("defer_store", ["1", "0"])
+def test_deferred_readback_matches_synchronous_runner(gpu, tmp_path, monkeypatch, defer_store):
     """learn() without a log directory issues each update with a deferred readback (the
     statistics are taken after the next rollout is issued); with one it reads them back at once.
     Same seeds, 3 iterations each: identical parameters, Adam moments, learning rate and final
-    iteration statistics (bitwise: the same kernels in the same order)."""
+    iteration statistics (bitwise: the same kernels in the same order).  The synchronous run keeps
+    every step's storage store in its own launch (LGX_DEFER_STORE=0); the deferred run rides it on
+    the next act's launch (lgx_ppo_act_store) or not (parametrized)."""
     from legged_gym_amd.envs.go1.go1_config import Go1RoughCfgPPO
     from legged_gym_amd.rl.runner import OnPolicyRunner
     from legged_gym_amd.utils.helpers import class_to_dict
     out = []
     for log_dir in (None, str(tmp_path)):
+        monkeypatch.setenv("LGX_DEFER_STORE", defer_store if log_dir is None else "0")
         env = make_env("go1_rough", num_envs=256, device="cuda:0", backend="lgx")
         cfg = class_to_dict(Go1RoughCfgPPO())
         cfg["runner"]["save_interval"] = 100
