@@ -357,6 +357,10 @@ typedef struct lgx_mlp_x3_desc {
 } lgx_mlp_x3_desc;
 int64_t lgx_mlp_x3_weight_elems(int32_t n_out, int32_t k_in);
 int lgx_mlp_x3_split(const float* W, int32_t n_out, int32_t k_in, uint16_t* dst, void* stream);
+/* lgx_mlp_x3_split of every layer of one network in one launch: W[l] is layer l's [dims[l+1],
+ * dims[l]] weight, dst[l] its image (lgx_mlp_x3_weight_elems(dims[l+1], dims[l]) bf16), nl <= 6. */
+int lgx_mlp_x3_split_layers(const float* const* W, const int32_t* dims, int32_t nl, uint16_t* const* dst,
+                            void* stream);
 int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* descs, int32_t count);   /* -1: unsupported */
 int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* descs, int32_t count, void* stream);
 

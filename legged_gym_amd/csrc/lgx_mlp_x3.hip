@@ -294,11 +294,26 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
 
 // weights W [n_out][k_in] (nn.Linear layout) -> fragment image [n/32][k/16][limb][32 n][16 k],
 // zero-padded to 32 n and 64 k; one thread per (n, k pair)
-__global__ void __launch_bounds__(256) xm_split_kernel(const float* __restrict__ W, int N, int K,
-                                                       uint16_t* __restrict__ dst) {
+// every layer of a network in one launch (blockIdx.y = layer): one launch per parameter version
+// and network instead of one per layer
+struct XmSplitJobs {
+  const float* W[XM_MAXL];
+  uint16_t* dst[XM_MAXL];
+  int32_t N[XM_MAXL], K[XM_MAXL];
+};
+
+__device__ __forceinline__ void xm_split_one(const float* __restrict__ W, int N, int K, uint16_t* __restrict__ dst,
+                                             int64_t i);
+
+__global__ void __launch_bounds__(256) xm_split_kernel(XmSplitJobs J) {
+  const int l = blockIdx.y;
+  xm_split_one(J.W[l], J.N[l], J.K[l], J.dst[l], (int64_t)blockIdx.x * 256 + threadIdx.x);
+}
+
+__device__ __forceinline__ void xm_split_one(const float* __restrict__ W, int N, int K, uint16_t* __restrict__ dst,
+                                             int64_t i) {
   const int KP = xm_kp(K), KB = KP / 16, pairs = KP / 2;
   const int64_t total = (int64_t)((N + 31) / 32) * 32 * pairs;
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int n = (int)(i / pairs), k = 2 * (int)(i - (int64_t)n * pairs);
   const float v0 = (n < N && k < K) ? W[(int64_t)n * K + k] : 0.f;
@@ -340,13 +355,29 @@ extern "C" int64_t lgx_mlp_x3_weight_elems(int32_t n_out, int32_t k_in) {
   return (int64_t)((n_out + 31) / 32) * (xm_kp(k_in) / 16) * 3 * 512;
 }
 
-extern "C" int lgx_mlp_x3_split(const float* W, int32_t n_out, int32_t k_in, uint16_t* dst, void* stream) {
-  if (!W || !dst || n_out <= 0 || k_in <= 0 || n_out > XM_MAXW || k_in > XM_MAXW || ((uintptr_t)dst & 3))
-    return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_split: bad args");
-  const int64_t total = (int64_t)((n_out + 31) / 32) * 32 * (xm_kp(k_in) / 2);
-  hipLaunchKernelGGL(xm_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), W, n_out, k_in, dst);
+extern "C" int lgx_mlp_x3_split_layers(const float* const* W, const int32_t* dims, int32_t nl, uint16_t* const* dst,
+                                       void* stream) {
+  if (!W || !dims || !dst || nl < 1 || nl > XM_MAXL) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_split: bad layer count");
+  XmSplitJobs J{};
+  int64_t most = 0;
+  for (int l = 0; l < nl; ++l) {
+    const int32_t k_in = dims[l], n_out = dims[l + 1];
+    if (!W[l] || !dst[l] || n_out <= 0 || k_in <= 0 || n_out > XM_MAXW || k_in > XM_MAXW || ((uintptr_t)dst[l] & 3))
+      return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_split: bad args");
+    J.W[l] = W[l];
+    J.dst[l] = dst[l];
+    J.N[l] = n_out;
+    J.K[l] = k_in;
+    most = std::max<int64_t>(most, (int64_t)((n_out + 31) / 32) * 32 * (xm_kp(k_in) / 2));
+  }
+  hipLaunchKernelGGL(xm_split_kernel, dim3((unsigned)((most + 255) / 256), (unsigned)nl), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), J);
   return lgx_hip_status("lgx_mlp_x3_split");
+}
+
+extern "C" int lgx_mlp_x3_split(const float* W, int32_t n_out, int32_t k_in, uint16_t* dst, void* stream) {
+  const int32_t dims[2] = {k_in, n_out};
+  return lgx_mlp_x3_split_layers(&W, dims, 1, &dst, stream);
 }
 
 extern "C" int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* d, int32_t count) {

@@ -107,10 +107,12 @@ class _FusedMLP:
                 if self._wl is None or self._wl[0].device != dev:
                     self._wl = [torch.empty(int(lib.lgx_mlp_x3_weight_elems(l.out_features, l.in_features)),
                                             dtype=torch.int16, device=dev) for l in self.linears]
-                for l, wl in zip(self.linears, self._wl):
-                    w = l.weight.detach().contiguous()
-                    lgxlib.check(lib.lgx_mlp_x3_split(C.c_void_p(w.data_ptr()), l.out_features, l.in_features,
-                                                      C.c_void_p(wl.data_ptr()), stream), "lgx_mlp_x3_split")
+                ws = [l.weight.detach().contiguous() for l in self.linears]   # (views of the flat buffer)
+                wp = (C.c_void_p * n)(*[w.data_ptr() for w in ws])
+                dp = (C.c_void_p * n)(*[wl.data_ptr() for wl in self._wl])
+                dims = (C.c_int32 * (n + 1))(*self.dims)
+                lgxlib.check(lib.lgx_mlp_x3_split_layers(wp, dims, n, dp, stream), "lgx_mlp_x3_split")   # one launch
+                self._split_keep = ws
                 self._ver["wl"] = ver
             if not x3 and (self._ver.get("wt") != ver or self._wt is None or self._wt[0].device != dev):
                 self._wt = [l.weight.detach().t().contiguous() for l in self.linears]
