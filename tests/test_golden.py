@@ -19,7 +19,9 @@ import torch
 from oracle_backend import load_oracle, make_env, vp
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = {"go1_flat": "go1", "go1_rough": "go1_rough", "anymal_c_rough": "anymal_c_rough"}
+CASES = {"go1_flat": "go1", "go1_rough": "go1_rough", "anymal_c_rough": "anymal_c_rough",
+         # 24 envs x 36 steps on other seeds / terrain draws (the short cases: 12-24 envs x 12-24)
+         "go1_rough_long": "go1_rough", "anymal_c_rough_long": "anymal_c_rough"}
 
 
 def load(name):

@@ -480,10 +480,14 @@ def anymal_rough():
 
 
 if __name__ == "__main__":
-    cases = sys.argv[1:] or ["go1_flat", "go1_rough", "anymal_c_rough"]
+    cases = sys.argv[1:] or ["go1_flat", "go1_rough", "anymal_c_rough", "go1_rough_long", "anymal_c_rough_long"]
     if "go1_flat" in cases:
         run_case("go1_flat", "Go1", go1_flat, 24, 24, 1, "go1_model.json")
     if "go1_rough" in cases:
         run_case("go1_rough", "Go1", go1_rough, 12, 12, 2, "go1_model.json")
     if "anymal_c_rough" in cases:
         run_case("anymal_c_rough", "Anymal", anymal_rough, 12, 12, 3, "anymal_c_model.json")
+    if "go1_rough_long" in cases:   # a longer horizon on another seed / terrain draw
+        run_case("go1_rough_long", "Go1", go1_rough, 24, 36, 4, "go1_model.json")
+    if "anymal_c_rough_long" in cases:
+        run_case("anymal_c_rough_long", "Anymal", anymal_rough, 24, 36, 5, "anymal_c_model.json")
