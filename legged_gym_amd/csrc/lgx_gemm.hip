@@ -250,10 +250,21 @@ __global__ void __launch_bounds__(256) gather_rows_padded_kernel(const float* __
   const float* s = src + idx[r] * width;
   const int64_t dr = dup > 0 ? (r / dup) * 2 * dup + r % dup : r;
   float* d = dst + dr * dst_ld;
-  for (int c = lane; c < dst_ld; c += 64) {
-    const float v = c < width ? s[c] : 0.f;
-    d[c] = v;
-    if (dup > 0) d[dup * dst_ld + c] = v;
+  // four loads in flight per lane from clamped (always valid) columns, then the predicated stores
+  // (a load under `c < width` compiled to one exposed round trip per column group)
+  for (int c0 = 0; c0 < dst_ld; c0 += 256) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = s[min(c0 + 64 * i + lane, width - 1)];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = c0 + 64 * i + lane;
+      const float x = c < width ? v[i] : 0.f;
+      if (c < dst_ld) {
+        d[c] = x;
+        if (dup > 0) d[dup * dst_ld + c] = x;
+      }
+    }
   }
 }
 }  // namespace

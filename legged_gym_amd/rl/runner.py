@@ -76,16 +76,19 @@ class OnPolicyRunner:
         # (otherwise it idles ~0.3 ms per iteration while the host returns from the update's
         # synchronisation and issues again).  Same computation, same results.
         defer = cuda and self.log_dir is None
-        pending = None
+        pending = prev_end = None
         # act -> env.step -> process_env_step: each step's storage-row store rides on the next act's
         # launch (LGX_DEFER_STORE=0: its own launch, as before)
         self.alg.defer_store = os.environ.get("LGX_DEFER_STORE", "1") != "0"
         tot_iter = self.current_learning_iteration + num_learning_iterations
         for it in range(self.current_learning_iteration, tot_iter):
             start = time.time()
-            if cuda:
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-                ev[0].record()
+            if cuda:   # (the previous iteration's end event is this one's start: one marker less)
+                ev = [prev_end if prev_end is not None else torch.cuda.Event(enable_timing=True)] + \
+                     [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                if prev_end is None:
+                    ev[0].record()
+                prev_end = ev[2] if defer else None   # (synchronous runs: host logging lies between)
             with torch.inference_mode():
                 for _ in range(self.num_steps_per_env):
                     actions = self.alg.act(obs, critic_obs)
