@@ -152,6 +152,7 @@ class PPO:
             actions = self._act_fused(obs, critic_obs)
             if actions is not None:
                 return actions
+        self.flush_store()   # (a deferred store reads the env's buffers before the next env.step)
         if hasattr(self.actor_critic, "act_and_evaluate"):
             actions, values = self.actor_critic.act_and_evaluate(obs, critic_obs)
             t.actions, t.values = actions.detach(), values.detach()
