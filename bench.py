@@ -40,7 +40,7 @@ def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
 
 
 PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
-PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc_ppo_kernels.json")
+PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_ppo_kernels.json")
 MI355X_BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PRODUCTS = 6                  # split-bf16: six bf16 limb products per f32 product (lgx_gemm_split.hip)
 

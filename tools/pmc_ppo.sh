@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic PMC passes (FETCH_SIZE, WRITE_SIZE; one counter group per rocprofv3 --pmc pass,
 # --kernel-trace only) over one bench.py iteration: the PPO-update kernels (lgx_gemm_nt, loss,
-# reductions) in situ -> profiles/r02_pmc_ppo_kernels.json (read by bench.py's roofline).
+# reductions) in situ -> profiles/r03_pmc_ppo_kernels.json (read by bench.py's roofline).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
 export TMPDIR=/tmp
