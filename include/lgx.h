@@ -357,8 +357,9 @@ typedef struct lgx_mlp_x3_desc {
 } lgx_mlp_x3_desc;
 int64_t lgx_mlp_x3_weight_elems(int32_t n_out, int32_t k_in);
 int lgx_mlp_x3_split(const float* W, int32_t n_out, int32_t k_in, uint16_t* dst, void* stream);
-/* lgx_mlp_x3_split of every layer of one network in one launch: W[l] is layer l's [dims[l+1],
- * dims[l]] weight, dst[l] its image (lgx_mlp_x3_weight_elems(dims[l+1], dims[l]) bf16), nl <= 6. */
+/* lgx_mlp_x3_split of every layer of one network in one launch (the rsl_rl ActorCritic MLP's
+ * weights after an optimizer step): W[l] is layer l's [dims[l+1], dims[l]] weight, dst[l] its image
+ * (lgx_mlp_x3_weight_elems(dims[l+1], dims[l]) bf16), nl <= 6. */
 int lgx_mlp_x3_split_layers(const float* const* W, const int32_t* dims, int32_t nl, uint16_t* const* dst,
                             void* stream);
 int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* descs, int32_t count);   /* -1: unsupported */
@@ -379,8 +380,9 @@ int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
 int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_values, float* returns,
             float* advantages, int32_t T, int32_t N, float gamma, float lam, void* stream);
 
-/* lgx_gae followed by rsl_rl's advantage normalisation (single process: rl/storage.py
- * compute_returns, `(adv - adv.mean()) / (adv.std() + 1e-8)`, unbiased std) in place - two
+/* lgx_gae followed by the advantage normalisation of rsl_rl v1.0.x RolloutStorage.compute_returns
+ * (external to the reference; called from on_policy_runner.learn, which scripts/train.py:43 runs):
+ * `(adv - adv.mean()) / (adv.std() + 1e-8)`, unbiased std, in place (single process) - two
  * launches instead of the GAE kernel + the torch mean / std / elementwise chain.  scratch:
  * lgx_gae_norm_scratch(N) doubles of device memory (per-workgroup sums, fixed order). */
 int64_t lgx_gae_norm_scratch(int32_t N);
@@ -429,8 +431,9 @@ typedef struct lgx_ppo_store_args {
   uint8_t* st_dones;
 } lgx_ppo_store_args;
 int lgx_ppo_store(const lgx_ppo_store_args* args, void* stream);
-/* lgx_ppo_act of step t+1 and the deferred lgx_ppo_store of step t in ONE launch (the store reads
- * only step t's env outputs and storage row t, which the act does not touch); same envs. */
+/* lgx_ppo_act of step t+1 and the deferred lgx_ppo_store of step t in ONE launch (rsl_rl
+ * PPO.act + PPO.process_env_step of the runner's collection loop; the store reads only step t's
+ * env outputs and storage row t, which the act does not touch); same envs. */
 int lgx_ppo_act_store(const lgx_ppo_act_args* args, const lgx_ppo_store_args* prev, void* stream);
 
 /* dst[r, :] = src[idx[r], :] for r < rows (minibatch gather of storage rows) */
