@@ -415,7 +415,11 @@ head_bwd_kernel(const float* __restrict__ d_mu, const float* __restrict__ d_v, c
 //      head_in in place, dW4 and db3 partials per workgroup (head_bwd_kernel's layout).
 // The loss finalize (d std, head-bias gradients, KL, stats, adaptive LR) runs later on one extra
 // workgroup of lgx_reduce_slices_finalize (it needs every workgroup's partials).
-constexpr int LB_ROWS = 32;
+#ifndef LGX_LB_ROWS
+#define LGX_LB_ROWS 32
+#endif
+constexpr int LB_ROWS = LGX_LB_ROWS;   // rows per workgroup (16 or 32: TPB / LB_ROWS lanes per row)
+static_assert(LB_ROWS == 16 || LB_ROWS == 32, "lanes per row must divide a wave");
 constexpr int LB_LPR = TPB / LB_ROWS;   // lanes per row in phases 1-2 (8)
 
 __device__ __forceinline__ float lb_rowsum(float v) {   // sum over the LB_LPR lanes of a row
