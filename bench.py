@@ -244,6 +244,32 @@ def cpu_baseline(task, n_envs):
                 runs=runs, host=info)
 
 
+def isolated_tn(fused, torch, reps=20):
+    """(algorithmic FLOP, ms, launches) of the update's dW launches (lgx_gemm_tn with the last
+    minibatch's arguments) run alone on the current stream after the timed region."""
+    import ctypes as C
+    dw = getattr(fused, "gemm_dw", None)
+    if not dw:
+        return None
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    flop = ms = 0.0
+    n = 0
+    for k in sorted(dw):
+        for t in dw[k]:
+            for _ in range(3):
+                fused.check(fused.lib.lgx_gemm_tn(C.byref(t), stream), "gemm_tn")
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                fused.check(fused.lib.lgx_gemm_tn(C.byref(t), stream), "gemm_tn")
+            e1.record()
+            e1.synchronize()
+            ms += e0.elapsed_time(e1)
+            n += reps
+            flop += reps * 2.0 * t.M * t.R * t.Cc * t.batch
+    return flop, ms, n
+
+
 def standalone_actuator_ms(lib, env, torch, launches=50):
     """Average duration of the standalone actuator-net launch over the env's current model_ins."""
     stream = torch.cuda.current_stream()
@@ -409,6 +435,14 @@ def main():
             gemm_roofs[-1]["concurrent"] = True
             gemm_roofs[-1]["note"] += ("; launched on a second stream concurrently with the dA GEMMs: durations "
                                        "are co-resident times (the CUs are shared), not the isolated kernel rate")
+            iso = isolated_tn(fused, torch)
+            if iso:
+                f_iso, ms_iso, n_iso = iso
+                gemm_roofs[-1]["isolated"] = {
+                    "achieved": f_iso / (ms_iso * 1e-3) / 1e12, "frac": f_iso / (ms_iso * 1e-3) / 1e12 / peak,
+                    "avg_ms": ms_iso / n_iso, "launches": n_iso,
+                    "note": "the same dW launches (last minibatch's arguments) alone on the main stream after the "
+                            "timed region, HIP events; the kernel's own rate without the co-resident dA GEMMs"}
     kernels = {n: {"avg_ms": round(a, 4), "launches_timed": int(c),
                    "share_of_iteration": round(a * steps_per_iter / it_ms, 4) if c else None}
                for n, a, c in zip(names, avg, cnt)}
