@@ -1,13 +1,8 @@
 #!/bin/bash
-# Same-box A/B of whole-iteration throughput: HEAD vs an older tree copied under build/old_tree.
+# Round-end rehearsal: smoke(), then tests / bench / rocprof (tools/gpu_round.sh).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
 mkdir -p gpurun_out
-ROOT=$PWD
-for r in 1 2 3; do
-  for v in head old; do
-    if [ $v = old ]; then cd $ROOT/build/old_tree; else cd $ROOT; fi
-    timeout -k 10 300 python bench.py --no_cpu_baseline > $ROOT/gpurun_out/ab_$v.json 2> $ROOT/gpurun_out/ab_$v.err || { echo "$v failed"; tail -5 $ROOT/gpurun_out/ab_$v.err; exit 1; }
-    echo "$v: $(grep -o '"ms_per_step": [0-9.]*' $ROOT/gpurun_out/ab_$v.json) $(grep -o '"collection_time": [0-9.]*' $ROOT/gpurun_out/ab_$v.json) $(grep -o '"learn_time": [0-9.]*' $ROOT/gpurun_out/ab_$v.json)"
-  done
-done
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+bash tools/gpu_round.sh all
