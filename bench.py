@@ -141,7 +141,7 @@ def parse():
     p.add_argument("--task", default="go1_rough")
     p.add_argument("--num_envs", type=int, default=4096)
     p.add_argument("--no_cpu_baseline", action="store_true")
-    p.add_argument("--cpu_envs", type=int, default=1024)
+    p.add_argument("--cpu_envs", type=int, default=4096)
     p.add_argument("--actuator_net_torques", action="store_true",
                    help="ANYmal: the SEA actuator network as the torque source (cfg.control.explicit_torques)")
     return p.parse_args()
@@ -212,7 +212,7 @@ def _cpu_iteration(task, n_envs, steps_per_env, threads):
 CPU_RUNS = [  # (label, task, envs, steps per env at full share, steps per env at 1 thread)
     ("C1", "go1_flat_bench", 64, 24, 24),
     ("C2", "go1_flat_bench", 4096, 24, 2),
-    ("C3", "go1_rough", 1024, 24, 4),
+    ("C3", "go1_rough", 4096, 24, 1),
 ]
 
 
@@ -291,8 +291,48 @@ def standalone_actuator_ms(lib, env, torch, launches=50):
     return s.elapsed_time(e) / launches, launches
 
 
+def param_fingerprint(flat, torch):
+    """Exact integer fingerprint of a float32 parameter vector: sum of its bit patterns x (index
+    mod 1021 + 1), in int64 (no overflow below 4e6 parameters) - equal on two ranks iff their
+    parameters are bitwise equal (up to a collision of this weighted sum)."""
+    bits = flat.detach().contiguous().view(torch.int32).to(torch.int64)
+    w = torch.arange(bits.numel(), device=bits.device, dtype=torch.int64) % 1021 + 1
+    return (bits * w).sum()
+
+
+def data_parallel_check(runner, fused, comm_t, world, backend, device, dist):
+    """After the timed region: what a multi-GPU run has to prove from its own JSON line - the ranks
+    that took part, that every rank ends with bitwise identical parameters (fingerprint MAX - MIN
+    over ranks == 0), whether the two-bucket gradient all-reduce ran (FusedPPOUpdate.bucketed), and
+    the event-timed all-reduce time per iteration (the timed minibatches, scaled)."""
+    import torch
+    alg = runner.alg
+    flat = fused.flat_p if fused is not None else torch.cat([p.detach().reshape(-1) for p in alg.actor_critic.parameters()])
+    fp = param_fingerprint(flat, torch).view(1)
+    out = {"world": world, "backend": backend, "param_fingerprint": int(fp.item())}
+    if world > 1:
+        hi, lo, ranks = fp.clone(), fp.clone(), torch.ones(1, dtype=torch.int64, device=device)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(ranks)
+        out.update(ranks_seen=int(ranks.item()), param_fingerprint_spread=int((hi - lo).item()),
+                   params_identical_across_ranks=bool((hi == lo).item()))
+    if fused is not None:
+        out["bucketed_allreduce"] = bool(fused.bucketed)
+        n, ms, nbytes, mbs = comm_t
+        mb_per_iter = alg.num_learning_epochs * alg.num_mini_batches
+        out["allreduce"] = {"collectives_timed": n, "bytes_per_minibatch": (nbytes / mbs) if mbs else 0,
+                            "ms_per_iteration": (ms / mbs * mb_per_iter) if mbs else 0.0,
+                            "note": "HIP events around every gradient all-reduce of every k-th minibatch "
+                                    "(LGX_BENCH_GEMM_TIMING), on the stream it is issued from"}
+    return out
+
+
 def main():
     args = parse()
+    if args.actuator_net_torques and not args.task.startswith("anymal"):
+        raise SystemExit("--actuator_net_torques: the SEA actuator network is ANYmal's (anymal.py:71-78); "
+                         f"task {args.task} has no actuator-net torque source")
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -328,6 +368,11 @@ def main():
     cli = get_args(["--sim_device", device, "--rl_device", device, "--headless", "--task", args.task])
     env, _ = task_registry.make_env(args.task, args=cli, env_cfg=env_cfg)
     runner, _ = task_registry.make_alg_runner(env, name=args.task, args=cli, train_cfg=train_cfg, log_root=None)
+    from legged_gym_amd.sim import abi
+    ctrl = {v: k for k, v in abi.CTRL.items()}.get(env._control_type(), "?")
+    if args.actuator_net_torques and ctrl != "SEA":
+        raise SystemExit(f"--actuator_net_torques: {args.task} resolved control type {ctrl}, not the SEA network "
+                         "(needs cfg.control.use_actuator_network)")
     lib = lgxlib.load()
     handle = env._backend.handle
 
@@ -351,6 +396,7 @@ def main():
     gc.enable()
     lib.lgx_profile_enable(handle, 0)
     gemm_t = fused.gemm_timings() if fused is not None else {}
+    comm_t = fused.comm_timings() if fused is not None else None
     if fused is not None:
         fused.time_gemms(0)
     ms = (C.c_double * 3)()
@@ -360,6 +406,7 @@ def main():
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+    data_parallel = data_parallel_check(runner, fused, comm_t, world, backend if world > 1 else None, device, dist)
     N = args.num_envs
     steps_per_iter = runner.num_steps_per_env
     value = steps_per_iter * N * world * args.steps / elapsed
@@ -388,7 +435,7 @@ def main():
     decim = env.cfg.control.decimation
     phys_flop = N * decim * physics_flop_per_env_substep(
         env._lgx_model.num_points, 4.0, env.cfg.terrain.mesh_type in ("heightfield", "trimesh"))
-    roof = {"kernel": names[0], "bound": "mfma", "compute_pipe": "fp32 VALU",
+    roof = {"kernel": names[0], "bound": "valu", "compute_pipe": "fp32 VALU",
             "achieved": (phys_flop / (avg[0] * 1e-3) / 1e12) if avg[0] else None,
             "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
             "traffic": PHYS_PMC_TRAFFIC_BYTES if (N == 4096 and args.task == "go1_rough") else None,
@@ -463,7 +510,7 @@ def main():
         "ms_per_step": it_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (procedural curriculum terrain, random-init policy)",
         "config": {"workload": WORKLOADS.get(args.task, args.task) +
-                               (", SEA actuator-net torques" if args.actuator_net_torques else "") +
+                               (", SEA actuator-net torques" if ctrl == "SEA" else "") +
                                f", PPO {steps_per_iter} steps x {N} envs/GPU, "
                                f"{runner.alg.num_learning_epochs} epochs x {runner.alg.num_mini_batches} minibatches",
                    "envs_per_gpu": N, "global_envs": N * world, "parallelism": f"dp{world}"},
@@ -474,6 +521,7 @@ def main():
         "dominant_lgx_kernel": roof["kernel"],
         "lgx_kernels": kernels,
         "last_iteration": runner.last_iteration_stats,
+        "data_parallel": data_parallel,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -281,10 +281,13 @@ int lgx_simulate(lgx_sim* sim, int32_t n, void* stream);
 
 /* The drive inputs of lgx_step's physics launch with the dynamics frozen: clip the actions
  * (`actions`, or the bound buffer when NULL) into the bound actions buffer, the position targets
- * (_compute_poses, legged_robot.py:394-397) into dof_targets, and `decimation` substeps of the Go1
- * actuator-net history (go1.py:79-98) into act_hist / model_ins, all from the CURRENT dof state,
- * which stays unchanged (as the reference's decimation loop sees it when the physics does not move:
- * the golden replay).  Same device code as the physics launch's load stage. */
+ * (_compute_poses, legged_robot.py:394-397) into dof_targets, `decimation` substeps of the Go1
+ * actuator-net history (go1.py:79-98) into act_hist / model_ins, and with LGX_CTRL_SEA
+ * `decimation` steps of the SEA LSTM (anymal.py:71-77: sea_h / sea_c advanced, the last substep's
+ * torques, clamped to the effort limit, into torques), all from the CURRENT dof state, which stays
+ * unchanged (as the reference's decimation loop sees it when the physics does not move: the golden
+ * replay).  The actuator-network state (history, LSTM) advances as in that loop; the physical
+ * state (root, dof, contacts) does not.  Same device code as the physics launch's load stage. */
 int lgx_drive_inputs(lgx_sim* sim, const float* actions, void* stream);
 
 /* The physics launch's ground query for a batch of world points (tests, tools): points [n, 4] =
@@ -384,7 +387,8 @@ int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, con
  * (external to the reference; called from on_policy_runner.learn, which scripts/train.py:43 runs):
  * `(adv - adv.mean()) / (adv.std() + 1e-8)`, unbiased std, in place (single process) - two
  * launches instead of the GAE kernel + the torch mean / std / elementwise chain.  scratch:
- * lgx_gae_norm_scratch(N) doubles of device memory (per-workgroup sums, fixed order). */
+ * lgx_gae_norm_scratch(N) doubles of device memory (per-workgroup count / mean / M2, combined in a
+ * fixed order with Chan's pairwise formula: no cancellation when |mean| >> std). */
 int64_t lgx_gae_norm_scratch(int32_t N);
 int lgx_gae_norm(const float* rewards, const float* values, const uint8_t* dones, const float* last_values,
                  float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam, double* scratch,

@@ -403,7 +403,7 @@ int lgx_gae(const float* rewards, const float* values, const uint8_t* dones, con
                       "lgx_gae: launch (T, N must be > 0)");
 }
 
-int64_t lgx_gae_norm_scratch(int32_t N) { return N > 0 ? 2 * (int64_t)((N + 255) / 256) : -1; }
+int64_t lgx_gae_norm_scratch(int32_t N) { return N > 0 ? 3 * (int64_t)((N + 255) / 256) : -1; }
 
 int lgx_gae_norm(const float* rewards, const float* values, const uint8_t* dones, const float* last_values,
                  float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam, double* scratch,

@@ -187,6 +187,17 @@ LGX_DEV void reset_env(const lgx_env_params* __restrict__ P, const lgx_buffers& 
   resample_cmd(P, D, e, LGX_DRAW_RESET_CMD, step, tag, cmd);
   for (int j = 0; j < 12; ++j) { B.last_actions[(int64_t)e * 12 + j] = 0.f; B.last_dof_vel[(int64_t)e * 12 + j] = 0.f; }
   for (int f = 0; f < 4; ++f) B.feet_air_time[(int64_t)e * 4 + f] = 0.f;
+  if (B.sea_h && B.sea_c) {   // Anymal.reset_idx zeroes the SEA LSTM state (anymal.py:56-60)
+    const int64_t m = (int64_t)P->num_envs * 12;
+    float4* h = reinterpret_cast<float4*>(B.sea_h);
+    float4* c = reinterpret_cast<float4*>(B.sea_c);
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int L = 0; L < 2; ++L)
+      for (int i = 0; i < 24; ++i) {
+        h[((int64_t)L * m + (int64_t)e * 12) * 2 + i] = z;
+        c[((int64_t)L * m + (int64_t)e * 12) * 2 + i] = z;
+      }
+  }
   B.episode_length[e] = 0;
   B.reset[e] = 1;
 }

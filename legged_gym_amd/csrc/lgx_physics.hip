@@ -229,13 +229,14 @@ LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon,
 // One step of the ANYmal SEA actuator network for joint row r of m (anymal.py:71-78; upstream
 // LSTMsea.forward): x = [a*s + q0 - q, qd] * in_scale -> 2-layer LSTM(2 -> 8) -> Linear(8 -> 1) *
 // out_scale; torch gate order i, f, g, o.  Hidden / cell state in place in global memory ([2, m, 8]:
-// the reference's sea_hidden_state layout, L2-resident across the substeps); `zero`: start from the
-// zero state (reset); `store`: write the new state (false for padding lanes).  Weights are uniform
+// the reference's sea_hidden_state layout, L2-resident across the substeps; zeroed for envs that
+// reset by the post-physics reset_env, anymal.py:56-60); `store`: write the new state (false for
+// padding lanes).  Weights are uniform
 // (scalar loads).  Sigmoid 1/(1+exp(-x)) and tanh 1 - 2/(exp(2x)+1) on v_exp_f32 (|err| <= ~2e-7).
 LGX_DEV float sea_sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 LGX_DEV float sea_tanh(float x) { return 1.f - 2.f / (__expf(2.f * x) + 1.f); }
 LGX_DEV float sea_lstm(const float* __restrict__ w, float* __restrict__ h, float* __restrict__ c, int64_t r,
-                       int64_t m, float x0, float x1, bool zero, bool store) {
+                       int64_t m, float x0, float x1, bool store) {
   const float* Wl = w + 3 + 64 + 256 + 32 + 32 + 256 + 256 + 32 + 32;
   float inp[8] = {x0 * w[0], x1 * w[1], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -248,7 +249,6 @@ LGX_DEV float sea_lstm(const float* __restrict__ w, float* __restrict__ h, float
     float4* hp = reinterpret_cast<float4*>(h + ((int64_t)L * m + r) * 8);
     float4* cp = reinterpret_cast<float4*>(c + ((int64_t)L * m + r) * 8);
     float4 h0 = hp[0], h1 = hp[1], c0 = cp[0], c1 = cp[1];
-    if (zero) h0 = h1 = c0 = c1 = make_float4(0.f, 0.f, 0.f, 0.f);
     const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
     float cv[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
     float g[32];
@@ -790,7 +790,6 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       constexpr int PASSES = (3 + PP - 1) / PP;
       float mine[PASSES];
       const int64_t m = (int64_t)N * 12;
-      const bool fresh = s == 0 && B.episode_length[ec] == 0;
 #pragma unroll
       for (int q = 0; q < PASSES; ++q) {
         const int kk = pl + q * PP;
@@ -800,7 +799,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         const float qd = k == 0 ? thd[0] : (k == 1 ? thd[1] : thd[2]);
         const int j = 3 * leg + k;
         mine[q] = sea_lstm(B.sea_w, B.sea_h, B.sea_c, (int64_t)ec * 12 + j, m,
-                           a * P->action_scale + P->default_dof_pos[j] - qq, qd, fresh, valid && kk < 3);
+                           a * P->action_scale + P->default_dof_pos[j] - qq, qd, valid && kk < 3);
       }
       const int base = (threadIdx.x & 63) - 4 * pl;   // this leg's lane p = 0 in the wave
 #pragma unroll
@@ -823,8 +822,12 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     }
     LGX_CLK(0);
     // frozen (lgx_drive_inputs): the drive inputs above - clipped actions, targets, actuator-net
-    // history / model_ins rows - with the state held fixed, no dynamics (uniform branch)
-    if (frozen) continue;
+    // history / model_ins rows, SEA LSTM state and torques - with the physical state held fixed,
+    // no dynamics (uniform branch)
+    if (frozen) {
+      if (ctrl == LGX_CTRL_SEA) { tq[0] = tex[0]; tq[1] = tex[1]; tq[2] = tex[2]; }
+      continue;
+    }
     // ---- kinematics
     m33 R0 = quat_to_mat(qx, qy, qz, qw);
     m33 Rb[3];
@@ -1261,6 +1264,10 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
       float* h = B.act_hist + (int64_t)e * 120 + leg * 30;
 #pragma unroll
       for (int i = 0; i < 30; i += 2) *reinterpret_cast<float2*>(h + i) = make_float2(hist[i], hist[i + 1]);
+    }
+    if (ctrl == LGX_CTRL_SEA && from_actions && nsub > 0) {   // the last substep's network torques
+      float* tqo = B.torques + (int64_t)e * 12 + leg * 3;
+      tqo[0] = tq[0]; tqo[1] = tq[1]; tqo[2] = tq[2];
     }
     return;
   }

@@ -6,15 +6,28 @@
 
 #include <algorithm>
 
-// part != nullptr: each workgroup also writes the sum and the sum of squares of its advantages
-// (double, fixed reduction order) to part[2 * blockIdx.x ...] for lgx_adv_norm_kernel
+// Chan et al.'s pairwise combination of (count, mean, M2) summaries (M2 = sum of squared
+// deviations from the mean): no cancellation when |mean| >> std, unlike sum / sum-of-squares
+struct MomentSummary {
+  double n, mean, m2;
+};
+LGX_DEV MomentSummary moments_combine(MomentSummary a, MomentSummary b) {
+  const double n = a.n + b.n;
+  if (n == 0.0) return a;
+  const double d = b.mean - a.mean;
+  return {n, a.mean + d * (b.n / n), a.m2 + b.m2 + d * d * (a.n * b.n / n)};
+}
+
+// part != nullptr: each workgroup also writes the (count, mean, M2) of its advantages (double,
+// Welford per thread over its T steps, then a fixed-order Chan tree) to part[3 * blockIdx.x ...]
+// for lgx_adv_norm_kernel
 __global__ void __launch_bounds__(256) lgx_gae_kernel(const float* __restrict__ rew, const float* __restrict__ val,
                                                       const uint8_t* __restrict__ dones,
                                                       const float* __restrict__ last_val, float* __restrict__ ret,
                                                       float* __restrict__ adv, int32_t T, int32_t N, float gamma,
                                                       float lam, double* __restrict__ part) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  double s = 0.0, q = 0.0;
+  MomentSummary ms = {0.0, 0.0, 0.0};
   if (e < N) {
     float next_v = last_val[e];
     float a = 0.f;
@@ -28,44 +41,39 @@ __global__ void __launch_bounds__(256) lgx_gae_kernel(const float* __restrict__ 
       ret[i] = r;
       const float d = r - v;
       adv[i] = d;
-      s += d;
-      q += (double)d * d;
+      ms.n += 1.0;                       // Welford
+      const double dd = (double)d - ms.mean;
+      ms.mean += dd / ms.n;
+      ms.m2 += dd * ((double)d - ms.mean);
       next_v = v;
     }
   }
   if (!part) return;
-  __shared__ double rs[256], rq[256];
-  rs[threadIdx.x] = s;
-  rq[threadIdx.x] = q;
+  __shared__ MomentSummary rs[256];
+  rs[threadIdx.x] = ms;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      rs[threadIdx.x] += rs[threadIdx.x + w];
-      rq[threadIdx.x] += rq[threadIdx.x + w];
-    }
+    if ((int)threadIdx.x < w) rs[threadIdx.x] = moments_combine(rs[threadIdx.x], rs[threadIdx.x + w]);
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = rs[0];
-    part[2 * blockIdx.x + 1] = rq[0];
+    part[3 * blockIdx.x] = rs[0].n;
+    part[3 * blockIdx.x + 1] = rs[0].mean;
+    part[3 * blockIdx.x + 2] = rs[0].m2;
   }
 }
 
 // rsl_rl's advantage normalisation, (adv - adv.mean()) / (adv.std() + 1e-8) with the unbiased
-// std, in place: every workgroup re-reduces the GAE partials in the same order (double), then
+// std, in place: every workgroup re-combines the GAE summaries in the same order (double), then
 // normalises its slice in f32 as torch does from the f32 mean / std
 __global__ void __launch_bounds__(256) lgx_adv_norm_kernel(float* __restrict__ adv, int64_t n,
                                                            const double* __restrict__ part, int32_t nparts) {
   __shared__ float ms[2];
   if (threadIdx.x == 0) {
-    double s = 0.0, q = 0.0;
-    for (int i = 0; i < nparts; ++i) {
-      s += part[2 * i];
-      q += part[2 * i + 1];
-    }
-    const double mean = s / (double)n;
-    const double var = n > 1 ? fmax((q - (double)n * mean * mean) / (double)(n - 1), 0.0) : 0.0;
-    ms[0] = (float)mean;
+    MomentSummary s = {0.0, 0.0, 0.0};
+    for (int i = 0; i < nparts; ++i) s = moments_combine(s, {part[3 * i], part[3 * i + 1], part[3 * i + 2]});
+    const double var = n > 1 ? s.m2 / (double)(n - 1) : 0.0;
+    ms[0] = (float)s.mean;
     ms[1] = (float)sqrt(var) + 1e-8f;
   }
   __syncthreads();

@@ -673,8 +673,31 @@ class FusedPPOUpdate:
     # ------------------------------------------------------------------ GEMM timing (bench.py)
     def time_gemms(self, period):
         """Bracket every lgx_gemm_nt launch of every `period`-th minibatch with HIP events on the
-        launch stream (0: off); gemm_timings() reads them back per epilogue (kernel instantiation)."""
+        launch stream (0: off); gemm_timings() reads them back per epilogue (kernel instantiation).
+        The data-parallel gradient all-reduces of those minibatches are bracketed too
+        (comm_timings())."""
         self._t_period, self._t_count, self._t_events, self._t_mb = int(period), 0, [], 0
+        self._c_events = []
+
+    def _all_reduce(self, buf, torch_stream):
+        """ppo.dist.all_reduce(buf) issued on `torch_stream` (the current stream), with HIP events
+        around it on that stream when this minibatch is timed."""
+        rec = getattr(self, "_t_period", 0) and self._t_count % self._t_period == 0
+        if rec:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(torch_stream)
+        self.ppo.dist.all_reduce(buf)
+        if rec:
+            e1.record(torch_stream)
+            self._c_events.append((buf.numel() * buf.element_size(), e0, e1))
+
+    def comm_timings(self):
+        """(collectives timed, total ms, total bytes, timed minibatches) of the all-reduces of the
+        timed minibatches."""
+        torch.cuda.synchronize()
+        ev = getattr(self, "_c_events", [])
+        return (len(ev), sum(e0.elapsed_time(e1) for _, e0, e1 in ev), sum(b for b, _, _ in ev),
+                getattr(self, "_t_mb", 0))
 
     def _gemm(self, g, stream):
         rec = getattr(self, "_t_period", 0) and self._t_count % self._t_period == 0
@@ -845,7 +868,7 @@ class FusedPPOUpdate:
             # communicator: the collectives run in issue order on every rank)
             with torch.cuda.stream(self._side):
                 self.g_comm[self.n:].copy_(self.stats[0:1])
-                ppo.dist.all_reduce(self.g_comm[self.nW1:])
+                self._all_reduce(self.g_comm[self.nW1:], self._side)
         if 0 in self.gemm_dw and fused:     # lgx_gemm_tn over the minibatch's padded input rows
             t = self.gemm_dw[0]
             t[0].B = xp.data_ptr()
@@ -865,7 +888,7 @@ class FusedPPOUpdate:
         if early:   # (dW1's partials come from this stream; the side stream's blocks are joined below)
             chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
             if bucketed:
-                ppo.dist.all_reduce(self.g_comm[:self.nW1])
+                self._all_reduce(self.g_comm[:self.nW1], torch.cuda.current_stream(self.dev))
             self._ev_out.record(self._side)
             torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
         elif self.loss_bwd:
@@ -881,7 +904,7 @@ class FusedPPOUpdate:
             # above, or one collective here
             if not bucketed:
                 self.g_comm[self.n:].copy_(self.stats[0:1])
-                ppo.dist.all_reduce(self.g_comm)
+                self._all_reduce(self.g_comm, torch.cuda.current_stream(self.dev))
             grad_scale = 1.0 / ppo.dist.get_world_size()
             if adaptive:
                 chk(lib.lgx_ppo_adapt_lr(C.c_void_p(self.g_comm.data_ptr() + 4 * self.n), grad_scale,

@@ -81,67 +81,74 @@ class OnPolicyRunner:
         # launch (LGX_DEFER_STORE=0: its own launch, as before)
         self.alg.defer_store = os.environ.get("LGX_DEFER_STORE", "1") != "0"
         tot_iter = self.current_learning_iteration + num_learning_iterations
-        for it in range(self.current_learning_iteration, tot_iter):
-            start = time.time()
-            if cuda:   # (the previous iteration's end event is this one's start: one marker less)
-                ev = [prev_end if prev_end is not None else torch.cuda.Event(enable_timing=True)] + \
-                     [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                if prev_end is None:
-                    ev[0].record()
-                prev_end = ev[2] if defer else None   # (synchronous runs: host logging lies between)
-            with torch.inference_mode():
-                for _ in range(self.num_steps_per_env):
-                    actions = self.alg.act(obs, critic_obs)
-                    obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
-                    critic_obs = privileged_obs if privileged_obs is not None else obs
-                    obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
-                    rewards, dones = rewards.to(self.device), dones.to(self.device)
-                    self.alg.process_env_step(rewards, dones, infos)
-                    if self.log_dir is not None:
-                        if "episode" in infos:
-                            ep_infos.append(infos["episode"])
-                        cur_reward_sum += rewards
-                        cur_episode_length += 1
-                        new_ids = (dones > 0).nonzero(as_tuple=False)
-                        rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
-                        lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
-                        cur_reward_sum[new_ids] = 0
-                        cur_episode_length[new_ids] = 0
-                if cuda:
-                    ev[1].record()
+        try:
+            for it in range(self.current_learning_iteration, tot_iter):
+                start = time.time()
+                if cuda:   # (the previous iteration's end event is this one's start: one marker less)
+                    ev = [prev_end if prev_end is not None else torch.cuda.Event(enable_timing=True)] + \
+                         [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                    if prev_end is None:
+                        ev[0].record()
+                    prev_end = ev[2] if defer else None   # (synchronous runs: host logging lies between)
+                with torch.inference_mode():
+                    for _ in range(self.num_steps_per_env):
+                        actions = self.alg.act(obs, critic_obs)
+                        obs, privileged_obs, rewards, dones, infos = self.env.step(actions)
+                        critic_obs = privileged_obs if privileged_obs is not None else obs
+                        obs, critic_obs = obs.to(self.device), critic_obs.to(self.device)
+                        rewards, dones = rewards.to(self.device), dones.to(self.device)
+                        self.alg.process_env_step(rewards, dones, infos)
+                        if self.log_dir is not None:
+                            if "episode" in infos:
+                                ep_infos.append(infos["episode"])
+                            cur_reward_sum += rewards
+                            cur_episode_length += 1
+                            new_ids = (dones > 0).nonzero(as_tuple=False)
+                            rewbuffer.extend(cur_reward_sum[new_ids][:, 0].cpu().numpy().tolist())
+                            lenbuffer.extend(cur_episode_length[new_ids][:, 0].cpu().numpy().tolist())
+                            cur_reward_sum[new_ids] = 0
+                            cur_episode_length[new_ids] = 0
+                    if cuda:
+                        ev[1].record()
+                    stop = time.time()
+                    collection_time = stop - start
+                    start = stop
+                    self.alg.flush_store()           # (the last step's storage row: no act follows it)
+                    self.alg.compute_returns(critic_obs)
+                if pending is not None:
+                    self._finish_deferred(pending)
+                    pending = None
+                if defer:
+                    self.alg.update(defer=True)
+                    ev[2].record()
+                    pending = ev
+                    ep_infos.clear()
+                    continue
+                mean_value_loss, mean_surrogate_loss = self.alg.update()
                 stop = time.time()
-                collection_time = stop - start
-                start = stop
-                self.alg.flush_store()           # (the last step's storage row: no act follows it)
-                self.alg.compute_returns(critic_obs)
+                learn_time = stop - start
+                if cuda:
+                    ev[2].record()
+                    ev[2].synchronize()
+                    collection_time = ev[0].elapsed_time(ev[1]) * 1e-3
+                    learn_time = ev[1].elapsed_time(ev[2]) * 1e-3
+                self.last_iteration_stats = dict(collection_time=collection_time, learn_time=learn_time,
+                                                 value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
+                                                 learning_rate=self.alg.learning_rate)
+                if self.log_dir is not None:
+                    self.log(locals())
+                    if it % self.save_interval == 0:
+                        self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
+                ep_infos.clear()
+        finally:
+            # also on an exception: no deferred storage row may outlive learn() holding pointers to
+            # the env's reward / reset / time-out buffers (the env has not stepped since that row's
+            # process_env_step: every env.step follows an act, which takes the pending row), and no
+            # update readback stays pending
+            self.alg.flush_store()
+            self.alg.defer_store = False
             if pending is not None:
                 self._finish_deferred(pending)
-                pending = None
-            if defer:
-                self.alg.update(defer=True)
-                ev[2].record()
-                pending = ev
-                ep_infos.clear()
-                continue
-            mean_value_loss, mean_surrogate_loss = self.alg.update()
-            stop = time.time()
-            learn_time = stop - start
-            if cuda:
-                ev[2].record()
-                ev[2].synchronize()
-                collection_time = ev[0].elapsed_time(ev[1]) * 1e-3
-                learn_time = ev[1].elapsed_time(ev[2]) * 1e-3
-            self.last_iteration_stats = dict(collection_time=collection_time, learn_time=learn_time,
-                                             value_loss=mean_value_loss, surrogate_loss=mean_surrogate_loss,
-                                             learning_rate=self.alg.learning_rate)
-            if self.log_dir is not None:
-                self.log(locals())
-                if it % self.save_interval == 0:
-                    self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
-            ep_infos.clear()
-        if pending is not None:
-            self._finish_deferred(pending)
-        self.alg.defer_store = False
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))

@@ -896,6 +896,11 @@ static void reset_envs(const ctx_t* cx, const int32_t* ids, int n, int64_t step,
     resample_cmd(cx, e, LGX_DRAW_RESET_CMD, step, tag);
     for (int j = 0; j < 12; ++j) { b->last_actions[e * 12 + j] = 0; b->last_dof_vel[e * 12 + j] = 0; }
     for (int f = 0; f < 4; ++f) b->feet_air_time[e * 4 + f] = 0;
+    if (b->sea_h && b->sea_c) /* Anymal.reset_idx zeroes the SEA LSTM state (anymal.py:56-60) */
+      for (int L = 0; L < 2; ++L) {
+        memset(b->sea_h + ((int64_t)L * N * 12 + (int64_t)e * 12) * 8, 0, 12 * 8 * sizeof(float));
+        memset(b->sea_c + ((int64_t)L * N * 12 + (int64_t)e * 12) * 8, 0, 12 * 8 * sizeof(float));
+      }
     b->episode_length[e] = 0;
     b->reset[e] = 1;
   }
@@ -1032,23 +1037,17 @@ void lgxo_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t 
  * source of one substep (LGX_CTRL_SEA): sea_input = [a * action_scale + q0 - q, qd] per joint row
  * (env-major, as sea_input[:, 0, :] = (...).flatten()), one step of the SEA LSTM on the
  * [2, N*12, 8] hidden / cell state, torques clamped to the drive effort limit (PhysX DOF effort
- * mode).  The state of an env whose episode_length is 0 when the step starts (reset at the end of
- * the previous step, anymal.py:56-60) is zeroed first. */
+ * mode).  The state of an env that resets is zeroed by reset_envs (anymal.py:56-60). */
 static void sea_torques(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b, int substep) {
   const int64_t M = (int64_t)p->num_envs * 12;
   float* x = (float*)malloc(sizeof(float) * 2 * M);
   float* tau = (float*)malloc(sizeof(float) * M);
+  (void)substep;
   for (int e = 0; e < p->num_envs; ++e) {
-    const int fresh = substep == 0 && b->episode_length[e] == 0;
     for (int j = 0; j < 12; ++j) {
       const int64_t r = (int64_t)e * 12 + j;
       x[2 * r] = b->actions[r] * p->action_scale + p->default_dof_pos[j] - b->dof_state[2 * r];
       x[2 * r + 1] = b->dof_state[2 * r + 1];
-      if (fresh)
-        for (int L = 0; L < 2; ++L) {
-          memset(b->sea_h + ((int64_t)L * M + r) * 8, 0, 8 * sizeof(float));
-          memset(b->sea_c + ((int64_t)L * M + r) * 8, 0, 8 * sizeof(float));
-        }
     }
   }
   lgxo_actuator_lstm(x, b->sea_h, b->sea_c, tau, M, b->sea_w);
@@ -1058,6 +1057,22 @@ static void sea_torques(const lgx_model* m, const lgx_env_params* p, const lgx_b
   }
   free(x);
   free(tau);
+}
+
+/* the drive inputs of lgxo_step's decimation loop with the dynamics frozen (the golden replay;
+ * the HIP lgx_drive_inputs): clip, then per substep the Go1 actuator history (go1.py:79-98) and the
+ * position targets (legged_robot.py:394-397), the SEA LSTM torques (anymal.py:71-77, state
+ * advanced) or the explicit P / V / T torques (legged_robot.py:370-392), from the unchanged state */
+void lgxo_drive_inputs(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b) {
+  ctx_t cx = {m, p, b, NULL, 0};
+  for (int i = 0; i < p->num_envs * 12; ++i) b->actions[i] = clampf(b->actions[i], -p->clip_actions, p->clip_actions);
+  for (int s = 0; s < p->decimation; ++s) {
+    if (p->use_actuator_history)
+      for (int e = 0; e < p->num_envs; ++e) actuator_history(&cx, e, s);
+    if (p->control_type == LGX_CTRL_POS_DRIVE) lgxo_compute_targets(m, p, b);
+    else if (p->control_type == LGX_CTRL_SEA) sea_torques(m, p, b, s);
+    else lgxo_explicit_torques(p, b);
+  }
 }
 
 /* full LeggedRobot.step (legged_robot.py:79-107) */

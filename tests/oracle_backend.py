@@ -33,6 +33,7 @@ def load_oracle():
         "lgxo_reset_idx": (C.c_int, [M, P, B, vp, vp, i32, i64, i32]),
         "lgxo_simulate": (None, [M, P, B, i32]),
         "lgxo_compute_targets": (None, [M, P, B]),
+        "lgxo_drive_inputs": (None, [M, P, B]),
         "lgxo_actuator_history": (None, [M, P, B, i32]),
         "lgxo_explicit_torques": (None, [P, B]),
         "lgxo_actuator_mlp": (None, [vp, vp, i64, vp, vp]),

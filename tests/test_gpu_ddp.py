@@ -117,3 +117,31 @@ def test_fused_update_two_ranks_equal_one_process(gpu, early):
         big += int((d > 1e-5).sum())
         total += d.size
     assert big <= 1e-3 * total, (big, total)
+
+
+@pytest.mark.timeout(280)
+def test_bench_two_ranks_self_check(gpu, tmp_path):
+    """bench.py --gpus 2 under torch.distributed.run, two ranks sharing cuda:0 over gloo
+    (LGX_DIST_BACKEND=gloo; RCCL refuses two ranks on one device): the JSON line carries the
+    data-parallel self-check the driver's 8-GPU run is judged by - both ranks seen, bitwise
+    identical parameters after the timed iterations (fingerprint spread 0), the two-bucket gradient
+    all-reduce taken, event-timed all-reduces."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LGX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", LGX_BENCH_GEMM_TIMING="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--task", "go1_flat_bench", "--num_envs", "256",
+           "--no_cpu_baseline"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2 and d["config"]["global_envs"] == 512
+    dp = d["data_parallel"]
+    assert dp["world"] == 2 and dp["backend"] == "gloo" and dp["ranks_seen"] == 2
+    assert dp["params_identical_across_ranks"] and dp["param_fingerprint_spread"] == 0
+    assert dp["bucketed_allreduce"] is True
+    assert dp["allreduce"]["collectives_timed"] >= 2 and dp["allreduce"]["ms_per_iteration"] > 0

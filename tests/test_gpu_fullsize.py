@@ -1,5 +1,5 @@
 """GPU at the benchmark sizes: C3 (go1_rough, 4096 envs/GPU: one round of lgx_physics_kernel<4>
-workgroups), C5 (anymal_c_rough with friction / base-mass / push randomisation, 8192 envs/GPU: two
+workgroups), C2 (go1_flat_bench: plane, PD drive, no randomisation, 4096 envs), C5 (anymal_c_rough with friction / base-mass / push randomisation, 8192 envs/GPU: two
 rounds) and 16384 envs (four rounds): size-independent properties of a rollout, oracle parity of a strided 64-env subset
 taken from the full-size run, and the every-env-resets-at-once edge case.
 
@@ -14,7 +14,7 @@ from test_gpu_parity import close, randomize_state, sync
 pytestmark = pytest.mark.gpu
 
 N = 4096
-SIZES = [("go1_rough", 4096), ("anymal_c_rough", 8192), ("anymal_c_rough", 16384)]
+SIZES = [("go1_rough", 4096), ("go1_flat_bench", 4096), ("anymal_c_rough", 8192), ("anymal_c_rough", 16384)]
 _ENVS = {}
 
 
@@ -73,7 +73,9 @@ def test_full_size_subset_matches_oracle(gpu, task, n):
     assert lgxlib.load().lgx_physics_lane_split(N) == 4
     idx = torch.arange(0, N, N // 64)
     ora = make_env(task, num_envs=64, device="cpu", backend="oracle", overrides=_no_noise)
-    if not torch.equal(ora.height_samples, dev.height_samples.cpu()):
+    if dev.height_samples is None:     # C2: plane
+        assert ora.height_samples is None
+    elif not torch.equal(ora.height_samples, dev.height_samples.cpu()):
         pytest.skip("heightfield depends on num_envs")
     gen = torch.Generator().manual_seed(5)
     ora.dof_state.view(64, 12, 2).copy_(dev.dof_state.view(N, 12, 2)[idx.cuda()].cpu())

@@ -394,6 +394,27 @@ def test_gae_kernel_matches_torch_loop(gpu, N):
     assert ok, f"advantages max err {e}"
 
 
+def test_gae_norm_large_mean_advantages(gpu):
+    """Advantages with |mean| >> std (rewards ~3e3 +- 1e-2): the per-workgroup (count, mean, M2)
+    summaries combined with Chan's formula keep the normalised advantages at float64 accuracy (a
+    one-pass sum-of-squares variance cancels to nothing here)."""
+    from legged_gym_amd.rl.storage import RolloutStorage
+    T, N = 24, 4096
+    gen = torch.Generator().manual_seed(2)
+    st = RolloutStorage(N, T, [4], [None], [2], str(gpu))
+    rew = 3e3 + 1e-2 * torch.randn(T, N, 1, generator=gen)
+    st.rewards.copy_(rew)
+    st.values.zero_()
+    st.dones.zero_()
+    last = torch.zeros(N, 1)
+    st.compute_returns(last.to(gpu), 0.0, 0.95)   # gamma 0: advantage = reward - value
+    adv = st.returns.double().cpu()            # values are zero: raw advantages = returns
+    want = (adv - adv.mean()) / (adv.std() + 1e-8)
+    got = st.advantages.double().cpu()
+    assert (got - want).abs().max().item() <= 2e-3 * want.abs().max().item()
+    assert abs(got.std().item() - 1.0) < 1e-3
+
+
 def test_splitk_linear_gradients_match_torch(gpu):
     from legged_gym_amd.rl.actor_critic import LgxLinear
     torch.manual_seed(0)
@@ -547,6 +568,10 @@ def test_anymal_sea_torque_step_matches_oracle(gpu, monkeypatch, pp):
         assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf), it
         if it == 0:
             assert ora.reset_buf[:4].all()
+        if it == 0:   # reset_idx zeroed the LSTM state of the envs that reset (anymal.py:56-60)
+            assert (dev.sea_hidden_state.view(2, 64, 12, 8)[:, :4] == 0).all()
+            assert (dev.sea_cell_state.view(2, 64, 12, 8)[:, :4] == 0).all()
+            assert (dev.sea_hidden_state.view(2, 64, 12, 8)[:, 4:] != 0).any()
         if it == 1:   # the envs reset by step 0 restarted their LSTM state from zero
             assert (dev._episode_length_buf[:4] == 1).all()
         # LSTM state after 4 substeps: f32 with fma contraction and v_exp-based sigmoid / tanh in

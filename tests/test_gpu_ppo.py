@@ -8,6 +8,7 @@ to 1e-4 relative, parameters to 2 Adam steps of the smallest learning rate for t
 coordinates whose gradient is at rounding level (Adam normalises their sign), 1e-5 otherwise.
 """
 import copy
+import os
 
 import pytest
 import torch
@@ -20,13 +21,14 @@ pytestmark = pytest.mark.gpu
 T, N, OBS, ACT = 6, 1024, 235, 12
 
 
-def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128)):
+def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128), T=T, N=N, epochs=2):
     """Reference (autograd) and fused PPO on identical storage; cobs = privileged critic
-    observation width (None: the critic reads the actor's observations)."""
+    observation width (None: the critic reads the actor's observations); T x N transitions in
+    4 minibatches, `epochs` learning epochs."""
     torch.manual_seed(0)
     ac = ActorCritic(OBS, cobs or OBS, ACT, list(hidden), list(hidden))
     ac2 = copy.deepcopy(ac)
-    kw = dict(num_learning_epochs=2, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95, value_loss_coef=1.0,
+    kw = dict(num_learning_epochs=epochs, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95, value_loss_coef=1.0,
               entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0, schedule=schedule, desired_kl=0.01,
               device="cuda:0")
     ref = PPO(ac, use_fused_update=False, **kw)
@@ -59,7 +61,7 @@ def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128)):
 
 def autograd_grads(ref, idx):
     st = ref.storage
-    B = T * N
+    B = st.num_transitions_per_env * st.num_envs
     ac = ref.actor_critic
     obs = st.observations.view(B, -1)[idx]
     cobs = st.privileged_observations.view(B, -1)[idx] if st.privileged_observations is not None else obs
@@ -375,4 +377,50 @@ def test_fused_update_every_step_is_exact(gpu, monkeypatch, schedule, cobs, algo
         assert ((rec["m1"].double() - m_want).abs() <= 1e-5 * m_scale + 1e-12).all(), t
         assert ((rec["v1"].double() - v_want).abs() <= 2e-5 * v_want.abs() + 1e-18).all(), t
         if t > 0:   # every step starts from the previous step's result
+            assert torch.equal(rec["p0"], tr.steps[t - 1]["p1"])
+
+
+@pytest.mark.parametrize("n_envs", [4096, 8192])
+def test_fused_update_bench_shape_every_step_is_exact(gpu, n_envs):
+    """The composed update at the shapes bench.py runs: 24 steps x 4096 envs
+    (C3: 24,576-row minibatches) and x 8192 envs (C5: 49,152 rows), the default schedule - the
+    two-stream backward with dW row slices sized for half the CUs, the early reduction on the
+    second stream, the K-specialised and half-tile forward instantiations - one epoch of 4
+    minibatches, every coordinate of every step checked as in test_fused_update_every_step_is_exact
+    (gradient vs autograd at the recorded parameters and rows, the step vs float64 clip + Adam)."""
+    from ppo_trace import StepTrace, adam64, flat_view
+    for var in ("LGX_GEMM_ALGO", "LGX_PPO_DW_SIDE", "LGX_PPO_EARLY_REDUCE", "LGX_PPO_SPLITS", "LGX_GEMM_X3P_PM"):
+        assert var not in os.environ, var     # the bench's default schedule
+    Tb = 24
+    ref, fus = make_pair("adaptive", None, T=Tb, N=n_envs, epochs=1)
+    f = fus._fused
+    tr = StepTrace(f)
+    torch.manual_seed(11)
+    fus.update()
+    tr.close()
+    assert f.M == Tb * n_envs // 4 and f.split and f.tn and f.loss_bwd and f.dw1_batched
+    assert getattr(f, "_side", None) is not None      # the dW GEMMs ran on the second stream
+    assert f.Sk == [f._tn_slices(512, OBS, f.M, fill=0.5), f._tn_slices(256, 512, f.M, fill=0.5),
+                    f._tn_slices(128, 256, f.M, fill=0.5)]
+    torch.manual_seed(11)
+    ref.update()
+    assert fus.learning_rate == ref.learning_rate
+    assert len(tr.steps) == 4
+    params = list(ref.actor_critic.parameters())
+    for t, rec in enumerate(tr.steps):
+        with torch.no_grad():
+            for p, q in zip(params, f.optimizer.params):
+                off = f.off[id(q)]
+                p.copy_(rec["p0"][off:off + q.numel()].view_as(p))
+        g_ref = flat_view(f, list(autograd_grads(ref, rec["idx"]).values()))
+        g = rec["g"].double()
+        bad = ((g - g_ref).abs() > 1e-5 + 2e-3 * g_ref.abs()).sum().item()
+        assert bad == 0, (n_envs, t, bad, (g - g_ref).abs().max().item())
+        p_want, m_want, v_want = adam64(rec, fus.max_grad_norm)
+        dp = (rec["p1"].double() - p_want).abs()
+        assert (dp <= 1e-6 + 1e-3 * rec["lr"]).all(), (n_envs, t, dp.max().item(), rec["lr"])
+        m_scale = 0.9 * rec["m0"].double().abs() + (m_want - 0.9 * rec["m0"].double()).abs()
+        assert ((rec["m1"].double() - m_want).abs() <= 1e-5 * m_scale + 1e-12).all(), t
+        assert ((rec["v1"].double() - v_want).abs() <= 2e-5 * v_want.abs() + 1e-18).all(), t
+        if t > 0:
             assert torch.equal(rec["p0"], tr.steps[t - 1]["p1"])

@@ -3,8 +3,8 @@ anymal.py:71-78 with use_actuator_network, reached through cfg.control.explicit_
 
 CPU: the oracle's step against torch's own nn.LSTM with the weights of the reference's
 anydrive_v3_lstm.pt (extracted to resources/actuator_nets/anydrive_v3_lstm.npz): one substep
-(decimation 1), so the reported torques are exactly the LSTM output of that substep; the state of
-an env reset in the previous step (episode_length 0) starts from zero (anymal.py:56-60).
+(decimation 1), so the reported torques are exactly the LSTM output of that substep; an env that
+resets in the step ends it with zero LSTM state (Anymal.reset_idx, anymal.py:56-60), read back.
 GPU: tests/test_gpu_parity.py::test_anymal_sea_torque_step_matches_oracle.
 """
 import os
@@ -44,15 +44,16 @@ def test_sea_torque_step_matches_torch_lstm():
     env.sea_hidden_state.copy_(torch.randn(2, N * 12, 8, generator=g) * 0.3)
     env.sea_cell_state.copy_(torch.randn(2, N * 12, 8, generator=g) * 0.3)
     env._episode_length_buf[:] = torch.arange(N) * 7 + 1
-    env._episode_length_buf[3] = 0                       # reset in the previous step: zero state
+    env._episode_length_buf[3] = int(env.max_episode_length)   # times out in this step
     a = (torch.rand(N, 12, generator=g) - 0.5) * 2
     x = torch.stack([(a * env.cfg.control.action_scale + env.default_dof_pos - env.dof_pos).flatten(),
                      env.dof_vel.flatten()], dim=1)
     h0, c0 = env.sea_hidden_state.clone(), env.sea_cell_state.clone()
-    h0.view(2, N, 12, 8)[:, 3] = 0
-    c0.view(2, N, 12, 8)[:, 3] = 0
     tau, h2, c2 = _torch_sea(net, x, h0, c0)
     env.step(a)
+    assert bool(env.reset_buf[3]) and int(env.reset_buf.sum()) == 1
+    h2.view(2, N, 12, 8)[:, 3] = 0      # reset_idx zeroed env 3's state after its last substep
+    c2.view(2, N, 12, 8)[:, 3] = 0
     eff = env.torque_limits.repeat(N)
     want = torch.clamp(tau, -eff, eff).view(N, 12)
     assert torch.allclose(env.torques, want, atol=1e-4, rtol=1e-5), (env.torques - want).abs().max()

@@ -11,7 +11,17 @@ What it does
   * steps the reference `Go1` / `Anymal` envs and records, per step, the inputs (actions,
     scripted physics state, draw table) and the outputs of the reference's own code
     (obs, rew, resets, time-outs, extras, commands, feet air time, episode sums, post-reset
-    state, last_* buffers, heights, actuator-net inputs, terrain levels/origins).
+    state, last_* buffers, heights, actuator-net inputs, terrain levels/origins);
+  * the actuator networks: `torch.jit.load` (which would execute code stored in the archive) is
+    replaced by modules rebuilt from the archives' weights (resources/actuator_nets/*.npz,
+    extracted statically by tools/export_actuator_nets.py) with the architecture of the archives'
+    code text (`MLP.architecture`: Linear 30-128, Tanh, 128-128, Tanh, 128-128, Tanh, 128-3;
+    `LSTMsea`: x * in_scale -> LSTM(2, 8, 2 layers, batch_first) -> out_scale * squeeze(Linear(8, 1))).
+    The reference's own wrappers run around them: Go1's `UniNet` leg slicing and `dVel *= vel_std`
+    (go1.py:22-35,100-105), recorded per substep as `step_dvel`; ANYmal's `_compute_torques`
+    (anymal.py:71-77, unreachable from this fork's step) called `decimation` times per step on the
+    pre-step state as the decimation loop would, recorded as `step_sea_torques`, and the LSTM
+    state after the step (after `reset_idx`'s zeroing, anymal.py:56-60) as `step_sea_h/c`.
 Nothing here ships: the reference never reaches the GPU box, only the .npz vectors do.
 
 Usage: python tools/golden/gen_golden.py            -> tests/golden/*.npz
@@ -231,6 +241,63 @@ def make_isaacgym_stub(model):
     sys.modules["rsl_rl.runners"].OnPolicyRunner = object
 
 
+# ----------------------------------------------------------------------------- actuator networks
+def _net_weights(name):
+    return dict(np.load(os.path.join(ROOT, "legged_gym_amd", "resources", "actuator_nets", name + ".npz"),
+                        allow_pickle=False))
+
+
+class Go1NetFromWeights(torch.nn.Sequential):
+    """go1_net.pt's MLP.architecture (archive code text): Linear(30,128) Tanh Linear(128,128) Tanh
+    Linear(128,128) Tanh Linear(128,3), weights from go1_net.npz."""
+
+    def __init__(self):
+        w = _net_weights("go1_net")
+        with torch.random.fork_rng():    # (module init must not move the reference's RNG streams)
+            layers = [torch.nn.Linear(30, 128), torch.nn.Tanh(), torch.nn.Linear(128, 128), torch.nn.Tanh(),
+                      torch.nn.Linear(128, 128), torch.nn.Tanh(), torch.nn.Linear(128, 3)]
+        super().__init__(*layers)
+        with torch.no_grad():
+            for k, lin in enumerate(layers[0::2]):
+                lin.weight.copy_(torch.from_numpy(w[f"w{k}"]))
+                lin.bias.copy_(torch.from_numpy(w[f"b{k}"]))
+
+
+class LSTMseaFromWeights(torch.nn.Module):
+    """anydrive_v3_lstm.pt's LSTMsea.forward (archive code text): x * in_scale -> LSTM(2, 8, 2
+    layers, batch_first=True) -> out_scale * squeeze(Linear(8, 1)(x1)), returns (torques, (h, c));
+    weights from anydrive_v3_lstm.npz."""
+
+    def __init__(self):
+        super().__init__()
+        w = _net_weights("anydrive_v3_lstm")
+        with torch.random.fork_rng():
+            self.lstm = torch.nn.LSTM(2, 8, 2, batch_first=True)
+            self.linear = torch.nn.Linear(8, 1)
+        with torch.no_grad():
+            for L in range(2):
+                for k in ("weight_ih", "weight_hh", "bias_ih", "bias_hh"):
+                    src = k.replace("weight", "w").replace("bias", "b") + f"_l{L}"
+                    getattr(self.lstm, f"{k}_l{L}").copy_(torch.from_numpy(w[src]))
+            self.linear.weight.copy_(torch.from_numpy(w["w_lin"]))
+            self.linear.bias.copy_(torch.from_numpy(w["b_lin"]))
+        self.register_buffer("in_scale", torch.from_numpy(w["in_scale"]))
+        self.register_buffer("out_scale", torch.from_numpy(w["out_scale"]))
+
+    def forward(self, x, hc0):
+        x1, hcn = self.lstm(x * self.in_scale, hc0)
+        return self.out_scale * torch.squeeze(self.linear(x1)), hcn
+
+
+def load_actuator_net_module(path, *a, **k):
+    base = os.path.basename(str(path))
+    if base.startswith("go1_net"):
+        return Go1NetFromWeights()
+    if "lstm" in base:
+        return LSTMseaFromWeights()
+    raise ValueError(f"no weights-only restatement for {path}")
+
+
 # ----------------------------------------------------------------------------- instrumentation
 def instrument(env, stride):
     """Route every post-physics random draw of the reference env through DrawCtx."""
@@ -347,13 +414,9 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
                 self.vertices = np.zeros((4, 3), np.float32)
                 self.triangles = np.zeros((2, 3), np.uint32)
     lr.Terrain = TerrainForRef
-    # Go1's actuator net: the TorchScript archive is not loaded (no executing loader); the
-    # recorded quantity is the actuator-net INPUT history (model_ins), which is what the
-    # reference computes on the step path (the MLP output dVel is discarded, go1.py:71-73)
-    class _NoNet(torch.nn.Module):
-        def forward(self, x, *a):
-            return torch.zeros(x.shape[0], 3)
-    torch.jit.load = lambda *a, **k: _NoNet()
+    # actuator nets: the TorchScript archives are not loaded (no executing loader); modules rebuilt
+    # from their weights stand in (see the module docstring)
+    torch.jit.load = load_actuator_net_module
     cfg = cfg_fn()
     cfg.env.num_envs = num_envs
     torch.manual_seed(seed)
@@ -364,6 +427,16 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
     stride = abi.DRAW_NOISE + env.num_obs
     gen = torch.Generator().manual_seed(seed + 100)
     instrument(env, stride)
+    dvel_sub = []
+    if hasattr(env, "actuator_network") and hasattr(env, "actuator_advance"):   # Go1: record dVel per substep
+        orig_adv = env.actuator_advance
+
+        def actuator_advance(actions):
+            d = orig_adv(actions)
+            dvel_sub.append(d.detach().clone())
+            return d
+        env.actuator_advance = actuator_advance
+    sea = hasattr(env, "sea_hidden_state") and getattr(cfg.control, "use_actuator_network", False)
     setup_levels = env.terrain_levels.clone().numpy() if hasattr(env, "terrain_levels") else None
     setup_origins = env.env_origins.clone().numpy()
     # initial reset() with injected draws
@@ -387,6 +460,9 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
     init_state = snapshot(env, REC_KEYS + ["terrain_levels"] if hasattr(env, "terrain_levels") else REC_KEYS)
     init_state["episode_sums"] = np.stack([env.episode_sums[k].numpy() for k in env.episode_sums])
     init_state["common_step_counter"] = np.array(env.common_step_counter)
+    if sea:
+        init_state["sea_h"] = env.sea_hidden_state.numpy().copy()
+        init_state["sea_c"] = env.sea_cell_state.numpy().copy()
     if hasattr(env, "pos_err_buffs"):
         init_state["act_hist"] = np.concatenate([env.pos_err_buffs, env.vel_buffs], axis=2).astype(np.float32)
     if env.height_samples is not None:
@@ -398,7 +474,7 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
     rec["episode_keys"] = np.array(list(env.episode_sums.keys()))
     per_step = {k: [] for k in ["actions", "draws", "next_root", "next_dof", "next_cf", "next_tq", "extras",
                                 "extras_time_outs", "episode_sums", "terrain_levels", "measured_heights", "model_ins",
-                                "reset_ids"] + REC_KEYS}
+                                "reset_ids", "dvel", "sea_torques", "sea_h", "sea_c"] + REC_KEYS}
     for t in range(steps):
         DrawCtx.table = torch.rand(num_envs, stride, generator=gen)
         actions = (torch.rand(num_envs, env.num_actions, generator=gen) - 0.5) * 4.0
@@ -407,7 +483,17 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
         gym.next_state = nxt
         gym.decimation = cfg.control.decimation
         env.extras.pop("episode", None)
+        if sea:   # anymal.py:71-77 per substep on the pre-step state (scripted physics moves at the last)
+            clipped = torch.clip(actions, -cfg.normalization.clip_actions, cfg.normalization.clip_actions)
+            per_step["sea_torques"].append(np.stack([env._compute_torques(clipped).detach().clone().view(
+                num_envs, env.num_actions).numpy() for _ in range(cfg.control.decimation)]))
+        dvel_sub.clear()
         env.step(actions)
+        if dvel_sub:
+            per_step["dvel"].append(torch.stack(dvel_sub).numpy())
+        if sea:   # after reset_idx zeroed the state of the envs that reset (anymal.py:56-60)
+            per_step["sea_h"].append(env.sea_hidden_state.numpy().copy())
+            per_step["sea_c"].append(env.sea_cell_state.numpy().copy())
         per_step["actions"].append(actions.numpy())
         per_step["draws"].append(DrawCtx.table.numpy())
         for k, v in zip(["next_root", "next_dof", "next_cf", "next_tq"], nxt):
@@ -430,7 +516,7 @@ def run_case(name, env_cls_name, cfg_fn, num_envs, steps, seed, model_json, stan
         per_step["reset_ids"].append(np.zeros(0, np.int32))
     DrawCtx.cursor = None
     for k, v in per_step.items():
-        if k == "reset_ids":
+        if k == "reset_ids" or not v:
             continue
         rec["step_" + k] = np.stack(v)
     for k, v in init_state.items():
