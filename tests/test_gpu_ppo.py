@@ -398,7 +398,7 @@ def test_fused_update_bench_shape_every_step_is_exact(gpu, n_envs):
     torch.manual_seed(11)
     fus.update()
     tr.close()
-    assert f.M == Tb * n_envs // 4 and f.split and f.tn and f.loss_bwd and f.dw1_batched
+    assert f.M == Tb * n_envs // 4 and f.split and f.tn and f.loss_bwd and sorted(f.gemm_dw) == [0, 1, 2]
     assert getattr(f, "_side", None) is not None      # the dW GEMMs ran on the second stream
     assert f.Sk == [f._tn_slices(512, OBS, f.M, fill=0.5), f._tn_slices(256, 512, f.M, fill=0.5),
                     f._tn_slices(128, 256, f.M, fill=0.5)]
