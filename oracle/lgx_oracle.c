@@ -77,73 +77,92 @@ static float draw(const ctx_t* cx, int env, int slot, int64_t step, uint32_t tag
   return lgxo_uniform(cx->p->seed, env, slot, step, tag);
 }
 
+/* ------------------------------------------------------------------ arithmetic type of the physics
+ * `real` is float (the product's arithmetic) unless built with -DLGXO_REAL=double: the float64
+ * physics oracle (liblgx_oracle64.so, oracle/Makefile) that derives the physics tolerances - the
+ * same algorithm in double precision, state read from / written to the float32 buffers at substep
+ * boundaries (as in every build). */
+#ifndef LGXO_REAL
+#define LGXO_REAL float
+#endif
+typedef LGXO_REAL real;
+#define LGXO_F64 (sizeof(real) == 8)
+#define SQRT_R(x) (LGXO_F64 ? (real)sqrt(x) : (real)sqrtf(x))
+#define FABS_R(x) (LGXO_F64 ? (real)fabs(x) : (real)fabsf(x))
+#define FLOOR_R(x) (LGXO_F64 ? (real)floor(x) : (real)floorf(x))
+#define FMAX_R(x, y) (LGXO_F64 ? (real)fmax(x, y) : (real)fmaxf(x, y))
+#define FMIN_R(x, y) (LGXO_F64 ? (real)fmin(x, y) : (real)fminf(x, y))
+#define COS_R(x) (LGXO_F64 ? (real)cos(x) : (real)cosf(x))
+#define SIN_R(x) (LGXO_F64 ? (real)sin(x) : (real)sinf(x))
+static void ldr(real* o, const float* s, int n) { for (int i = 0; i < n; ++i) o[i] = (real)s[i]; }
+
 /* ------------------------------------------------------------------ small linear algebra */
-static void cross3(const float* a, const float* b, float* o) {
-  float x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+static void cross3(const real* a, const real* b, real* o) {
+  real x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
   o[0] = x; o[1] = y; o[2] = z;
 }
-static float dot3(const float* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
-static void matmul3(const float* A, const float* B, float* C) {
-  float T[9];
+static real dot3(const real* a, const real* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void matmul3(const real* A, const real* B, real* C) {
+  real T[9];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) T[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
   memcpy(C, T, sizeof T);
 }
-static void matvec3(const float* A, const float* x, float* y) {
-  float t0 = A[0] * x[0] + A[1] * x[1] + A[2] * x[2];
-  float t1 = A[3] * x[0] + A[4] * x[1] + A[5] * x[2];
-  float t2 = A[6] * x[0] + A[7] * x[1] + A[8] * x[2];
+static void matvec3(const real* A, const real* x, real* y) {
+  real t0 = A[0] * x[0] + A[1] * x[1] + A[2] * x[2];
+  real t1 = A[3] * x[0] + A[4] * x[1] + A[5] * x[2];
+  real t2 = A[6] * x[0] + A[7] * x[1] + A[8] * x[2];
   y[0] = t0; y[1] = t1; y[2] = t2;
 }
-static void quat_to_mat(const float* q, float* R) { /* xyzw */
-  float x = q[0], y = q[1], z = q[2], w = q[3];
+static void quat_to_mat(const real* q, real* R) { /* xyzw */
+  real x = q[0], y = q[1], z = q[2], w = q[3];
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - z * w);     R[2] = 2 * (x * z + y * w);
   R[3] = 2 * (x * y + z * w);     R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - x * w);
   R[6] = 2 * (x * z - y * w);     R[7] = 2 * (y * z + x * w);     R[8] = 1 - 2 * (x * x + y * y);
 }
-static void axis_angle(const float* a, float th, float* R) { /* Rodrigues */
-  float c = cosf(th), s = sinf(th), t = 1 - c;
-  float x = a[0], y = a[1], z = a[2];
+static void axis_angle(const real* a, real th, real* R) { /* Rodrigues */
+  real c = COS_R(th), s = SIN_R(th), t = 1 - c;
+  real x = a[0], y = a[1], z = a[2];
   R[0] = t * x * x + c;     R[1] = t * x * y - s * z; R[2] = t * x * z + s * y;
   R[3] = t * x * y + s * z; R[4] = t * y * y + c;     R[5] = t * y * z - s * x;
   R[6] = t * x * z - s * y; R[7] = t * y * z + s * x; R[8] = t * z * z + c;
 }
 
 /* isaacgym.torch_utils semantics (xyzw) */
-static void quat_rotate_inverse(const float* q, const float* v, float* o) {
-  float w = q[3];
-  float a = 2.0f * w * w - 1.0f;
-  float cx[3]; cross3(q, v, cx);
-  float d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
+static void quat_rotate_inverse(const real* q, const real* v, real* o) {
+  real w = q[3];
+  real a = 2.0f * w * w - 1.0f;
+  real cx[3]; cross3(q, v, cx);
+  real d = q[0] * v[0] + q[1] * v[1] + q[2] * v[2];
   for (int i = 0; i < 3; ++i) o[i] = v[i] * a - cx[i] * w * 2.0f + q[i] * d * 2.0f;
 }
-static void quat_apply(const float* q, const float* v, float* o) {
-  float t[3]; cross3(q, v, t);
+static void quat_apply(const real* q, const real* v, real* o) {
+  real t[3]; cross3(q, v, t);
   for (int i = 0; i < 3; ++i) t[i] *= 2.0f;
-  float u[3]; cross3(q, t, u);
+  real u[3]; cross3(q, t, u);
   for (int i = 0; i < 3; ++i) o[i] = v[i] + q[3] * t[i] + u[i];
 }
 
 /* Cholesky solve of a dense SPD n x n system (in place, row-major lda = n) */
-static void chol_solve(float* A, float* b, int n) {
+static void chol_solve(real* A, real* b, int n) {
   for (int j = 0; j < n; ++j) {
-    float s = A[j * n + j];
+    real s = A[j * n + j];
     for (int k = 0; k < j; ++k) s -= A[j * n + k] * A[j * n + k];
-    float d = sqrtf(s > 1e-20f ? s : 1e-20f);
+    real d = SQRT_R(s > 1e-20f ? s : 1e-20f);
     A[j * n + j] = d;
     for (int i = j + 1; i < n; ++i) {
-      float t = A[i * n + j];
+      real t = A[i * n + j];
       for (int k = 0; k < j; ++k) t -= A[i * n + k] * A[j * n + k];
       A[i * n + j] = t / d;
     }
   }
   for (int i = 0; i < n; ++i) {
-    float t = b[i];
+    real t = b[i];
     for (int k = 0; k < i; ++k) t -= A[i * n + k] * b[k];
     b[i] = t / A[i * n + i];
   }
   for (int i = n - 1; i >= 0; --i) {
-    float t = b[i];
+    real t = b[i];
     for (int k = i + 1; k < n; ++k) t -= A[k * n + i] * b[k];
     b[i] = t / A[i * n + i];
   }
@@ -152,24 +171,24 @@ static void chol_solve(float* A, float* b, int n) {
 /* ------------------------------------------------------------------ terrain */
 /* ground height / normal of the triangulated heightfield (two triangles per cell, diagonal
  * (i,j)-(i+1,j+1), as isaacgym terrain_utils.convert_heightfield_to_trimesh builds it) */
-static float ground(const ctx_t* cx, float x, float y, float* n) {
+static real ground(const ctx_t* cx, real x, real y, real* n) {
   const lgx_env_params* p = cx->p;
   const lgx_buffers* b = cx->b;
   if (p->terrain_kind == 0 || !b->height_samples) { n[0] = 0; n[1] = 0; n[2] = 1; return 0.0f; }
-  float ihs = 1.0f / p->horizontal_scale, vs = p->vertical_scale;   /* reciprocal scale, as the kernel */
-  float u = (x + p->border_size) * ihs, v = (y + p->border_size) * ihs;
-  int i = (int)floorf(u), j = (int)floorf(v);
+  real ihs = 1.0f / p->horizontal_scale, vs = p->vertical_scale;   /* reciprocal scale, as the kernel */
+  real u = (x + p->border_size) * ihs, v = (y + p->border_size) * ihs;
+  int i = (int)FLOOR_R(u), j = (int)FLOOR_R(v);
   if (i < 0) i = 0; if (i > b->hf_rows - 2) i = b->hf_rows - 2;
   if (j < 0) j = 0; if (j > b->hf_cols - 2) j = b->hf_cols - 2;
-  float fu = u - (float)i, fv = v - (float)j;
+  real fu = u - (real)i, fv = v - (real)j;
   if (fu < 0) fu = 0; if (fu > 1) fu = 1; if (fv < 0) fv = 0; if (fv > 1) fv = 1;
   const int16_t* H = b->height_samples;
-  float h00 = H[i * b->hf_cols + j] * vs, h10 = H[(i + 1) * b->hf_cols + j] * vs;
-  float h01 = H[i * b->hf_cols + j + 1] * vs, h11 = H[(i + 1) * b->hf_cols + j + 1] * vs;
-  float gx, gy, h;
+  real h00 = H[i * b->hf_cols + j] * vs, h10 = H[(i + 1) * b->hf_cols + j] * vs;
+  real h01 = H[i * b->hf_cols + j + 1] * vs, h11 = H[(i + 1) * b->hf_cols + j + 1] * vs;
+  real gx, gy, h;
   if (fu >= fv) { gx = (h10 - h00) * ihs; gy = (h11 - h10) * ihs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
   else          { gx = (h11 - h01) * ihs; gy = (h01 - h00) * ihs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
-  float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
+  real inv = 1.0f / SQRT_R(gx * gx + gy * gy + 1.0f);
   n[0] = -gx * inv; n[1] = -gy * inv; n[2] = inv;
   return h;
 }
@@ -177,53 +196,53 @@ static float ground(const ctx_t* cx, float x, float y, float* n) {
 /* ---- contact against the slope-corrected trimesh (terrain.py:70-73, legged_robot.py:629-643;
  * lgx_buffers.hf_trimesh): same model as the kernel, restated on plain arrays.  Closest point of a
  * triangle: Ericson, Real-Time Collision Detection 5.1.5. */
-static void v3(float* o, float x, float y, float z) { o[0] = x; o[1] = y; o[2] = z; }
-static void sub3(const float* a, const float* b, float* o) { v3(o, a[0] - b[0], a[1] - b[1], a[2] - b[2]); }
-static void axpy3(const float* a, float s, const float* d, float* o) { v3(o, a[0] + s * d[0], a[1] + s * d[1], a[2] + s * d[2]); }
+static void v3(real* o, real x, real y, real z) { o[0] = x; o[1] = y; o[2] = z; }
+static void sub3(const real* a, const real* b, real* o) { v3(o, a[0] - b[0], a[1] - b[1], a[2] - b[2]); }
+static void axpy3(const real* a, real s, const real* d, real* o) { v3(o, a[0] + s * d[0], a[1] + s * d[1], a[2] + s * d[2]); }
 
-static void closest_on_tri(const float* p, const float* a, const float* b, const float* c, float* o) {
-  float ab[3], ac[3], ap[3], bp[3], cq[3], bc[3];
+static void closest_on_tri(const real* p, const real* a, const real* b, const real* c, real* o) {
+  real ab[3], ac[3], ap[3], bp[3], cq[3], bc[3];
   sub3(b, a, ab); sub3(c, a, ac); sub3(p, a, ap);
-  float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-  if (d1 <= 0 && d2 <= 0) { memcpy(o, a, 12); return; }
+  real d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { memcpy(o, a, 3 * sizeof(real)); return; }
   sub3(p, b, bp);
-  float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-  if (d3 >= 0 && d4 <= d3) { memcpy(o, b, 12); return; }
-  float vc = d1 * d4 - d3 * d2;
+  real d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { memcpy(o, b, 3 * sizeof(real)); return; }
+  real vc = d1 * d4 - d3 * d2;
   if (vc <= 0 && d1 >= 0 && d3 <= 0) { axpy3(a, d1 / (d1 - d3), ab, o); return; }
   sub3(p, c, cq);
-  float d5 = dot3(ab, cq), d6 = dot3(ac, cq);
-  if (d6 >= 0 && d5 <= d6) { memcpy(o, c, 12); return; }
-  float vb = d5 * d2 - d1 * d6;
+  real d5 = dot3(ab, cq), d6 = dot3(ac, cq);
+  if (d6 >= 0 && d5 <= d6) { memcpy(o, c, 3 * sizeof(real)); return; }
+  real vb = d5 * d2 - d1 * d6;
   if (vb <= 0 && d2 >= 0 && d6 <= 0) { axpy3(a, d2 / (d2 - d6), ac, o); return; }
-  float va = d3 * d6 - d5 * d4;
+  real va = d3 * d6 - d5 * d4;
   if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
     sub3(c, b, bc);
     axpy3(b, (d4 - d3) / ((d4 - d3) + (d5 - d6)), bc, o);
     return;
   }
-  float den = 1.0f / (va + vb + vc);
-  float t[3];
+  real den = 1.0f / (va + vb + vc);
+  real t[3];
   axpy3(a, vb * den, ab, t);
   axpy3(t, vc * den, ac, o);
 }
 
-typedef struct { float d2, cp[3], cn[3], top, tn[3]; } tmq_t;
+typedef struct { real d2, cp[3], cn[3], top, tn[3]; } tmq_t;
 
-static void tm_tri(tmq_t* q, const float* p, const float* a, const float* b, const float* c) {
-  float e1[3], e2[3], cp[3], dv[3];
+static void tm_tri(tmq_t* q, const real* p, const real* a, const real* b, const real* c) {
+  real e1[3], e2[3], cp[3], dv[3];
   sub3(b, a, e1); sub3(c, a, e2);
   closest_on_tri(p, a, b, c, cp);
   sub3(p, cp, dv);
-  float d2 = dot3(dv, dv);
-  if (d2 < q->d2) { q->d2 = d2; memcpy(q->cp, cp, 12); cross3(e1, e2, q->cn); }
-  float den = e1[0] * e2[1] - e1[1] * e2[0];
-  if (fabsf(den) > 1e-9f) {
-    float id = 1.0f / den;
-    float px = p[0] - a[0], py = p[1] - a[1];
-    float s = (px * e2[1] - py * e2[0]) * id, t = (e1[0] * py - e1[1] * px) * id;
+  real d2 = dot3(dv, dv);
+  if (d2 < q->d2) { q->d2 = d2; memcpy(q->cp, cp, 3 * sizeof(real)); cross3(e1, e2, q->cn); }
+  real den = e1[0] * e2[1] - e1[1] * e2[0];
+  if (FABS_R(den) > 1e-9f) {
+    real id = 1.0f / den;
+    real px = p[0] - a[0], py = p[1] - a[1];
+    real s = (px * e2[1] - py * e2[0]) * id, t = (e1[0] * py - e1[1] * px) * id;
     if (s >= -1e-6f && t >= -1e-6f && s + t <= 1.0f + 1e-6f) {
-      float hz = a[2] + s * e1[2] + t * e2[2];
+      real hz = a[2] + s * e1[2] + t * e2[2];
       if (hz > q->top) { q->top = hz; cross3(e1, e2, q->tn); }
     }
   }
@@ -231,10 +250,10 @@ static void tm_tri(tmq_t* q, const float* p, const float* a, const float* b, con
 
 /* signed depth of a sphere (radius r, centre p world) against the corrected mesh of the 3 x 3
  * cells around (i, j): nearest surface point, inside = below the surface under p */
-static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int j, float* n) {
+static real trimesh_depth(const ctx_t* cx, const real* p, real r, int i, int j, real* n) {
   const lgx_env_params* P = cx->p;
   const lgx_buffers* b = cx->b;
-  const float hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
+  const real hs = P->horizontal_scale, vs = P->vertical_scale, bo = P->border_size;
   const int rows = b->hf_rows, cols = b->hf_cols;
   { /* early out: more than r above every vertex of the 4 x 4 block */
     int hmax = -32768;
@@ -244,44 +263,44 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
         int h = b->height_samples[(int64_t)aa * cols + bc];
         if (h > hmax) hmax = h;
       }
-    if (p[2] - r > (float)hmax * vs) { v3(n, 0, 0, 1); return -1.0f; }
+    if (p[2] - r > (real)hmax * vs) { v3(n, 0, 0, 1); return -1.0f; }
   }
   /* frame at raw vertex (i, j): small coordinates (see the kernel) */
-  const float ox = (float)i * hs - bo, oy = (float)j * hs - bo;
-  float pl[3] = {p[0] - ox, p[1] - oy, p[2]};
+  const real ox = (real)i * hs - bo, oy = (real)j * hs - bo;
+  real pl[3] = {p[0] - ox, p[1] - oy, p[2]};
   p = pl;
   tmq_t q;
-  q.d2 = 3.0e38f; memcpy(q.cp, p, 12); v3(q.cn, 0, 0, 1);
+  q.d2 = 3.0e38f; memcpy(q.cp, p, 3 * sizeof(real)); v3(q.cn, 0, 0, 1);
   q.top = -3.0e38f; v3(q.tn, 0, 0, 1);
   for (int ci = i - 1 < 0 ? 0 : i - 1; ci <= (i + 1 < rows - 2 ? i + 1 : rows - 2); ++ci)
     for (int cj = j - 1 < 0 ? 0 : j - 1; cj <= (j + 1 < cols - 2 ? j + 1 : cols - 2); ++cj) {
-      float v[4][3];
+      real v[4][3];
       for (int k = 0; k < 4; ++k) {
         int a = ci + (k & 1), bb = cj + (k >> 1);
         int h = b->height_samples[(int64_t)a * cols + bb];
         int code = b->hf_trimesh[(int64_t)a * cols + bb] & 15;
         int dx = code / 3 - 1, dy = code % 3 - 1;
-        v3(v[k], (float)(a + dx - i) * hs, (float)(bb + dy - j) * hs, (float)h * vs);
+        v3(v[k], (real)(a + dx - i) * hs, (real)(bb + dy - j) * hs, (real)h * vs);
       }
-      float zmax = v[0][2], xmin = v[0][0], xmax = v[0][0], ymin = v[0][1], ymax = v[0][1];
+      real zmax = v[0][2], xmin = v[0][0], xmax = v[0][0], ymin = v[0][1], ymax = v[0][1];
       for (int k = 1; k < 4; ++k) {
-        zmax = fmaxf(zmax, v[k][2]);
-        xmin = fminf(xmin, v[k][0]); xmax = fmaxf(xmax, v[k][0]);
-        ymin = fminf(ymin, v[k][1]); ymax = fmaxf(ymax, v[k][1]);
+        zmax = FMAX_R(zmax, v[k][2]);
+        xmin = FMIN_R(xmin, v[k][0]); xmax = FMAX_R(xmax, v[k][0]);
+        ymin = FMIN_R(ymin, v[k][1]); ymax = FMAX_R(ymax, v[k][1]);
       }
       if (p[2] - r > zmax || p[0] < xmin - r || p[0] > xmax + r || p[1] < ymin - r || p[1] > ymax + r) continue;
       tm_tri(&q, p, v[0], v[3], v[2]);
       tm_tri(&q, p, v[0], v[1], v[3]);
     }
   int inside = p[2] < q.top;
-  float d = sqrtf(q.d2);
+  real d = SQRT_R(q.d2);
   if (d > 1e-7f) {
-    float inv = 1.0f / d;
+    real inv = 1.0f / d;
     for (int k = 0; k < 3; ++k) n[k] = inside ? inv * (q.cp[k] - p[k]) : inv * (p[k] - q.cp[k]);
   } else {
-    const float* c = q.top > -1e30f ? q.tn : q.cn;
-    float l = sqrtf(dot3(c, c));
-    float s = (c[2] < 0 ? -1.0f : 1.0f) / (l > 1e-30f ? l : 1e-30f);
+    const real* c = q.top > -1e30f ? q.tn : q.cn;
+    real l = SQRT_R(dot3(c, c));
+    real s = (c[2] < 0 ? -1.0f : 1.0f) / (l > 1e-30f ? l : 1e-30f);
     for (int k = 0; k < 3; ++k) n[k] = s * c[k];
   }
   return inside ? r + d : r - d;
@@ -290,33 +309,37 @@ static float trimesh_depth(const ctx_t* cx, const float* p, float r, int i, int 
 /* ground contact depth of a sphere / point: spheres (r > 0) against the corrected trimesh where the
  * contact table flags the cell; box corners (r = 0) and unflagged cells against the heightfield
  * triangle under p, depth along its face normal (the kernel's split) */
-static float ground_contact(const ctx_t* cx, const float* p, float r, float* n) {
+static real ground_contact(const ctx_t* cx, const real* p, real r, real* n) {
   const lgx_env_params* P = cx->p;
   const lgx_buffers* b = cx->b;
   if (r > 0.0f && b->hf_trimesh && P->terrain_kind != 0 && b->height_samples) {
-    const float ihs = 1.0f / P->horizontal_scale;
-    int i = (int)floorf((p[0] + P->border_size) * ihs);
-    int j = (int)floorf((p[1] + P->border_size) * ihs);
+    const real ihs = 1.0f / P->horizontal_scale;
+    int i = (int)FLOOR_R((p[0] + P->border_size) * ihs);
+    int j = (int)FLOOR_R((p[1] + P->border_size) * ihs);
     if (i < 0) i = 0; if (i > b->hf_rows - 2) i = b->hf_rows - 2;
     if (j < 0) j = 0; if (j > b->hf_cols - 2) j = b->hf_cols - 2;
     if (b->hf_trimesh[(int64_t)i * b->hf_cols + j] & 16) return trimesh_depth(cx, p, r, i, j, n);
   }
-  float h = ground(cx, p[0], p[1], n);
+  real h = ground(cx, p[0], p[1], n);
   return (h - p[2]) * n[2] + r;
 }
 
 /* test entry: ground_contact at world point p (radius r): depth, normal n[3] */
 float lgxo_ground_contact(const lgx_env_params* p, const lgx_buffers* b, const float* pt, float r, float* n) {
   ctx_t cx = {NULL, p, b, NULL, 0};
-  return ground_contact(&cx, pt, r, n);
+  real ptr[3], nr[3];
+  ldr(ptr, pt, 3);
+  real d = ground_contact(&cx, ptr, (real)r, nr);
+  for (int k = 0; k < 3; ++k) n[k] = (float)nr[k];
+  return (float)d;
 }
 
 /* ------------------------------------------------------------------ physics substep */
 typedef struct {
-  float R[LGX_NUM_DYN][9];  /* body rotation (world) */
-  float o[LGX_NUM_DYN][3];  /* body origin relative to base origin O */
-  float S[LGX_NUM_DOF][6];  /* joint motion subspace (ang; lin) at O */
-  float I6[LGX_NUM_DYN][36];
+  real R[LGX_NUM_DYN][9];  /* body rotation (world) */
+  real o[LGX_NUM_DYN][3];  /* body origin relative to base origin O */
+  real S[LGX_NUM_DOF][6];  /* joint motion subspace (ang; lin) at O */
+  real I6[LGX_NUM_DYN][36];
 } kin_t;
 
 static int chain_has(int body, int joint) { /* does body's kinematic chain contain joint? */
@@ -325,24 +348,25 @@ static int chain_has(int body, int joint) { /* does body's kinematic chain conta
   return joint / 3 == leg && joint % 3 <= k;
 }
 
-static void spatial_inertia(const lgx_model* m, int b, float scale, const float* R, const float* o, float* I6) {
+static void spatial_inertia(const lgx_model* m, int b, real scale, const real* R, const real* o, real* I6) {
   const float* in = m->body_inertia[b];
-  float Ib[9] = {in[0], in[3], in[4], in[3], in[1], in[5], in[4], in[5], in[2]};
-  float T[9], RT[9], Iw[9];
+  real Ib[9] = {in[0], in[3], in[4], in[3], in[1], in[5], in[4], in[5], in[2]};
+  real T[9], RT[9], Iw[9];
   for (int i = 0; i < 3; ++i) for (int j = 0; j < 3; ++j) RT[3 * i + j] = R[3 * j + i];
   matmul3(R, Ib, T); matmul3(T, RT, Iw);
-  float c[3]; matvec3(R, m->body_com[b], c);
+  real com[3]; ldr(com, m->body_com[b], 3);
+  real c[3]; matvec3(R, com, c);
   for (int i = 0; i < 3; ++i) c[i] += o[i];
-  float mass = m->body_mass[b] * scale;
+  real mass = m->body_mass[b] * scale;
   for (int i = 0; i < 9; ++i) Iw[i] *= scale;
-  float cc = dot3(c, c);
-  memset(I6, 0, 36 * sizeof(float));
+  real cc = dot3(c, c);
+  memset(I6, 0, 36 * sizeof(real));
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
       I6[i * 6 + j] = Iw[3 * i + j] + mass * ((i == j ? cc : 0.0f) - c[i] * c[j]);
       I6[(3 + i) * 6 + 3 + j] = (i == j) ? mass : 0.0f;
     }
-  float sk[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
+  real sk[9] = {0, -c[2], c[1], c[2], 0, -c[0], -c[1], c[0], 0};
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
       I6[i * 6 + 3 + j] = mass * sk[3 * i + j];
@@ -350,61 +374,61 @@ static void spatial_inertia(const lgx_model* m, int b, float scale, const float*
     }
 }
 
-static void crm(const float* V, const float* s, float* o) { /* V x_m s */
-  float a[3], l[3], t[3];
+static void crm(const real* V, const real* s, real* o) { /* V x_m s */
+  real a[3], l[3], t[3];
   cross3(V, s, a);
   cross3(V, s + 3, l); cross3(V + 3, s, t);
   o[0] = a[0]; o[1] = a[1]; o[2] = a[2];
   o[3] = l[0] + t[0]; o[4] = l[1] + t[1]; o[5] = l[2] + t[2];
 }
-static void crf(const float* V, const float* f, float* o) { /* V x_f f */
-  float a[3], b[3], l[3];
+static void crf(const real* V, const real* f, real* o) { /* V x_f f */
+  real a[3], b[3], l[3];
   cross3(V, f, a); cross3(V + 3, f + 3, b); cross3(V, f + 3, l);
   o[0] = a[0] + b[0]; o[1] = a[1] + b[1]; o[2] = a[2] + b[2];
   o[3] = l[0]; o[4] = l[1]; o[5] = l[2];
 }
-static void mv6(const float* M, const float* x, float* y) {
+static void mv6(const real* M, const real* x, real* y) {
   for (int i = 0; i < 6; ++i) {
-    float s = 0;
+    real s = 0;
     for (int j = 0; j < 6; ++j) s += M[i * 6 + j] * x[j];
     y[i] = s;
   }
 }
 
 /* body Jacobian column of generalized coordinate c for body b (6-vector, ang;lin) */
-static void body_jac_col(const kin_t* K, int b, int c, float* col) {
-  memset(col, 0, 6 * sizeof(float));
+static void body_jac_col(const kin_t* K, int b, int c, real* col) {
+  memset(col, 0, 6 * sizeof(real));
   if (c < 6) { col[c] = 1.0f; return; }
   int j = c - 6;
-  if (chain_has(b, j)) memcpy(col, K->S[j], 6 * sizeof(float));
+  if (chain_has(b, j)) memcpy(col, K->S[j], 6 * sizeof(real));
 }
 
 /* point Jacobian (3 x ND) of a point P (rel. O) on body b: v_P = v_lin + w x P */
-static void point_jac(const kin_t* K, int b, const float* P, float* J) {
-  memset(J, 0, 3 * ND * sizeof(float));
+static void point_jac(const kin_t* K, int b, const real* P, real* J) {
+  memset(J, 0, 3 * ND * sizeof(real));
   for (int c = 0; c < ND; ++c) {
-    float col[6]; body_jac_col(K, b, c, col);
-    float wxp[3]; cross3(col, P, wxp);
+    real col[6]; body_jac_col(K, b, c, col);
+    real wxp[3]; cross3(col, P, wxp);
     for (int r = 0; r < 3; ++r) J[r * ND + c] = col[3 + r] + wxp[r];
   }
 }
 
 typedef struct {
   int body, report;
-  float J[3 * ND];
-  float n[3];
-  float depth;
-  float mu;
+  real J[3 * ND];
+  real n[3];
+  real depth;
+  real mu;
   int status; /* 1 stick, 2 slide, 0 dropped */
-  float fslide[3];
+  real fslide[3];
 } contact_t;
 
-static void add_weighted_jtj(float* A, const float* J, const float* n, float wn, float wt) {
+static void add_weighted_jtj(real* A, const real* J, const real* n, real wn, real wt) {
   /* A += J^T (wn n n^T + wt (I - n n^T)) J */
-  float W[9];
+  real W[9];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) W[3 * i + j] = (wn - wt) * n[i] * n[j] + (i == j ? wt : 0.0f);
-  float WJ[3 * ND];
+  real WJ[3 * ND];
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < ND; ++c) WJ[r * ND + c] = W[3 * r] * J[c] + W[3 * r + 1] * J[ND + c] + W[3 * r + 2] * J[2 * ND + c];
   for (int a = 0; a < ND; ++a)
@@ -417,30 +441,32 @@ static void physics_env(const ctx_t* cx, int e) {
   const lgx_model* m = cx->m;
   const lgx_env_params* p = cx->p;
   const lgx_buffers* bf = cx->b;
-  const float dt = m->sim_dt;
+  const real dt = m->sim_dt;
   float* rs = bf->root_states + (int64_t)e * 13;
   float* ds = bf->dof_state + (int64_t)e * 24;
   const float* tgt = bf->dof_targets + (int64_t)e * 12;
-  float th[12], thd[12];
+  real th[12], thd[12];
   for (int j = 0; j < 12; ++j) { th[j] = ds[2 * j]; thd[j] = ds[2 * j + 1]; }
-  float u[ND];
+  real u[ND];
   u[0] = rs[10]; u[1] = rs[11]; u[2] = rs[12]; u[3] = rs[7]; u[4] = rs[8]; u[5] = rs[9];
   for (int j = 0; j < 12; ++j) u[6 + j] = thd[j];
 
   /* kinematics */
   kin_t K;
-  quat_to_mat(rs + 3, K.R[0]);
+  real q0[4]; ldr(q0, rs + 3, 4);
+  quat_to_mat(q0, K.R[0]);
   memset(K.o[0], 0, sizeof K.o[0]);
   for (int leg = 0; leg < 4; ++leg) {
     int pb = 0;
     for (int k = 0; k < 3; ++k) {
       int j = 3 * leg + k, b = 1 + j;
-      float Rjf[9], tmp[3];
-      matmul3(K.R[pb], m->joint_rot[j], Rjf);
-      matvec3(K.R[pb], m->joint_pos[j], tmp);
+      real Rjf[9], tmp[3], jrot[9], jpos[3], jax[3];
+      ldr(jrot, m->joint_rot[j], 9); ldr(jpos, m->joint_pos[j], 3); ldr(jax, m->joint_axis[j], 3);
+      matmul3(K.R[pb], jrot, Rjf);
+      matvec3(K.R[pb], jpos, tmp);
       for (int i = 0; i < 3; ++i) K.o[b][i] = K.o[pb][i] + tmp[i];
-      float aw[3]; matvec3(Rjf, m->joint_axis[j], aw);
-      float Rq[9]; axis_angle(m->joint_axis[j], th[j], Rq);
+      real aw[3]; matvec3(Rjf, jax, aw);
+      real Rq[9]; axis_angle(jax, th[j], Rq);
       matmul3(Rjf, Rq, K.R[b]);
       K.S[j][0] = aw[0]; K.S[j][1] = aw[1]; K.S[j][2] = aw[2];
       cross3(K.o[b], aw, K.S[j] + 3);
@@ -451,33 +477,33 @@ static void physics_env(const ctx_t* cx, int e) {
   for (int b = 0; b < LGX_NUM_DYN; ++b) spatial_inertia(m, b, mscale[b], K.R[b], K.o[b], K.I6[b]);
 
   /* mass matrix H = sum_b J_b^T I_b J_b (dense) */
-  float H[ND * ND];
+  real H[ND * ND];
   memset(H, 0, sizeof H);
   for (int b = 0; b < LGX_NUM_DYN; ++b) {
-    float Jb[6 * ND];
+    real Jb[6 * ND];
     for (int c = 0; c < ND; ++c) {
-      float col[6]; body_jac_col(&K, b, c, col);
+      real col[6]; body_jac_col(&K, b, c, col);
       for (int r = 0; r < 6; ++r) Jb[r * ND + c] = col[r];
     }
-    float IJ[6 * ND];
+    real IJ[6 * ND];
     for (int r = 0; r < 6; ++r)
       for (int c = 0; c < ND; ++c) {
-        float s = 0;
+        real s = 0;
         for (int k = 0; k < 6; ++k) s += K.I6[b][r * 6 + k] * Jb[k * ND + c];
         IJ[r * ND + c] = s;
       }
     for (int a = 0; a < ND; ++a)
       for (int c = 0; c < ND; ++c) {
-        float s = 0;
+        real s = 0;
         for (int k = 0; k < 6; ++k) s += Jb[k * ND + a] * IJ[k * ND + c];
         H[a * ND + c] += s;
       }
   }
 
   /* bias forces C = sum_b J_b^T (I_b A_b + V_b x* I_b V_b), A_0 = (0, -w x v - g) */
-  float V[LGX_NUM_DYN][6], A[LGX_NUM_DYN][6];
-  memcpy(V[0], u, 6 * sizeof(float));
-  float wxv[3]; cross3(u, u + 3, wxv);
+  real V[LGX_NUM_DYN][6], A[LGX_NUM_DYN][6];
+  memcpy(V[0], u, 6 * sizeof(real));
+  real wxv[3]; cross3(u, u + 3, wxv);
   A[0][0] = A[0][1] = A[0][2] = 0;
   for (int i = 0; i < 3; ++i) A[0][3 + i] = -wxv[i] - m->gravity[i];
   for (int leg = 0; leg < 4; ++leg) {
@@ -485,34 +511,34 @@ static void physics_env(const ctx_t* cx, int e) {
     for (int k = 0; k < 3; ++k) {
       int j = 3 * leg + k, b = 1 + j;
       for (int i = 0; i < 6; ++i) V[b][i] = V[pb][i] + K.S[j][i] * thd[j];
-      float c6[6]; crm(V[b], K.S[j], c6);
+      real c6[6]; crm(V[b], K.S[j], c6);
       for (int i = 0; i < 6; ++i) A[b][i] = A[pb][i] + c6[i] * thd[j];
       pb = b;
     }
   }
-  float Cb[ND];
+  real Cb[ND];
   memset(Cb, 0, sizeof Cb);
   for (int b = 0; b < LGX_NUM_DYN; ++b) {
-    float IA[6], IV[6], f[6], vf[6];
+    real IA[6], IV[6], f[6], vf[6];
     mv6(K.I6[b], A[b], IA); mv6(K.I6[b], V[b], IV); crf(V[b], IV, vf);
     for (int i = 0; i < 6; ++i) f[i] = IA[i] + vf[i];
     for (int c = 0; c < ND; ++c) {
-      float col[6]; body_jac_col(&K, b, c, col);
-      float s = 0;
+      real col[6]; body_jac_col(&K, b, c, col);
+      real s = 0;
       for (int i = 0; i < 6; ++i) s += col[i] * f[i];
       Cb[c] += s;
     }
   }
 
   /* joint drives / explicit torques, hard limits */
-  float g[ND]; memset(g, 0, sizeof g);
-  float Dimp[12]; int implicit_drive[12];
+  real g[ND]; memset(g, 0, sizeof g);
+  real Dimp[12]; int implicit_drive[12];
   for (int j = 0; j < 12; ++j) {
     Dimp[j] = 0; implicit_drive[j] = 0;
-    float eff = m->dof_effort[j];
+    real eff = m->dof_effort[j];
     if (p->control_type == LGX_CTRL_POS_DRIVE) {
-      float te = m->kp[j] * (tgt[j] - th[j]) - m->kd[j] * thd[j];
-      if (fabsf(te) <= eff) {
+      real te = m->kp[j] * (tgt[j] - th[j]) - m->kd[j] * thd[j];
+      if (FABS_R(te) <= eff) {
         implicit_drive[j] = 1;
         Dimp[j] += dt * (m->kd[j] + dt * m->kp[j]);
         g[6 + j] += m->kp[j] * (tgt[j] - th[j]);
@@ -536,18 +562,19 @@ static void physics_env(const ctx_t* cx, int e) {
   /* contacts (candidates = every primitive below the ground) */
   contact_t C[MAXC];
   int nc = 0;
-  float mu_env = bf->friction ? bf->friction[e] : 1.0f;
+  real mu_env = bf->friction ? bf->friction[e] : 1.0f;
   for (int i = 0; i < m->num_points; ++i) {
     int b = m->point_dyn[i];
-    float P[3]; matvec3(K.R[b], m->point_pos[i], P);
+    real ppos[3]; ldr(ppos, m->point_pos[i], 3);
+    real P[3]; matvec3(K.R[b], ppos, P);
     for (int k = 0; k < 3; ++k) P[k] += K.o[b][k];
-    float n[3];
-    const float Pw[3] = {P[0] + rs[0], P[1] + rs[1], P[2] + rs[2]};
-    float depth = ground_contact(cx, Pw, m->point_radius[i], n);
+    real n[3];
+    const real Pw[3] = {P[0] + rs[0], P[1] + rs[1], P[2] + rs[2]};
+    real depth = ground_contact(cx, Pw, m->point_radius[i], n);
     if (depth <= 0.0f) continue;
     contact_t* c = &C[nc++];
     c->body = b; c->report = m->point_report[i];
-    float Pc[3] = {P[0] - n[0] * m->point_radius[i], P[1] - n[1] * m->point_radius[i], P[2] - n[2] * m->point_radius[i]};
+    real Pc[3] = {P[0] - n[0] * m->point_radius[i], P[1] - n[1] * m->point_radius[i], P[2] - n[2] * m->point_radius[i]};
     point_jac(&K, b, Pc, c->J);
     memcpy(c->n, n, sizeof n);
     c->depth = depth;
@@ -555,26 +582,26 @@ static void physics_env(const ctx_t* cx, int e) {
     c->status = 1;
   }
 
-  float Hu[ND];
+  real Hu[ND];
   for (int a = 0; a < ND; ++a) {
-    float s = 0;
+    real s = 0;
     for (int c = 0; c < ND; ++c) s += H[a * ND + c] * u[c];
     Hu[a] = s;
   }
-  const float kn = m->contact_k, cn = m->contact_c, ct = m->friction_c;
-  float u2[ND];
+  const real kn = m->contact_k, cn = m->contact_c, ct = m->friction_c;
+  real u2[ND];
   for (int pass = 0; pass < 2; ++pass) {
-    float M[ND * ND], r[ND];
+    real M[ND * ND], r[ND];
     memcpy(M, H, sizeof M);
     for (int j = 0; j < 12; ++j) M[(6 + j) * ND + 6 + j] += Dimp[j];
     for (int a = 0; a < ND; ++a) r[a] = Hu[a] + dt * (g[a] - Cb[a]);
     for (int i = 0; i < nc; ++i) {
       contact_t* c = &C[i];
       if (c->status == 0) continue;
-      float wt = (pass == 0 || c->status == 1) ? dt * ct : 0.0f;
+      real wt = (pass == 0 || c->status == 1) ? dt * ct : 0.0f;
       add_weighted_jtj(M, c->J, c->n, dt * (cn + dt * kn), wt);
       for (int a = 0; a < ND; ++a) {
-        float jn = c->J[a] * c->n[0] + c->J[ND + a] * c->n[1] + c->J[2 * ND + a] * c->n[2];
+        real jn = c->J[a] * c->n[0] + c->J[ND + a] * c->n[1] + c->J[2 * ND + a] * c->n[2];
         r[a] += dt * kn * c->depth * jn;
         if (pass == 1 && c->status == 2)
           r[a] += dt * (c->J[a] * c->fslide[0] + c->J[ND + a] * c->fslide[1] + c->J[2 * ND + a] * c->fslide[2]);
@@ -585,20 +612,20 @@ static void physics_env(const ctx_t* cx, int e) {
     if (pass == 0) {
       for (int i = 0; i < nc; ++i) {
         contact_t* c = &C[i];
-        float vp[3];
+        real vp[3];
         for (int k = 0; k < 3; ++k) {
-          float s = 0;
+          real s = 0;
           for (int a = 0; a < ND; ++a) s += c->J[k * ND + a] * u2[a];
           vp[k] = s;
         }
-        float vn = dot3(vp, c->n);
-        float fn = kn * c->depth - (cn + dt * kn) * vn;
-        float vt[3] = {vp[0] - vn * c->n[0], vp[1] - vn * c->n[1], vp[2] - vn * c->n[2]};
-        float vtn = sqrtf(dot3(vt, vt));
+        real vn = dot3(vp, c->n);
+        real fn = kn * c->depth - (cn + dt * kn) * vn;
+        real vt[3] = {vp[0] - vn * c->n[0], vp[1] - vn * c->n[1], vp[2] - vn * c->n[2]};
+        real vtn = SQRT_R(dot3(vt, vt));
         if (fn <= 0.0f) c->status = 0;
         else if (ct * vtn > c->mu * fn) {
           c->status = 2;
-          float s = -c->mu * fn / vtn;
+          real s = -c->mu * fn / vtn;
           c->fslide[0] = s * vt[0]; c->fslide[1] = s * vt[1]; c->fslide[2] = s * vt[2];
         } else c->status = 1;
       }
@@ -611,18 +638,18 @@ static void physics_env(const ctx_t* cx, int e) {
   for (int i = 0; i < nc; ++i) {
     contact_t* c = &C[i];
     if (c->status == 0) continue;
-    float vp[3];
+    real vp[3];
     for (int k = 0; k < 3; ++k) {
-      float s = 0;
+      real s = 0;
       for (int a = 0; a < ND; ++a) s += c->J[k * ND + a] * u2[a];
       vp[k] = s;
     }
-    float vn = dot3(vp, c->n);
-    float fn = kn * c->depth - (cn + dt * kn) * vn;
+    real vn = dot3(vp, c->n);
+    real fn = kn * c->depth - (cn + dt * kn) * vn;
     if (fn < 0) fn = 0;
-    float f[3];
+    real f[3];
     for (int k = 0; k < 3; ++k) {
-      float ft = c->status == 1 ? -ct * (vp[k] - vn * c->n[k]) : c->fslide[k];
+      real ft = c->status == 1 ? -ct * (vp[k] - vn * c->n[k]) : c->fslide[k];
       f[k] = fn * c->n[k] + ft;
     }
     for (int k = 0; k < 3; ++k) cf[c->report * 3 + k] += f[k];
@@ -631,12 +658,12 @@ static void physics_env(const ctx_t* cx, int e) {
   /* joint outputs */
   float* tq = bf->torques + (int64_t)e * 12;
   for (int j = 0; j < 12; ++j) {
-    float qd = u2[6 + j];
-    float vl = m->dof_vel_limit[j];
+    real qd = u2[6 + j];
+    real vl = m->dof_vel_limit[j];
     if (vl > 0) { if (qd > vl) qd = vl; if (qd < -vl) qd = -vl; }
     if (p->control_type == LGX_CTRL_POS_DRIVE) {
-      float eff = m->dof_effort[j];
-      float t;
+      real eff = m->dof_effort[j];
+      real t;
       if (implicit_drive[j]) t = m->kp[j] * (tgt[j] - th[j] - dt * u2[6 + j]) - m->kd[j] * u2[6 + j];
       else t = m->kp[j] * (tgt[j] - th[j]) - m->kd[j] * thd[j];
       if (t > eff) t = eff; if (t < -eff) t = -eff;
@@ -646,19 +673,20 @@ static void physics_env(const ctx_t* cx, int e) {
     ds[2 * j + 1] = qd;
   }
   /* root integration (semi-implicit Euler; quaternion q' = q + dt/2 (w,0) x q, normalised) */
-  float w[3] = {u2[0], u2[1], u2[2]}, v[3] = {u2[3], u2[4], u2[5]};
-  for (int i = 0; i < 3; ++i) rs[i] += dt * v[i];
-  float* q = rs + 3;
-  float wq[3]; cross3(w, q, wq);
-  float dq[4] = {0.5f * (q[3] * w[0] + wq[0]), 0.5f * (q[3] * w[1] + wq[1]), 0.5f * (q[3] * w[2] + wq[2]),
+  real w[3] = {u2[0], u2[1], u2[2]}, v[3] = {u2[3], u2[4], u2[5]};
+  for (int i = 0; i < 3; ++i) rs[i] = (float)((real)rs[i] + dt * v[i]);
+  real q[4]; ldr(q, rs + 3, 4);
+  real wq[3]; cross3(w, q, wq);
+  real dq[4] = {0.5f * (q[3] * w[0] + wq[0]), 0.5f * (q[3] * w[1] + wq[1]), 0.5f * (q[3] * w[2] + wq[2]),
                  -0.5f * dot3(w, q)};
   for (int i = 0; i < 4; ++i) q[i] += dt * dq[i];
-  float qn = 1.0f / sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  for (int i = 0; i < 4; ++i) q[i] *= qn;
+  real qn = 1.0f / SQRT_R(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  for (int i = 0; i < 4; ++i) rs[3 + i] = (float)(q[i] * qn);
   rs[7] = v[0]; rs[8] = v[1]; rs[9] = v[2];
   rs[10] = w[0]; rs[11] = w[1]; rs[12] = w[2];
 }
 
+#ifndef LGXO_PHYSICS_ONLY   /* (the float64 build holds the physics alone) */
 /* ------------------------------------------------------------------ actuator history (Go1) */
 static void actuator_history(const ctx_t* cx, int e, int substep) {
   const lgx_env_params* p = cx->p;
@@ -710,12 +738,15 @@ void lgxo_explicit_torques(const lgx_env_params* p, const lgx_buffers* b) {
     }
 }
 
+#endif /* LGXO_PHYSICS_ONLY */
+
 void lgxo_simulate(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b, int n) {
   ctx_t cx = {m, p, b, NULL, 0};
   for (int s = 0; s < n; ++s)
     for (int e = 0; e < p->num_envs; ++e) physics_env(&cx, e);
 }
 
+#ifndef LGXO_PHYSICS_ONLY
 static void resample_cmd(const ctx_t* cx, int e, int slot, int64_t step, uint32_t tag) {
   const lgx_env_params* p = cx->p;
   float* c = cx->b->commands + (int64_t)e * 4;
@@ -1158,3 +1189,4 @@ void lgxo_actuator_lstm(const float* x, float* h, float* c, float* tau, int64_t 
     tau[r] = out_s[0] * s;
   }
 }
+#endif /* LGXO_PHYSICS_ONLY */

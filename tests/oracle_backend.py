@@ -14,8 +14,11 @@ import torch
 from legged_gym_amd.sim import abi
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liblgx_oracle.so")
+# LGX_ORACLE_SO: another build of the same oracle (tests/test_oracle_sanitize.py: the ASan/UBSan one)
+ORACLE_SO = os.environ.get("LGX_ORACLE_SO") or os.path.join(ROOT, "oracle", "liblgx_oracle.so")
+ORACLE64_SO = os.path.join(ROOT, "oracle", "liblgx_oracle64.so")
 _LIB = None
+_LIB64 = None
 
 
 def load_oracle():
@@ -48,6 +51,27 @@ def load_oracle():
     abi.check_layout(lib.lgxo_struct_sizes, n=3)
     _LIB = lib
     return lib
+
+
+def load_oracle64():
+    """The float64 build of the oracle's physics (oracle/Makefile: -DLGXO_REAL=double): the same
+    algorithm in double precision, the truth the physics tolerances are derived from."""
+    global _LIB64
+    if _LIB64 is None:
+        if not os.path.exists(ORACLE64_SO):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "liblgx_oracle64.so"])
+        lib = C.CDLL(ORACLE64_SO)
+        M, P, B = C.POINTER(abi.LgxModel), C.POINTER(abi.LgxEnvParams), C.POINTER(abi.LgxBuffers)
+        lib.lgxo_simulate.argtypes, lib.lgxo_simulate.restype = [M, P, B, C.c_int32], None
+        lib.lgxo_struct_sizes.argtypes, lib.lgxo_struct_sizes.restype = [C.POINTER(C.c_int64)], None
+        abi.check_layout(lib.lgxo_struct_sizes, n=3)
+        _LIB64 = lib
+    return _LIB64
+
+
+def simulate64(env, n):
+    """`n` physics substeps of an oracle-backed env in float64 arithmetic (state in its buffers)."""
+    load_oracle64().lgxo_simulate(*env._backend._args(), n)
 
 
 def vp(t):

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from oracle_backend import make_env
-from test_gpu_parity import close, randomize_state, sync
+from test_gpu_parity import PHYS_QTY, check_derived, close, float64_truth, randomize_state, sync
 
 pytestmark = pytest.mark.gpu
 
@@ -92,16 +92,24 @@ def test_full_size_subset_matches_oracle(gpu, task, n):
     a_sub = (torch.rand(64, 12, generator=gen) - 0.5) * 2
     a_full = torch.zeros(N, 12)
     a_full[idx] = a_sub
+    # the float64 truth of the step's physics: the step's clip + position targets, then 4 substeps
+    from oracle_backend import load_oracle
+    ora.actions.copy_(torch.clamp(a_sub, -ora.cfg.normalization.clip_actions, ora.cfg.normalization.clip_actions))
+    load_oracle().lgxo_compute_targets(*ora._backend._args())
+    t64 = float64_truth(ora, 4)
     ora.step(a_sub)
     dev.step(a_full.cuda())
     torch.cuda.synchronize()
     rd = dev.reset_buf[idx.cuda()].cpu()
     assert torch.equal(rd, ora.reset_buf)
     keep = ~rd
+    # physics of the envs that did not reset (post-physics leaves their state alone: no push at
+    # counter 100): HIP vs float64 within the derived tolerance of test_gpu_parity.check_derived
+    sub_dev = {k: f(dev)[idx.cuda()] for k, f in PHYS_QTY.items()}
+    check_derived(t64, {k: f(ora) for k, f in PHYS_QTY.items()}, sub_dev, keep=keep,
+                  qty=["root_pose", "root_vel", "dof_pos", "dof_vel", "torques", "contact_forces"])
     ok, e = close(dev.root_states[idx.cuda()][keep.cuda()], ora.root_states[keep], 2e-3, 2e-3)
     assert ok, f"root max err {e}"
-    ok, e = close(dev.dof_state.view(N, 12, 2)[idx.cuda()][keep.cuda()], ora.dof_state.view(64, 12, 2)[keep], 5e-3, 2e-3)
-    assert ok, f"dof max err {e}"
     ok, e = close(dev.rew_buf[idx.cuda()][keep.cuda()], ora.rew_buf[keep], 1e-4, 1e-3)
     assert ok, f"rew max err {e}"
     ok, e = close(dev.obs_buf[idx.cuda()][keep.cuda()], ora.obs_buf[keep], 5e-3, 5e-3)

@@ -152,3 +152,86 @@ def test_returned_obs_survive_the_next_step():
     assert obs1.data_ptr() != obs0.data_ptr()
     assert torch.equal(obs0, keep)
     assert torch.equal(env.get_observations(), obs1)
+
+
+def _pendulum_period(lib_simulate, kp, steps=700):
+    """Calf joint of leg 0 as a torsional pendulum: no gravity, the base made 1e6x heavier (a fixed
+    pivot), hip / thigh held by stiff implicit drives, the calf's implicit position drive with
+    stiffness kp and no damping as the spring.  Returns (measured period, discrete-map period,
+    continuous period 2 pi sqrt(I / kp)) in seconds."""
+    env = fresh(n=2)
+    m = env._backend.m
+    dt = float(m.sim_dt)
+    m.gravity[0] = m.gravity[1] = m.gravity[2] = 0.0
+    j = 2                                          # FL calf; dynamic body 1 + j
+    b = 1 + j
+    for k in range(12):
+        m.kp[k], m.kd[k] = (kp, 0.0) if k == j else (1e5, 50.0)
+    env.body_mass_scale[:, 0] = 1e6
+    env.root_states[:, :3] = torch.tensor([0.0, 0.0, 5.0])
+    env.root_states[:, 3:7] = torch.tensor([0, 0, 0, 1.0])
+    env.root_states[:, 7:] = 0
+    env.dof_pos[:] = env.default_dof_pos
+    env.dof_vel[:] = 0
+    env.target_poses[:] = env.default_dof_pos
+    th0 = float(env.default_dof_pos[0, j])
+    env.dof_pos[:, j] = th0 + 0.1
+    # effective inertia about the joint axis: axis^T I_com axis + m |axis x com|^2 (body frame)
+    a = np.array(m.joint_axis[j][:], np.float64)
+    I6 = np.array(m.body_inertia[b][:], np.float64)
+    Ib = np.array([[I6[0], I6[3], I6[4]], [I6[3], I6[1], I6[5]], [I6[4], I6[5], I6[2]]])
+    c = np.array(m.body_com[b][:], np.float64)
+    I_eff = a @ Ib @ a + float(m.body_mass[b]) * (c @ c - (a @ c) ** 2)
+    k = float(np.float32(kp)) / I_eff
+    # implicit drive, kd = 0: (I + dt^2 kp) v' = I v - dt kp th, th' = th + dt v' (DESIGN.md section 3)
+    al = 1.0 / (1.0 + dt * dt * k)
+    trace, det = 1.0 + al * (1.0 - dt * dt * k), al
+    phi = np.arccos(trace / (2.0 * np.sqrt(det)))
+    t_disc, t_cont = 2 * np.pi * dt / phi, 2 * np.pi / np.sqrt(k)
+    th = []
+    for _ in range(steps):
+        lib_simulate(env, 1)
+        th.append(float(env.dof_pos[0, j]) - th0)
+    th = np.array(th)
+    ups = [i + th[i] / (th[i] - th[i + 1]) for i in range(len(th) - 1) if th[i] < 0 <= th[i + 1]]
+    assert len(ups) >= 3, ups
+    t_meas = (ups[-1] - ups[0]) / (len(ups) - 1) * dt
+    return t_meas, t_disc, t_cont
+
+
+@pytest.mark.parametrize("build", ["f32", "f64"])
+def test_pendulum_period(build):
+    """SURVEY.md 8(c) known answer: a one-joint torsional pendulum oscillates with the period of
+    the integrator's own map (1e-4 in float32, 5e-5 in float64; measured 7e-6 - the residual is the
+    coupling to the stiffly held joints and the 1e6x base) and within 0.5 % of the continuous
+    2 pi sqrt(I / kp) (implicit Euler's phase lag: 0.13 % at omega dt = 0.063)."""
+    from oracle_backend import simulate64
+    sim = (lambda env, n: env.simulate(n)) if build == "f32" else simulate64
+    kp = 1.2
+    t_meas, t_disc, t_cont = _pendulum_period(sim, kp)
+    assert 0.3 < t_cont < 3.0, t_cont
+    tol = 1e-4 if build == "f32" else 5e-5
+    assert abs(t_meas / t_disc - 1) < tol, (t_meas, t_disc)
+    assert abs(t_meas / t_cont - 1) < 5e-3, (t_meas, t_cont)
+
+
+def test_float64_oracle_bounds_float32_error():
+    """The float64 physics build agrees with the float32 one to float32 rounding through the
+    ill-conditioned implicit solve (one env step = 4 substeps, rough terrain, 64 envs): velocities
+    to 2e-3 relative to their scale, contact forces to 0.05 N, and the two builds are not identical
+    (it is a different arithmetic, not a copy)."""
+    from oracle_backend import simulate64
+    from test_gpu_parity import randomize_state
+    env = make_env("go1_rough", num_envs=64, device="cpu", backend="oracle")
+    g = torch.Generator().manual_seed(3)
+    randomize_state(env, g)
+    s0 = {k: getattr(env, k).clone() for k in ("root_states", "dof_state")}
+    env.simulate(4)
+    f32 = (env.root_states.clone(), env.dof_state.clone(), env.contact_forces.clone())
+    env.root_states.copy_(s0["root_states"])
+    env.dof_state.copy_(s0["dof_state"])
+    simulate64(env, 4)
+    f64 = (env.root_states.clone(), env.dof_state.clone(), env.contact_forces.clone())
+    for a, b, tol in zip(f32, f64, (2e-3, 2e-3, 0.05)):
+        d = (a - b).abs().max().item()
+        assert 0 < d <= tol * max(1.0, b.abs().max().item() if tol < 0.01 else 1.0), d
