@@ -20,6 +20,6 @@ for i in 1 2; do
   for S in default 32,16,32; do
     if [[ $S == default ]]; then unset LGX_PPO_SPLITS; else export LGX_PPO_SPLITS=$S; fi
     timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no_cpu_baseline > gpurun_out/r04a_bench_${S}_$i.json 2> gpurun_out/r04a_bench.err || { echo "bench failed"; tail -20 gpurun_out/r04a_bench.err; exit 1; }
-    python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,4), round(d['ms_per_step'],3), d['last_iteration']['collection_time'], d['last_iteration']['learn_time'])" gpurun_out/r04a_bench_${S}_$i.json $S
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], round(d['value']/1e6,4), round(d['ms_per_step'],3), d['last_iteration']['collection_time'], d['last_iteration']['learn_time'])" gpurun_out/r04a_bench_${S}_$i.json $S
   done
 done
