@@ -130,6 +130,8 @@ WORKLOADS = {
     "go1_flat_bench": "C2 go1_flat_bench: Go1 flat, PD drive, no domain randomisation",
     "anymal_c_rough": "C5 anymal_c_rough: ANYmal-C trimesh curriculum terrain + 187-point height scan, friction/mass "
                       "randomisation, pushes",
+    "cassie": "cassie: the biped (2 legs x 6 joints, dense joint-space physics kernel) on trimesh curriculum terrain "
+              "+ 121-point height scan",
 }
 
 

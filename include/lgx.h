@@ -49,7 +49,9 @@ enum lgx_reward_term {
   LGX_R_ENERGY, LGX_R_DOF_VEL, LGX_R_DOF_ACC, LGX_R_ACTION_RATE, LGX_R_COLLISION,
   LGX_R_TERMINATION, LGX_R_DOF_POS_LIMITS, LGX_R_DOF_VEL_LIMITS, LGX_R_TORQUE_LIMITS,
   LGX_R_TRACKING_LIN_VEL, LGX_R_TRACKING_ANG_VEL, LGX_R_FEET_AIR_TIME, LGX_R_STUMBLE,
-  LGX_R_STAND_STILL, LGX_R_FEET_CONTACT_FORCES, LGX_R_HIP_MOTION, LGX_R_COUNT
+  LGX_R_STAND_STILL, LGX_R_FEET_CONTACT_FORCES, LGX_R_HIP_MOTION,
+  LGX_R_NO_FLY,  /* Cassie: exactly one foot with F_z > 0.1 N (envs/cassie/cassie.py:42-46) */
+  LGX_R_COUNT
 };
 
 /* control paths: position drive (the reference step path, legged_robot.py:93-96) or
@@ -71,9 +73,10 @@ enum lgx_control { LGX_CTRL_POS_DRIVE = 0, LGX_CTRL_P = 1, LGX_CTRL_V = 2, LGX_C
 #define LGX_DRAW_NOISE 32       /* num_obs: obs noise U[0,1) (legged_robot.py:231) */
 
 typedef struct lgx_model {
-  /* kinematic tree: 4 legs x 3 revolute joints; joint j = 3*leg + k, its parent is the
-   * base (k == 0) or dyn body 1 + 3*leg + k-1.  Joint frame = parent frame * (rot, pos);
-   * child body frame = joint frame * Rot(axis, q_j). */
+  /* kinematic tree: 12 revolute joints in serial leg chains of leg_dof joints off the base (4 x 3:
+   * the quadrupeds; 2 x 6: Cassie); joint j = leg_dof*leg + k moves dyn body 1 + j, its parent is
+   * the base (k == 0) or dyn body j (k > 0).  Joint frame = parent frame * (rot, pos); child body
+   * frame = joint frame * Rot(axis, q_j). */
   float joint_rot[LGX_NUM_DOF][9];
   float joint_pos[LGX_NUM_DOF][3];
   float joint_axis[LGX_NUM_DOF][3];
@@ -90,6 +93,9 @@ typedef struct lgx_model {
   /* contact primitives: sphere (radius > 0) or corner (radius 0) in dyn-body frame */
   int32_t num_points;
   int32_t num_report_bodies;
+  int32_t leg_dof;                  /* 3 (4 legs: the arrowhead physics kernel) or 6 (2 legs: the
+                                       dense physics kernel); 0 is read as 3 */
+  int32_t pad_model;
   float point_pos[LGX_MAX_POINTS][3];
   float point_radius[LGX_MAX_POINTS];
   int32_t point_dyn[LGX_MAX_POINTS];

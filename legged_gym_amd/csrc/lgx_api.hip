@@ -33,6 +33,7 @@ static int launch_check(int rc, const char* what) {
 
 struct lgx_sim {
   int device;
+  bool dense;             // physics on lgx_physics_dense_kernel (leg_dof 6 / LGX_PHYS_DENSE=1)
   lgx_env_params params;  // host copy
   lgx_buffers bufs;
   lgx_dev_model* d_model;
@@ -134,12 +135,21 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   if (params->curriculum && (!bufs->terrain_levels || !bufs->terrain_types || !bufs->terrain_origins))
     return fail(LGX_EINVAL, "lgx_sim_create: curriculum buffers are null");
 
+  // the dense joint-space kernel for the 2 x 6 biped (and, as an A/B and cross-check path, for any
+  // robot with LGX_PHYS_DENSE=1); the arrowhead kernel for the 4 x 3 quadrupeds
+  const int leg_dof = model->leg_dof == 0 ? 3 : model->leg_dof;
+  if (leg_dof != 3 && leg_dof != 6) return fail(LGX_EINVAL, "lgx_sim_create: leg_dof must be 3 or 6");
+  const char* force_dense = getenv("LGX_PHYS_DENSE");
+  const bool dense = leg_dof == 6 || (force_dense && atoi(force_dense) == 1);
+  if (dense && (params->control_type == LGX_CTRL_SEA || params->use_actuator_history))
+    return fail(LGX_EINVAL, "lgx_sim_create: the dense physics kernel has no SEA / actuator-history drive inputs");
   // per-lane contact candidate tables: leg points to their leg's lane, base points round-robin
   lgx_dev_model dm;
   memset(&dm, 0, sizeof dm);
   dm.m = *model;
+  dm.m.leg_dof = leg_dof;
   int rr = 0;
-  for (int i = 0; i < model->num_points; ++i) {
+  for (int i = 0; i < (dense ? 0 : model->num_points); ++i) {
     int d = model->point_dyn[i];
     int rep = model->point_report[i];
     if (d < 0 || d >= LGX_NUM_DYN) return fail(LGX_EINVAL, "lgx_sim_create: bad point_dyn");
@@ -161,6 +171,7 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   lgx_sim* s = new (std::nothrow) lgx_sim();
   if (!s) return fail(LGX_ENOMEM, "lgx_sim_create: out of host memory");
   s->device = device;
+  s->dense = dense;
   s->params = *params;
   s->bufs = *bufs;
   s->draws = nullptr;
@@ -241,21 +252,25 @@ int lgx_sync_aux(lgx_sim* s, void* stream) {
   return join_aux(s, (hipStream_t)stream);
 }
 
+// the physics launch of a sim: the arrowhead kernel, or the dense one (lgx_sim.dense)
+static int physics(lgx_sim* s, int32_t nsub, int32_t from_actions, const float* actions, hipStream_t st, int32_t frozen) {
+  return s->dense ? lgx_launch_physics_dense(s->d_model, s->d_params, s->bufs, s->params.num_envs, nsub, from_actions,
+                                             actions, st, frozen)
+                  : lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, nsub, from_actions, actions,
+                                       st, frozen);
+}
+
 int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
   if (!s || n < 0) return fail(LGX_EINVAL, "lgx_simulate: bad arguments");
   if (n == 0) return 0;
   if (int rc = join_aux(s, (hipStream_t)stream)) return rc;
-  return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, n, 0, nullptr,
-                                         (hipStream_t)stream),
-                      "lgx_simulate: physics launch");
+  return launch_check(physics(s, n, 0, nullptr, (hipStream_t)stream, 0), "lgx_simulate: physics launch");
 }
 
 int lgx_drive_inputs(lgx_sim* s, const float* actions, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_drive_inputs: null sim");
   if (int rc = join_aux(s, (hipStream_t)stream)) return rc;   // the last actuator net still reads model_ins
-  return launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, s->params.decimation, 1,
-                                         actions, (hipStream_t)stream, 1),
-                      "lgx_drive_inputs: launch");
+  return launch_check(physics(s, s->params.decimation, 1, actions, (hipStream_t)stream, 1), "lgx_drive_inputs: launch");
 }
 
 int lgx_ground_contact(lgx_sim* s, const float* points, int32_t n, float* out, void* stream) {
@@ -284,8 +299,7 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
   int rc = join_aux(s, st);  // the last actuator net still reads model_ins
   if (rc) return rc;
   arm(s, 0, sample);
-  rc = launch_check(lgx_launch_physics(s->d_model, s->d_params, s->bufs, p.num_envs, p.decimation, 1, actions, st),
-                    "lgx_step: physics launch");
+  rc = launch_check(physics(s, p.decimation, 1, actions, st, 0), "lgx_step: physics launch");
   if (rc) return rc;
   const bool act_net = p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel;
   const int mode = act_mode();

@@ -151,6 +151,11 @@ LGX_DEV float reward_term(const lgx_env_params* __restrict__ P, const EnvView& v
     case LGX_R_HIP_MOTION:
       for (int j = 0; j < 12; j += 3) s += fabsf(v.ds[2 * j] - P->default_dof_pos[j]);
       return s;
+    case LGX_R_NO_FLY: {  // Cassie (cassie.py:42-46): exactly one foot with F_z > 0.1 N
+      int n = 0;
+      for (int f = 0; f < P->num_feet; ++f) n += v.cf[3 * P->feet_indices[f] + 2] > 0.1f ? 1 : 0;
+      return n == 1 ? 1.f : 0.f;
+    }
   }
   return 0.f;
 }

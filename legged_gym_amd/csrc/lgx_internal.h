@@ -24,6 +24,10 @@ int lgx_physics_pp(int32_t n_envs);   // lanes per leg of the physics launch at 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                        int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
                        int32_t frozen = 0);
+// the dense joint-space kernel (lgx_physics.hip): leg_dof == 6 robots, or any with LGX_PHYS_DENSE=1
+int lgx_launch_physics_dense(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
+                             int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
+                             int32_t frozen);
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
                             int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
                             float* extras_snapshot, hipStream_t stream);

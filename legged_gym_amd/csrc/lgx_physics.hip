@@ -1352,6 +1352,529 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
 }
 
 
+// ============================================================================================
+// Dense joint-space physics (lgx_model.leg_dof == 6: Cassie's 2 legs x 6 joints, which the
+// arrowhead kernel's 4-leg x 3-joint lane mapping does not cover; any robot with LGX_PHYS_DENSE=1).
+// One env per wavefront (64-thread workgroup), the same model and algorithm as the oracle
+// (oracle/lgx_oracle.c physics_env: dense 18 x 18 H = sum_b J_b^T I_b J_b, RNEA bias, implicit PD
+// drives and limit springs, compliant contact with the two-pass stick / slide classification,
+// dense Cholesky), the work of every phase spread over the wave's lanes with the per-env arrays in
+// LDS: forward kinematics one lane per leg chain, spatial inertias / body forces one lane per body,
+// H / M one lane per matrix entry, contacts one lane per candidate point (ballot-compacted in point
+// order, so every sum over contacts runs in the oracle's order), the Cholesky columns one lane per
+// row.  Latency-bound like the arrowhead kernel (a serial chain of small dependent steps per env).
+// ============================================================================================
+namespace {
+
+constexpr int DN = 18;                     // generalised velocity [w(3), v(3), qd(12)]
+constexpr int DMAXC = LGX_MAX_POINTS;
+
+struct DenseLds {
+  float R[LGX_NUM_DYN][9], o[LGX_NUM_DYN][3], S[LGX_NUM_DOF][6], I6[LGX_NUM_DYN][36];
+  float H[DN * DN], M[DN * DN];
+  float V[LGX_NUM_DYN][6], A[LGX_NUM_DYN][6], F[LGX_NUM_DYN][6];
+  float Cb[DN], g[DN], Hu[DN], r[DN], u[DN], u2[DN];
+  float th[12], thd[12], tgt[12], tex[12], Dimp[12];
+  float root[13];
+  int impl[12];
+  int nc;
+  float cJ[DMAXC][3 * DN], cP[DMAXC][3], cn[DMAXC][3], cdepth[DMAXC], cmu[DMAXC], cfs[DMAXC][3], cf[DMAXC][3];
+  int cbody[DMAXC], creport[DMAXC], cstat[DMAXC];
+};
+
+// does dyn body `body`'s chain contain joint `joint` (legs of LD joints)
+LGX_DEV bool d_chain_has(int body, int joint, int LD) {
+  if (body == 0) return false;
+  const int leg = (body - 1) / LD, k = (body - 1) % LD;
+  return joint / LD == leg && joint % LD <= k;
+}
+
+// column c of body b's 6 x 18 Jacobian (ang; lin at the base origin)
+LGX_DEV void d_body_col(const DenseLds& L, int b, int c, int LD, float* col) {
+#pragma unroll
+  for (int i = 0; i < 6; ++i) col[i] = 0.f;
+  if (c < 6) { col[c] = 1.f; return; }
+  const int j = c - 6;
+  if (d_chain_has(b, j, LD))
+#pragma unroll
+    for (int i = 0; i < 6; ++i) col[i] = L.S[j][i];
+}
+
+LGX_DEV bool d_col_nonzero(int b, int c, int LD) { return c < 6 || d_chain_has(b, c - 6, LD); }
+
+LGX_DEV void d_crm(const float* V, const float* s, float* o) {   // V x_m s
+  const f3 a = cross(mk3(V[0], V[1], V[2]), mk3(s[0], s[1], s[2]));
+  const f3 l = cross(mk3(V[0], V[1], V[2]), mk3(s[3], s[4], s[5])) + cross(mk3(V[3], V[4], V[5]), mk3(s[0], s[1], s[2]));
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = l.x; o[4] = l.y; o[5] = l.z;
+}
+LGX_DEV void d_crf(const float* V, const float* f, float* o) {   // V x_f f
+  const f3 a = cross(mk3(V[0], V[1], V[2]), mk3(f[0], f[1], f[2])) + cross(mk3(V[3], V[4], V[5]), mk3(f[3], f[4], f[5]));
+  const f3 l = cross(mk3(V[0], V[1], V[2]), mk3(f[3], f[4], f[5]));
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = l.x; o[4] = l.y; o[5] = l.z;
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_model* __restrict__ DMg,
+                                                               const lgx_env_params* __restrict__ P, lgx_buffers B,
+                                                               int32_t nsub, int32_t from_actions,
+                                                               const float* __restrict__ act_src, int32_t frozen) {
+  __shared__ DenseLds L;
+  const lgx_model* __restrict__ M = &DMg->m;
+  const int lane = threadIdx.x;
+  const int e = blockIdx.x;
+  const int N = P->num_envs;
+  if (e >= N) return;
+  const int LD = M->leg_dof == 6 ? 6 : 3, NL = LGX_NUM_DOF / LD;
+  const int ctrl = P->control_type;
+  const float dt = M->sim_dt;
+  // ---- load: state, clipped actions, position targets (legged_robot.py:85-86, 394-397)
+  if (lane < 12) {
+    const int j = lane;
+    L.th[j] = B.dof_state[(int64_t)e * 24 + 2 * j];
+    L.thd[j] = B.dof_state[(int64_t)e * 24 + 2 * j + 1];
+    float a = 0.f;
+    if (from_actions) a = clampf(act_src[(int64_t)e * 12 + j], -P->clip_actions, P->clip_actions);
+    if (ctrl == LGX_CTRL_POS_DRIVE)
+      L.tgt[j] = from_actions ? clampf(a * P->action_scale + P->default_dof_pos[j], P->soft_lower[j], P->soft_upper[j])
+                              : B.dof_targets[(int64_t)e * 12 + j];
+    if (from_actions) {
+      B.actions[(int64_t)e * 12 + j] = a;
+      if (ctrl == LGX_CTRL_POS_DRIVE) B.dof_targets[(int64_t)e * 12 + j] = L.tgt[j];
+    }
+  }
+  if (lane < 13) L.root[lane] = B.root_states[(int64_t)e * 13 + lane];
+  if (frozen) return;
+  const float mu_env = B.friction ? B.friction[e] : 1.f;
+  const float kn = M->contact_k, cn = M->contact_c, ct = M->friction_c;
+  __syncthreads();
+
+  for (int s = 0; s < nsub; ++s) {
+    // ---- explicit torques (_compute_torques, legged_robot.py:370-392): caller-provided or P / V / T
+    if (lane < 12 && ctrl != LGX_CTRL_POS_DRIVE) {
+      const int j = lane;
+      float t;
+      if (!from_actions) t = B.torques[(int64_t)e * 12 + j];
+      else {
+        const float a = B.actions[(int64_t)e * 12 + j] * P->action_scale;
+        if (ctrl == LGX_CTRL_P) t = P->p_gains[j] * (a + P->default_dof_pos[j] - L.th[j]) - P->d_gains[j] * L.thd[j];
+        else if (ctrl == LGX_CTRL_V)
+          t = P->p_gains[j] * (a - L.thd[j]) - P->d_gains[j] * (L.thd[j] - B.last_dof_vel[(int64_t)e * 12 + j]) / dt;
+        else t = a;
+        t = clampf(t, -P->torque_limits[j], P->torque_limits[j]);
+      }
+      L.tex[j] = t;
+    }
+    if (lane < 6) {
+      L.u[lane] = lane < 3 ? L.root[10 + lane] : L.root[7 + lane - 3];
+    } else if (lane < DN) {
+      L.u[lane] = L.thd[lane - 6];
+    }
+    // ---- kinematics: one lane per leg chain
+    const m33 R0 = quat_to_mat(L.root[3], L.root[4], L.root[5], L.root[6]);
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 9; ++i) L.R[0][i] = R0.a[i];
+      L.o[0][0] = L.o[0][1] = L.o[0][2] = 0.f;
+    }
+    if (lane < NL) {
+      m33 Rp = R0;
+      f3 op = mk3(0.f, 0.f, 0.f);
+      for (int k = 0; k < LD; ++k) {
+        const int j = LD * lane + k, b = 1 + j;
+        m33 Jr;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Jr.a[i] = M->joint_rot[j][i];
+        const m33 Rjf = mul(Rp, Jr);
+        const f3 ob = op + mul(Rp, mk3(M->joint_pos[j][0], M->joint_pos[j][1], M->joint_pos[j][2]));
+        const f3 ax = mk3(M->joint_axis[j][0], M->joint_axis[j][1], M->joint_axis[j][2]);
+        const f3 aw = mul(Rjf, ax);
+        const m33 Rb = mul(Rjf, axis_angle(ax, L.th[j]));
+        const f3 ow = cross(ob, aw);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) L.R[b][i] = Rb.a[i];
+        L.o[b][0] = ob.x; L.o[b][1] = ob.y; L.o[b][2] = ob.z;
+        L.S[j][0] = aw.x; L.S[j][1] = aw.y; L.S[j][2] = aw.z;
+        L.S[j][3] = ow.x; L.S[j][4] = ow.y; L.S[j][5] = ow.z;
+        Rp = Rb;
+        op = ob;
+      }
+    }
+    __syncthreads();
+    // ---- spatial inertias at the base origin: one lane per body (oracle spatial_inertia)
+    if (lane < LGX_NUM_DYN) {
+      const int b = lane;
+      const float* in = M->body_inertia[b];
+      const float scale = B.body_mass_scale[(int64_t)e * LGX_NUM_DYN + b];
+      m33 R, Ib;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) R.a[i] = L.R[b][i];
+      Ib.a[0] = in[0]; Ib.a[1] = in[3]; Ib.a[2] = in[4]; Ib.a[3] = in[3]; Ib.a[4] = in[1]; Ib.a[5] = in[5];
+      Ib.a[6] = in[4]; Ib.a[7] = in[5]; Ib.a[8] = in[2];
+      m33 RT;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) RT.a[3 * i + j] = R.a[3 * j + i];
+      m33 Iw = mul(mul(R, Ib), RT);
+      const f3 c = mul(R, mk3(M->body_com[b][0], M->body_com[b][1], M->body_com[b][2])) +
+                   mk3(L.o[b][0], L.o[b][1], L.o[b][2]);
+      const float mass = M->body_mass[b] * scale;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Iw.a[i] *= scale;
+      const float cc = dot(c, c);
+      const float cv[3] = {c.x, c.y, c.z};
+      float* I6 = L.I6[b];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          I6[i * 6 + j] = Iw.a[3 * i + j] + mass * ((i == j ? cc : 0.f) - cv[i] * cv[j]);
+          I6[(3 + i) * 6 + 3 + j] = i == j ? mass : 0.f;
+        }
+      const float sk[9] = {0.f, -c.z, c.y, c.z, 0.f, -c.x, -c.y, c.x, 0.f};
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          I6[i * 6 + 3 + j] = mass * sk[3 * i + j];
+          I6[(3 + i) * 6 + j] = mass * sk[3 * j + i];
+        }
+    } else if (lane >= 32 && lane < 32 + NL) {
+      // ---- RNEA velocities / accelerations along each leg chain (A_0 = (0, -w x v - g))
+      const int leg = lane - 32;
+      float Vp[6], Ap[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Vp[i] = L.u[i];
+      const f3 wxv = cross(mk3(L.u[0], L.u[1], L.u[2]), mk3(L.u[3], L.u[4], L.u[5]));
+      Ap[0] = Ap[1] = Ap[2] = 0.f;
+      Ap[3] = -wxv.x - M->gravity[0]; Ap[4] = -wxv.y - M->gravity[1]; Ap[5] = -wxv.z - M->gravity[2];
+      if (leg == 0)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { L.V[0][i] = Vp[i]; L.A[0][i] = Ap[i]; }
+      for (int k = 0; k < LD; ++k) {
+        const int j = LD * leg + k, b = 1 + j;
+        float Sj[6], c6[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { Sj[i] = L.S[j][i]; Vp[i] = Vp[i] + Sj[i] * L.thd[j]; }
+        d_crm(Vp, Sj, c6);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) { Ap[i] = Ap[i] + c6[i] * L.thd[j]; L.V[b][i] = Vp[i]; L.A[b][i] = Ap[i]; }
+      }
+    }
+    __syncthreads();
+    // ---- H = sum_b J_b^T I_b J_b (all 324 entries; the Cholesky reads the lower triangle, H u
+    // the whole matrix) and the body forces f_b = I_b A_b + V_b x* I_b V_b
+    for (int q = lane; q < DN * DN; q += 64) {
+      const int a = q / DN, c = q % DN;
+      float h = 0.f;
+      for (int b = 0; b < LGX_NUM_DYN; ++b) {
+        if (!d_col_nonzero(b, a, LD) || !d_col_nonzero(b, c, LD)) continue;
+        float ca[6], cc[6];
+        d_body_col(L, b, a, LD, ca);
+        d_body_col(L, b, c, LD, cc);
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+          float ij = 0.f;
+#pragma unroll
+          for (int m = 0; m < 6; ++m) ij += L.I6[b][k * 6 + m] * cc[m];
+          sum += ca[k] * ij;
+        }
+        h += sum;
+      }
+      L.H[q] = h;
+    }
+    if (lane < LGX_NUM_DYN) {
+      const int b = lane;
+      float IA[6], IV[6], vf[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        float x = 0.f, y = 0.f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) { x += L.I6[b][i * 6 + j] * L.A[b][j]; y += L.I6[b][i * 6 + j] * L.V[b][j]; }
+        IA[i] = x; IV[i] = y;
+      }
+      d_crf(L.V[b], IV, vf);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) L.F[b][i] = IA[i] + vf[i];
+    }
+    // ---- drives (implicit PD while within the effort limit) and hard-limit springs
+    if (lane < 12) {
+      const int j = lane;
+      float gj = 0.f, dimp = 0.f;
+      int impl = 0;
+      const float eff = M->dof_effort[j];
+      const float th = L.th[j], thd = L.thd[j];
+      if (ctrl == LGX_CTRL_POS_DRIVE) {
+        const float te = M->kp[j] * (L.tgt[j] - th) - M->kd[j] * thd;
+        if (fabsf(te) <= eff) {
+          impl = 1;
+          dimp += dt * (M->kd[j] + dt * M->kp[j]);
+          gj += M->kp[j] * (L.tgt[j] - th);
+        } else {
+          gj += te > 0.f ? eff : -eff;
+        }
+      } else {
+        gj += L.tex[j];
+      }
+      if (M->dof_lower[j] < M->dof_upper[j]) {
+        if (th < M->dof_lower[j]) {
+          dimp += dt * (M->limit_c + dt * M->limit_k);
+          gj += M->limit_k * (M->dof_lower[j] - th);
+        } else if (th > M->dof_upper[j]) {
+          dimp += dt * (M->limit_c + dt * M->limit_k);
+          gj -= M->limit_k * (th - M->dof_upper[j]);
+        }
+      }
+      L.g[6 + j] = gj;
+      L.Dimp[j] = dimp;
+      L.impl[j] = impl;
+    } else if (lane < 18) {
+      L.g[lane - 12] = 0.f;
+    }
+    // ---- contact candidates: one lane per point, compacted in point order
+    if (lane == 0) L.nc = 0;
+    __syncthreads();
+    const int npts = M->num_points;
+    for (int i0 = 0; i0 < npts; i0 += 64) {
+      const int i = i0 + lane;
+      bool hit = false;
+      f3 Pc, n;
+      float depth = 0.f;
+      int b = 0;
+      if (i < npts) {
+        b = M->point_dyn[i];
+        m33 R;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R.a[k] = L.R[b][k];
+        const f3 Pp = mul(R, mk3(M->point_pos[i][0], M->point_pos[i][1], M->point_pos[i][2])) +
+                      mk3(L.o[b][0], L.o[b][1], L.o[b][2]);
+        const float rad = M->point_radius[i];
+        depth = ground_contact(P, B, Pp + mk3(L.root[0], L.root[1], L.root[2]), rad, &n, nullptr, 0, 0);
+        hit = depth > 0.f;
+        Pc = Pp - rad * n;
+      }
+      const uint64_t mask = __ballot(hit);
+      const int base = L.nc;
+      if (hit) {
+        const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
+        L.cbody[slot] = b;
+        L.creport[slot] = M->point_report[i];
+        L.cP[slot][0] = Pc.x; L.cP[slot][1] = Pc.y; L.cP[slot][2] = Pc.z;
+        L.cn[slot][0] = n.x; L.cn[slot][1] = n.y; L.cn[slot][2] = n.z;
+        L.cdepth[slot] = depth;
+        L.cmu[slot] = 0.5f * (mu_env + M->ground_friction);
+        L.cstat[slot] = 1;
+      }
+      __syncthreads();
+      if (lane == 0) L.nc = base + __popcll(mask);
+      __syncthreads();
+    }
+    const int nc = L.nc;
+    // contact point Jacobians (3 x 18): v_P = v_lin + w x P, one lane per (contact, column)
+    for (int q = lane; q < nc * DN; q += 64) {
+      const int i = q / DN, c = q % DN;
+      float col[6];
+      d_body_col(L, L.cbody[i], c, LD, col);
+      const f3 wxp = cross(mk3(col[0], col[1], col[2]), mk3(L.cP[i][0], L.cP[i][1], L.cP[i][2]));
+      L.cJ[i][c] = col[3] + wxp.x;
+      L.cJ[i][DN + c] = col[4] + wxp.y;
+      L.cJ[i][2 * DN + c] = col[5] + wxp.z;
+    }
+    __syncthreads();
+    // C (bias) and H u
+    if (lane < DN) {
+      const int c = lane;
+      float cb = 0.f, hu = 0.f;
+      for (int b = 0; b < LGX_NUM_DYN; ++b) {
+        if (!d_col_nonzero(b, c, LD)) continue;
+        float col[6];
+        d_body_col(L, b, c, LD, col);
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) sum += col[i] * L.F[b][i];
+        cb += sum;
+      }
+      for (int k = 0; k < DN; ++k) hu += L.H[c * DN + k] * L.u[k];
+      L.Cb[c] = cb;
+      L.Hu[c] = hu;
+    }
+    __syncthreads();
+    // ---- two passes: all penetrating points sticking, then sliding points as Coulomb forces
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int q = lane; q < DN * DN; q += 64) {     // lower triangle + diagonal of M
+        const int a = q / DN, c = q % DN;
+        if (c > a) continue;
+        float m = L.H[q];
+        if (a == c && a >= 6) m += L.Dimp[a - 6];
+        for (int i = 0; i < nc; ++i) {
+          if (L.cstat[i] == 0) continue;
+          const float wt = (pass == 0 || L.cstat[i] == 1) ? dt * ct : 0.f;
+          const float wn = dt * (cn + dt * kn);
+          const float* J = L.cJ[i];
+          const float nv[3] = {L.cn[i][0], L.cn[i][1], L.cn[i][2]};
+          float WJ[3];
+#pragma unroll
+          for (int rr = 0; rr < 3; ++rr) {
+            float w0 = (wn - wt) * nv[rr] * nv[0] + (rr == 0 ? wt : 0.f);
+            float w1 = (wn - wt) * nv[rr] * nv[1] + (rr == 1 ? wt : 0.f);
+            float w2 = (wn - wt) * nv[rr] * nv[2] + (rr == 2 ? wt : 0.f);
+            WJ[rr] = w0 * J[c] + w1 * J[DN + c] + w2 * J[2 * DN + c];
+          }
+          m += J[a] * WJ[0] + J[DN + a] * WJ[1] + J[2 * DN + a] * WJ[2];
+        }
+        L.M[q] = m;
+      }
+      if (lane < DN) {
+        const int a = lane;
+        float rv = L.Hu[a] + dt * (L.g[a] - L.Cb[a]);
+        for (int i = 0; i < nc; ++i) {
+          if (L.cstat[i] == 0) continue;
+          const float* J = L.cJ[i];
+          const float jn = J[a] * L.cn[i][0] + J[DN + a] * L.cn[i][1] + J[2 * DN + a] * L.cn[i][2];
+          rv += dt * kn * L.cdepth[i] * jn;
+          if (pass == 1 && L.cstat[i] == 2)
+            rv += dt * (J[a] * L.cfs[i][0] + J[DN + a] * L.cfs[i][1] + J[2 * DN + a] * L.cfs[i][2]);
+        }
+        L.r[a] = rv;
+      }
+      __syncthreads();
+      // Cholesky (lower), one lane per row of each column
+      for (int j = 0; j < DN; ++j) {
+        float sjj = L.M[j * DN + j];
+        for (int k = 0; k < j; ++k) sjj -= L.M[j * DN + k] * L.M[j * DN + k];
+        const float d = sqrtf(sjj > 1e-20f ? sjj : 1e-20f);
+        const int i = lane;
+        float t = 0.f;
+        if (i > j && i < DN) {
+          t = L.M[i * DN + j];
+          for (int k = 0; k < j; ++k) t -= L.M[i * DN + k] * L.M[j * DN + k];
+        }
+        __syncthreads();
+        if (lane == j) L.M[j * DN + j] = d;
+        if (i > j && i < DN) L.M[i * DN + j] = t / d;
+        __syncthreads();
+      }
+      if (lane == 0) {
+        float x[DN];
+        for (int i = 0; i < DN; ++i) {
+          float t = L.r[i];
+          for (int k = 0; k < i; ++k) t -= L.M[i * DN + k] * x[k];
+          x[i] = t / L.M[i * DN + i];
+        }
+        for (int i = DN - 1; i >= 0; --i) {
+          float t = x[i];
+          for (int k = i + 1; k < DN; ++k) t -= L.M[k * DN + i] * x[k];
+          x[i] = t / L.M[i * DN + i];
+        }
+        for (int i = 0; i < DN; ++i) L.u2[i] = x[i];
+      }
+      __syncthreads();
+      if (pass == 0) {   // classify: separating, sliding (Coulomb cone), sticking
+        for (int i = lane; i < nc; i += 64) {
+          const float* J = L.cJ[i];
+          float vp[3];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            float sv = 0.f;
+            for (int a = 0; a < DN; ++a) sv += J[k * DN + a] * L.u2[a];
+            vp[k] = sv;
+          }
+          const f3 nn = mk3(L.cn[i][0], L.cn[i][1], L.cn[i][2]);
+          const float vn = vp[0] * nn.x + vp[1] * nn.y + vp[2] * nn.z;
+          const float fn = kn * L.cdepth[i] - (cn + dt * kn) * vn;
+          const float vt[3] = {vp[0] - vn * nn.x, vp[1] - vn * nn.y, vp[2] - vn * nn.z};
+          const float vtn = sqrtf(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
+          if (fn <= 0.f) L.cstat[i] = 0;
+          else if (ct * vtn > L.cmu[i] * fn) {
+            L.cstat[i] = 2;
+            const float sc = -L.cmu[i] * fn / vtn;
+            L.cfs[i][0] = sc * vt[0]; L.cfs[i][1] = sc * vt[1]; L.cfs[i][2] = sc * vt[2];
+          } else L.cstat[i] = 1;
+        }
+        __syncthreads();
+      }
+    }
+    // ---- reported contact forces (net force per reporting body, the last substep's)
+    for (int i = lane; i < nc; i += 64) {
+      float f[3] = {0.f, 0.f, 0.f};
+      if (L.cstat[i] != 0) {
+        const float* J = L.cJ[i];
+        float vp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          float sv = 0.f;
+          for (int a = 0; a < DN; ++a) sv += J[k * DN + a] * L.u2[a];
+          vp[k] = sv;
+        }
+        const float vn = vp[0] * L.cn[i][0] + vp[1] * L.cn[i][1] + vp[2] * L.cn[i][2];
+        float fn = kn * L.cdepth[i] - (cn + dt * kn) * vn;
+        if (fn < 0.f) fn = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float ft = L.cstat[i] == 1 ? -ct * (vp[k] - vn * L.cn[i][k]) : L.cfs[i][k];
+          f[k] = fn * L.cn[i][k] + ft;
+        }
+      }
+      L.cf[i][0] = f[0]; L.cf[i][1] = f[1]; L.cf[i][2] = f[2];
+    }
+    __syncthreads();
+    if (s == nsub - 1 && lane < LGX_MAX_BODIES) {   // (every substep's would be overwritten)
+      float f[3] = {0.f, 0.f, 0.f};
+      for (int i = 0; i < nc; ++i)
+        if (L.creport[i] == lane) { f[0] += L.cf[i][0]; f[1] += L.cf[i][1]; f[2] += L.cf[i][2]; }
+      float* cfo = B.contact_forces + ((int64_t)e * LGX_MAX_BODIES + lane) * 3;
+      cfo[0] = f[0]; cfo[1] = f[1]; cfo[2] = f[2];
+    }
+    // ---- joint outputs and the root (semi-implicit Euler, quaternion renormalised)
+    if (lane < 12) {
+      const int j = lane;
+      float qd = L.u2[6 + j];
+      const float vl = M->dof_vel_limit[j];
+      if (vl > 0.f) qd = clampf(qd, -vl, vl);
+      if (ctrl == LGX_CTRL_POS_DRIVE && s == nsub - 1) {
+        const float eff = M->dof_effort[j];
+        float t;
+        if (L.impl[j]) t = M->kp[j] * (L.tgt[j] - L.th[j] - dt * L.u2[6 + j]) - M->kd[j] * L.u2[6 + j];
+        else t = M->kp[j] * (L.tgt[j] - L.th[j]) - M->kd[j] * L.thd[j];
+        B.torques[(int64_t)e * 12 + j] = clampf(t, -eff, eff);
+      }
+      L.th[j] = L.th[j] + dt * qd;
+      L.thd[j] = qd;
+    } else if (lane == 32) {
+      const f3 w = mk3(L.u2[0], L.u2[1], L.u2[2]), v = mk3(L.u2[3], L.u2[4], L.u2[5]);
+      L.root[0] += dt * v.x; L.root[1] += dt * v.y; L.root[2] += dt * v.z;
+      const f3 q = mk3(L.root[3], L.root[4], L.root[5]);
+      const float qw = L.root[6];
+      const f3 wq = cross(w, q);
+      float dq[4] = {0.5f * (qw * w.x + wq.x), 0.5f * (qw * w.y + wq.y), 0.5f * (qw * w.z + wq.z), -0.5f * dot(w, q)};
+      float qq[4] = {q.x + dt * dq[0], q.y + dt * dq[1], q.z + dt * dq[2], qw + dt * dq[3]};
+      const float qn = 1.0f / sqrtf(qq[0] * qq[0] + qq[1] * qq[1] + qq[2] * qq[2] + qq[3] * qq[3]);
+      L.root[3] = qq[0] * qn; L.root[4] = qq[1] * qn; L.root[5] = qq[2] * qn; L.root[6] = qq[3] * qn;
+      L.root[7] = v.x; L.root[8] = v.y; L.root[9] = v.z;
+      L.root[10] = w.x; L.root[11] = w.y; L.root[12] = w.z;
+    }
+    __syncthreads();
+  }
+  // ---- write back
+  if (lane < 12) {
+    B.dof_state[(int64_t)e * 24 + 2 * lane] = L.th[lane];
+    B.dof_state[(int64_t)e * 24 + 2 * lane + 1] = L.thd[lane];
+    if (ctrl != LGX_CTRL_POS_DRIVE && nsub > 0) B.torques[(int64_t)e * 12 + lane] = L.tex[lane];
+  }
+  if (lane < 13) B.root_states[(int64_t)e * 13 + lane] = L.root[lane];
+}
+
+int lgx_launch_physics_dense(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
+                             int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
+                             int32_t frozen) {
+  if (!act_src) act_src = b.actions;
+  LGX_LAUNCH(lgx_physics_dense_kernel, dim3(n_envs), dim3(64), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+
 #ifdef LGX_PHASE_CLOCK_BUF
 // instrumented builds only (tools/phase_clock.sh): the per-workgroup clock table of the last physics launch
 extern "C" int lgx_debug_clock(unsigned long long* out, int32_t nblocks) {

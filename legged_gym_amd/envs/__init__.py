@@ -2,8 +2,8 @@
 
 go1 (configs C1/C2 defaults), go1_rough (C3/C4: trimesh + height scan), go1_flat_bench (C2 as
 BASELINE states it: PD, no domain randomisation), anymal_c_rough (C5), anymal_c_flat, and the
-remaining quadrupeds of the reference registry: anymal_b, a1, a1_src, aliengo.  (cassie, the
-biped, is outside the 4-leg x 3-DoF model: SURVEY.md §8(f).)
+remaining robots of the reference registry: anymal_b, a1, a1_src, aliengo and cassie (the biped:
+2 legs x 6 joints on the dense physics kernel).
 """
 from legged_gym_amd import LEGGED_GYM_ENVS_DIR, LEGGED_GYM_ROOT_DIR  # noqa: F401
 from legged_gym_amd.utils.task_registry import task_registry
@@ -15,6 +15,8 @@ from .anymal_b.anymal_b_config import AnymalBRoughCfg, AnymalBRoughCfgPPO
 from .anymal_c.anymal import Anymal
 from .anymal_c.anymal_c_config import AnymalCFlatCfg, AnymalCFlatCfgPPO, AnymalCRoughCfg, AnymalCRoughCfgPPO
 from .base.legged_robot import LeggedRobot
+from .cassie.cassie import Cassie
+from .cassie.cassie_config import CassieRoughCfg, CassieRoughCfgPPO
 from .base.legged_robot_config import LeggedRobotCfg, LeggedRobotCfgPPO
 from .go1.go1 import Go1
 from .go1.go1_config import Go1FlatBenchCfg, Go1RoughCfg, Go1RoughCfgPPO, Go1RoughTerrainCfg
@@ -28,3 +30,4 @@ task_registry.register("anymal_b", Anymal, AnymalBRoughCfg(), AnymalBRoughCfgPPO
 task_registry.register("a1", LeggedRobot, A1RoughCfg(), A1RoughCfgPPO())
 task_registry.register("a1_src", LeggedRobot, A1SrcRoughCfg(), A1SrcRoughCfgPPO())
 task_registry.register("aliengo", Aliengo, AliengoRoughCfg(), AliengoRoughCfgPPO())
+task_registry.register("cassie", Cassie, CassieRoughCfg(), CassieRoughCfgPPO())

@@ -343,7 +343,9 @@ class LeggedRobot(BaseTask):
         self.last_root_vel = torch.zeros(N, 6, **f)
         self.commands = torch.zeros(N, self.cfg.commands.num_commands, **f)
         self.commands_scale = torch.tensor([self.obs_scales.lin_vel, self.obs_scales.lin_vel, self.obs_scales.ang_vel], **f)
-        self.feet_air_time = torch.zeros(N, self.feet_indices.shape[0], **f)
+        # the kernels keep 4 slots per env (lgx.h feet_air_time [N,4]); the biped uses the first 2
+        self._feet_air_time_full = torch.zeros(N, 4, **f)
+        self.feet_air_time = self._feet_air_time_full[:, :self.feet_indices.shape[0]]
         self.last_contacts = torch.zeros(N, len(self.feet_indices), dtype=torch.bool, device=dev)
         self.base_lin_vel = quat_rotate_inverse(self.base_quat, self.root_states[:, 7:10]).contiguous()
         self.base_ang_vel = quat_rotate_inverse(self.base_quat, self.root_states[:, 10:13]).contiguous()
@@ -406,7 +408,9 @@ class LeggedRobot(BaseTask):
             self.reward_names.append(name)
         rows = self.reward_names + (["termination"] if "termination" in self.reward_scales else [])
         self._episode_sums_buf = torch.zeros(max(len(rows), 1), self.num_envs, dtype=torch.float, device=self.device)
-        self.episode_sums = {name: self._episode_sums_buf[i] for i, name in enumerate(rows)}
+        # dict keys in the reference's order (reward_scales: alphabetical, "termination" in its place,
+        # legged_robot.py:596-597); buffer rows: the terms in evaluation order, then termination
+        self.episode_sums = {name: self._episode_sums_buf[rows.index(name)] for name in self.reward_scales}
         # extras rows: one per episode-sum row (alphabetical key order as the reference dict)
         T = len(rows)
         self._extras_buf = torch.zeros(T + 2, dtype=torch.float, device=self.device)
@@ -511,7 +515,7 @@ class LeggedRobot(BaseTask):
                          ("last_actions", self.last_actions), ("last_dof_vel", self.last_dof_vel),
                          ("last_root_vel", self.last_root_vel), ("commands", self.commands),
                          ("base_lin_vel", self.base_lin_vel), ("base_ang_vel", self.base_ang_vel),
-                         ("projected_gravity", self.projected_gravity), ("feet_air_time", self.feet_air_time),
+                         ("projected_gravity", self.projected_gravity), ("feet_air_time", self._feet_air_time_full),
                          ("obs", self.obs_buf), ("rew", self.rew_buf), ("episode_sums", self._episode_sums_buf),
                          ("measured_heights", self.measured_heights), ("env_origins", self.env_origins),
                          ("terrain_origins", self.terrain_origins), ("body_mass_scale", self.body_mass_scale),

@@ -21,7 +21,7 @@ REWARD_IDS = {
     "dof_vel": 6, "dof_acc": 7, "action_rate": 8, "collision": 9, "termination": 10,
     "dof_pos_limits": 11, "dof_vel_limits": 12, "torque_limits": 13, "tracking_lin_vel": 14,
     "tracking_ang_vel": 15, "feet_air_time": 16, "stumble": 17, "stand_still": 18,
-    "feet_contact_forces": 19, "hip_motion": 20,
+    "feet_contact_forces": 19, "hip_motion": 20, "no_fly": 21,
 }
 CTRL = {"POS_DRIVE": 0, "P": 1, "V": 2, "T": 3, "SEA": 4}
 
@@ -38,7 +38,7 @@ class LgxModel(C.Structure):
         ("dof_lower", f32 * NUM_DOF), ("dof_upper", f32 * NUM_DOF), ("dof_vel_limit", f32 * NUM_DOF),
         ("dof_effort", f32 * NUM_DOF), ("kp", f32 * NUM_DOF), ("kd", f32 * NUM_DOF),
         ("body_mass", f32 * NUM_DYN), ("body_com", f32 * 3 * NUM_DYN), ("body_inertia", f32 * 6 * NUM_DYN),
-        ("num_points", i32), ("num_report_bodies", i32),
+        ("num_points", i32), ("num_report_bodies", i32), ("leg_dof", i32), ("pad_model", i32),
         ("point_pos", f32 * 3 * MAX_POINTS), ("point_radius", f32 * MAX_POINTS),
         ("point_dyn", i32 * MAX_POINTS), ("point_report", i32 * MAX_POINTS),
         ("contact_k", f32), ("contact_c", f32), ("friction_c", f32), ("limit_k", f32), ("limit_c", f32),

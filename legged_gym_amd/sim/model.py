@@ -69,6 +69,7 @@ def build_model(asset: RobotAsset, cfg, sim_params):
         raise ValueError(f"robot has {len(pts)} contact primitives > {abi.MAX_POINTS}")
     m.num_points = len(pts)
     m.num_report_bodies = asset.num_bodies
+    m.leg_dof = int(d.get("leg_dof", 3))
     for i, p in enumerate(pts):
         for k in range(3):
             m.point_pos[i][k] = p["pos"][k]

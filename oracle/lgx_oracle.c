@@ -340,12 +340,15 @@ typedef struct {
   real o[LGX_NUM_DYN][3];  /* body origin relative to base origin O */
   real S[LGX_NUM_DOF][6];  /* joint motion subspace (ang; lin) at O */
   real I6[LGX_NUM_DYN][36];
+  int LD;                  /* joints per leg */
 } kin_t;
 
-static int chain_has(int body, int joint) { /* does body's kinematic chain contain joint? */
+/* legs of LD joints (lgx_model.leg_dof: 4 x 3 quadrupeds, 2 x 6 Cassie) */
+static int leg_dof(const lgx_model* m) { return m->leg_dof == 6 ? 6 : 3; }
+static int chain_has(int body, int joint, int LD) { /* does body's kinematic chain contain joint? */
   if (body == 0) return 0;
-  int leg = (body - 1) / 3, k = (body - 1) % 3;
-  return joint / 3 == leg && joint % 3 <= k;
+  int leg = (body - 1) / LD, k = (body - 1) % LD;
+  return joint / LD == leg && joint % LD <= k;
 }
 
 static void spatial_inertia(const lgx_model* m, int b, real scale, const real* R, const real* o, real* I6) {
@@ -400,7 +403,7 @@ static void body_jac_col(const kin_t* K, int b, int c, real* col) {
   memset(col, 0, 6 * sizeof(real));
   if (c < 6) { col[c] = 1.0f; return; }
   int j = c - 6;
-  if (chain_has(b, j)) memcpy(col, K->S[j], 6 * sizeof(real));
+  if (chain_has(b, j, K->LD)) memcpy(col, K->S[j], 6 * sizeof(real));
 }
 
 /* point Jacobian (3 x ND) of a point P (rel. O) on body b: v_P = v_lin + w x P */
@@ -453,13 +456,15 @@ static void physics_env(const ctx_t* cx, int e) {
 
   /* kinematics */
   kin_t K;
+  const int LD = leg_dof(m);
+  K.LD = LD;
   real q0[4]; ldr(q0, rs + 3, 4);
   quat_to_mat(q0, K.R[0]);
   memset(K.o[0], 0, sizeof K.o[0]);
-  for (int leg = 0; leg < 4; ++leg) {
+  for (int leg = 0; leg < LGX_NUM_DOF / LD; ++leg) {
     int pb = 0;
-    for (int k = 0; k < 3; ++k) {
-      int j = 3 * leg + k, b = 1 + j;
+    for (int k = 0; k < LD; ++k) {
+      int j = LD * leg + k, b = 1 + j;
       real Rjf[9], tmp[3], jrot[9], jpos[3], jax[3];
       ldr(jrot, m->joint_rot[j], 9); ldr(jpos, m->joint_pos[j], 3); ldr(jax, m->joint_axis[j], 3);
       matmul3(K.R[pb], jrot, Rjf);
@@ -506,10 +511,10 @@ static void physics_env(const ctx_t* cx, int e) {
   real wxv[3]; cross3(u, u + 3, wxv);
   A[0][0] = A[0][1] = A[0][2] = 0;
   for (int i = 0; i < 3; ++i) A[0][3 + i] = -wxv[i] - m->gravity[i];
-  for (int leg = 0; leg < 4; ++leg) {
+  for (int leg = 0; leg < LGX_NUM_DOF / LD; ++leg) {
     int pb = 0;
-    for (int k = 0; k < 3; ++k) {
-      int j = 3 * leg + k, b = 1 + j;
+    for (int k = 0; k < LD; ++k) {
+      int j = LD * leg + k, b = 1 + j;
       for (int i = 0; i < 6; ++i) V[b][i] = V[pb][i] + K.S[j][i] * thd[j];
       real c6[6]; crm(V[b], K.S[j], c6);
       for (int i = 0; i < 6; ++i) A[b][i] = A[pb][i] + c6[i] * thd[j];
@@ -878,6 +883,11 @@ static float reward_term(const ctx_t* cx, int e, int id) {
     case LGX_R_HIP_MOTION:
       for (int j = 0; j < 12; j += 3) s += fabsf(ds[2 * j] - p->default_dof_pos[j]);
       return s;
+    case LGX_R_NO_FLY: { /* envs/cassie/cassie.py:42-46 */
+      int n = 0;
+      for (int f = 0; f < p->num_feet; ++f) n += cf[3 * p->feet_indices[f] + 2] > 0.1f;
+      return n == 1 ? 1.0f : 0.0f;
+    }
   }
   return 0.0f;
 }

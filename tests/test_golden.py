@@ -21,7 +21,9 @@ from oracle_backend import load_oracle, make_env, vp
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = {"go1_flat": "go1", "go1_rough": "go1_rough", "anymal_c_rough": "anymal_c_rough",
          # 24 envs x 36 steps on other seeds / terrain draws (the short cases: 12-24 envs x 12-24)
-         "go1_rough_long": "go1_rough", "anymal_c_rough_long": "anymal_c_rough"}
+         "go1_rough_long": "go1_rough", "anymal_c_rough_long": "anymal_c_rough",
+         # the biped (envs/cassie: 2 feet, _reward_no_fly, 11 x 11 scan, pelvis termination)
+         "cassie_rough": "cassie"}
 
 
 def load(name):
@@ -48,11 +50,27 @@ def build(name, g, device="cpu", backend="oracle", overrides=None):
     env.actions.copy_(st("last_actions"))
     if "init_terrain_levels" in g:
         env.terrain_levels.copy_(st("terrain_levels"))
-    env._episode_sums_buf.copy_(st("episode_sums"))
+    rows = env.reward_names + (["termination"] if "termination" in env.reward_scales else [])
+    init = st("episode_sums")
+    for i, k in enumerate(env.episode_sums):     # golden rows are in dict key order
+        env._episode_sums_buf[rows.index(k)].copy_(init[i])
     if "init_act_hist" in g:
         env.actuator_history.copy_(st("act_hist").reshape(env.num_envs, -1))
     env.common_step_counter = int(g["init_common_step_counter"])
     return env
+
+
+def sums_by_key(env, buf=None):
+    """Episode sums stacked in the env's dict key order (the reference's: the golden's rows)."""
+    buf = env._episode_sums_buf if buf is None else buf
+    rows = env.reward_names + (["termination"] if "termination" in env.reward_scales else [])
+    return buf[[rows.index(k) for k in env.episode_sums]]
+
+
+def extras_by_key(env):
+    """extras["episode"] reward means in the env's dict key order (the golden's rows)."""
+    rows = dict(env._extras_rows)
+    return env._extras_buf[[rows["rew_" + k] for k in env.episode_sums]]
 
 
 def close(a, b, atol, rtol):
@@ -126,7 +144,7 @@ def test_post_physics_replay_matches_reference(name):
                                ("projected_gravity", env.projected_gravity, (1e-6, 1e-6)),
                                ("env_origins", env.env_origins, (0, 0)), ("target_poses", env.target_poses, (1e-6, 1e-6)),
                                ("rew_buf", env.rew_buf, (1e-5, 1e-4)),
-                               ("episode_sums", env._episode_sums_buf, (1e-5, 1e-4))):
+                               ("episode_sums", sums_by_key(env), (1e-5, 1e-4))):
             ok, err = close(mine.numpy(), g["step_" + key][t], *tol)
             assert ok, f"{tag} {key} max err {err}"
         if "height_samples" in g:
@@ -139,7 +157,7 @@ def test_post_physics_replay_matches_reference(name):
         ref_ex = g["step_extras"][t]
         if not np.isnan(ref_ex[0]):   # the reference publishes extras only when an env reset
             T_rows = len(env.episode_sums)
-            ok, err = close(env._extras_buf.numpy()[:T_rows], ref_ex[:T_rows], 1e-6, 1e-4)
+            ok, err = close(extras_by_key(env).numpy(), ref_ex[:T_rows], 1e-6, 1e-4)
             assert ok, f"{tag} extras max err {err}"
             if env.cfg.terrain.curriculum:
                 ok, err = close(env._extras_buf.numpy()[T_rows], ref_ex[-1], 1e-6, 1e-6)

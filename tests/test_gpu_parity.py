@@ -688,3 +688,79 @@ def test_direct_actions_and_extras_snapshots(gpu):
     for ep, ref in zip(kept, expect):
         for key, row in a_env._extras_rows:
             assert torch.equal(ep[key], ref[row]), key
+
+
+def _cassie_state(env, gen):
+    """randomize_state at the biped's standing height (pelvis ~0.9 m) with its feet near the ground."""
+    randomize_state(env, gen)
+    N = env.num_envs
+    env.root_states[:, 2] = env.env_origins[:, 2] + 0.80 + 0.15 * torch.rand(N, generator=gen)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_cassie_dense_physics_matches_float64(gpu, seed):
+    """Cassie (2 legs x 6 joints: lgx_physics_dense_kernel) on its rough terrain: 4 substeps from
+    randomised states, HIP vs the float64 oracle with the derived tolerance (check_derived)."""
+    ora = make_env("cassie", num_envs=64, device="cpu", backend="oracle")
+    dev = make_env("cassie", num_envs=64, device="cuda:0", backend="lgx")
+    assert dev._lgx_model.leg_dof == 6
+    gen = torch.Generator().manual_seed(200 + seed)
+    _cassie_state(ora, gen)
+    sync(ora, dev)
+    dev.terrain_types.copy_(ora.terrain_types)
+    t64 = float64_truth(ora, 4)
+    ora.simulate(4)
+    dev.simulate(4)
+    torch.cuda.synchronize()
+    errs = check_derived(t64, {k: f(ora) for k, f in PHYS_QTY.items()}, {k: f(dev) for k, f in PHYS_QTY.items()})
+    assert ora.contact_forces[:, ora.feet_indices].abs().sum() > 0, "the test states should touch the ground"
+    assert errs["dof_vel"][0] < 0.05, errs
+
+
+def test_cassie_full_step_matches_oracle(gpu):
+    """lgx_step on the biped (dense physics + the env-logic kernel with no_fly, 2 feet, the 11 x 11
+    scan and pelvis termination) vs the oracle, 3 steps from randomised states."""
+    ora = make_env("cassie", num_envs=64, device="cpu", backend="oracle")
+    dev = make_env("cassie", num_envs=64, device="cuda:0", backend="lgx")
+    gen = torch.Generator().manual_seed(42)
+    for it in range(3):
+        _cassie_state(ora, gen)
+        sync(ora, dev)
+        dev.terrain_types.copy_(ora.terrain_types)
+        ora.common_step_counter = dev.common_step_counter = 10 * it
+        a = (torch.rand(64, 12, generator=gen) - 0.5) * 2
+        ora.step(a)
+        dev.step(a.cuda())
+        torch.cuda.synchronize()
+        assert torch.equal(dev.reset_buf.cpu(), ora.reset_buf), it
+        keep = ~ora.reset_buf
+        ok, e = close(dev.obs_buf.cpu()[keep], ora.obs_buf[keep], 5e-3, 5e-3)
+        assert ok, f"obs max err {e}"
+        ok, e = close(dev.rew_buf.cpu()[keep], ora.rew_buf[keep], 1e-4, 1e-3)
+        assert ok, f"rew max err {e}"
+        ok, e = close(dev.feet_air_time, ora.feet_air_time, 1e-5)
+        assert ok, f"feet air time max err {e}"
+
+
+@pytest.mark.parametrize("task", ["go1_flat_bench", "anymal_c_rough"])
+def test_dense_kernel_on_quadrupeds_matches_float64(gpu, monkeypatch, task):
+    """The dense joint-space kernel is a second, independent GPU formulation of the same physics
+    (LGX_PHYS_DENSE=1 selects it for the 4 x 3 quadrupeds): HIP vs the float64 oracle with the derived
+    tolerance, and vs the arrowhead kernel's result from the same state."""
+    ora = make_env(task, num_envs=64, device="cpu", backend="oracle")
+    arrow = make_env(task, num_envs=64, device="cuda:0", backend="lgx")
+    monkeypatch.setenv("LGX_PHYS_DENSE", "1")
+    dense = make_env(task, num_envs=64, device="cuda:0", backend="lgx")
+    gen = torch.Generator().manual_seed(7)
+    randomize_state(ora, gen)
+    for dev in (arrow, dense):
+        sync(ora, dev)
+        dev.terrain_types.copy_(ora.terrain_types)
+    t64 = float64_truth(ora, 4)
+    ora.simulate(4)
+    arrow.simulate(4)
+    dense.simulate(4)
+    torch.cuda.synchronize()
+    ov = {k: f(ora) for k, f in PHYS_QTY.items()}
+    check_derived(t64, ov, {k: f(dense) for k, f in PHYS_QTY.items()})
+    check_derived(t64, ov, {k: f(arrow) for k, f in PHYS_QTY.items()})

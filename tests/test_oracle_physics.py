@@ -18,8 +18,9 @@ def fresh(task="go1_flat_bench", n=4, **cfg):
     return make_env(task, num_envs=n, device="cpu", backend="oracle", overrides=ov)
 
 
-def test_free_fall_is_ballistic():
-    env = fresh()
+@pytest.mark.parametrize("task", ["go1_flat_bench", "cassie"])
+def test_free_fall_is_ballistic(task):
+    env = fresh(task, **{"terrain.mesh_type": "plane"})
     env.root_states[:, 2] = 5.0                  # far above the ground: no contact
     env.root_states[:, 3:7] = torch.tensor([0, 0, 0, 1.0])
     env.root_states[:, 7:13] = 0
@@ -55,12 +56,13 @@ def _com(env, e):
                    [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
     p0 = env.root_states[e, :3].double().numpy()
     bodies = d["dyn_bodies"]
+    LD = d.get("leg_dof", 3)
     tot = bodies[0]["mass"] * (p0 + R0 @ np.array(bodies[0]["com"]))
     msum = bodies[0]["mass"]
-    for leg in range(4):
+    for leg in range(12 // LD):
         R, o = R0, p0
-        for k in range(3):
-            j = 3 * leg + k
+        for k in range(LD):
+            j = LD * leg + k
             jt = d["joints"][j]
             E = np.array(jt["rot"]).reshape(3, 3)
             o = o + R @ np.array(jt["pos"])
@@ -71,8 +73,11 @@ def _com(env, e):
     return tot / msum
 
 
-def test_centre_of_mass_moves_uniformly_without_external_forces():
-    env = fresh(n=2, **{"asset.disable_gravity": True})
+@pytest.mark.parametrize("task", ["go1_flat_bench", "cassie"])
+def test_centre_of_mass_moves_uniformly_without_external_forces(task):
+    """Momentum conservation: internal drive forces cannot accelerate the centre of mass, for the
+    quadruped (4 x 3 joint chains) and the biped (2 x 6)."""
+    env = fresh(task, n=2, **{"asset.disable_gravity": True, "terrain.mesh_type": "plane"})
     env.body_mass_scale[:] = 1.0
     g = torch.Generator().manual_seed(0)
     env.root_states[:, 2] = 5.0

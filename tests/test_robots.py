@@ -20,6 +20,35 @@ OBS = {"a1": 235, "a1_src": 235, "aliengo": 48, "anymal_b": 235}
 EXPERIMENT = {"a1": "rough_a1", "a1_src": "rough_a1_src", "aliengo": "rough_aliengo", "anymal_b": "rough_anymal_b"}
 
 
+def test_cassie_registry_model_and_config():
+    """cassie (envs/__init__.py:54): the reference's biped - 2 legs x 6 revolute joints (leg_dof 6,
+    13 bodies named as Isaac Gym names them, the root 'pelvis'), 2 feet ('toe'), pelvis termination by
+    substring (pelvis + both *_pelvis_rotation bodies, legged_robot.py:678-680), 169 observations, the
+    no_fly term, the reference's gains and default angles (cassie_config.py)."""
+    import legged_gym_amd.envs  # noqa: F401
+    from legged_gym_amd import LEGGED_GYM_ROOT_DIR
+    from legged_gym_amd.utils.task_registry import task_registry
+    assert task_registry.task_classes["cassie"].__name__ == "Cassie"
+    assert task_registry.train_cfgs["cassie"].runner.experiment_name == "rough_cassie"
+    d = json.load(open(os.path.join(LEGGED_GYM_ROOT_DIR, "resources", "cassie_model.json")))
+    assert d["leg_dof"] == 6 and len(d["dof_names"]) == 12 and len(d["body_names"]) == 13
+    assert d["body_names"][0] == "pelvis" and d["body_names"][6] == "left_toe" and d["body_names"][12] == "right_toe"
+    np.testing.assert_allclose(sum(b["mass"] for b in d["dyn_bodies"]), 30.468, rtol=1e-4)   # URDF link masses
+    env = make_env("cassie", num_envs=4)
+    assert env._lgx_model.leg_dof == 6
+    assert env.num_obs == 169 and env.obs_buf.shape == (4, 169) and env.num_height_points == 121
+    assert env.feet_indices.tolist() == [6, 12] and env.feet_air_time.shape == (4, 2)
+    assert env.termination_contact_indices.tolist() == [0, 1, 7]
+    assert "no_fly" in env.reward_names and env.reward_scales["termination"] == pytest.approx(-200 * env.dt)
+    assert env.p_gains.tolist() == [100., 100., 200., 200., 200., 40.] * 2
+    assert env.default_dof_pos[0].tolist() == pytest.approx([0.1, 0., 1., -1.8, 1.57, -1.57, -0.1, 0., 1., -1.8, 1.57, -1.57])
+    env.reset()
+    g = torch.Generator().manual_seed(0)
+    for _ in range(10):
+        obs, _, rew, done, _ = env.step(torch.randn(4, 12, generator=g) * 0.3)
+        assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+
+
 def test_registry_holds_every_quadruped():
     import legged_gym_amd.envs  # noqa: F401
     from legged_gym_amd.utils.task_registry import task_registry

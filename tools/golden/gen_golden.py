@@ -560,13 +560,19 @@ def go1_rough():
     return c
 
 
+def cassie_rough():
+    from legged_gym.envs.cassie.cassie_config import CassieRoughCfg
+    return CassieRoughCfg()
+
+
 def anymal_rough():
     from legged_gym.envs.anymal_c.mixed_terrains.anymal_c_rough_config import AnymalCRoughCfg
     return AnymalCRoughCfg()
 
 
 if __name__ == "__main__":
-    cases = sys.argv[1:] or ["go1_flat", "go1_rough", "anymal_c_rough", "go1_rough_long", "anymal_c_rough_long"]
+    cases = sys.argv[1:] or ["go1_flat", "go1_rough", "anymal_c_rough", "go1_rough_long", "anymal_c_rough_long",
+                             "cassie_rough"]
     if "go1_flat" in cases:
         run_case("go1_flat", "Go1", go1_flat, 24, 24, 1, "go1_model.json")
     if "go1_rough" in cases:
@@ -577,3 +583,5 @@ if __name__ == "__main__":
         run_case("go1_rough_long", "Go1", go1_rough, 24, 36, 4, "go1_model.json")
     if "anymal_c_rough_long" in cases:
         run_case("anymal_c_rough_long", "Anymal", anymal_rough, 24, 36, 5, "anymal_c_model.json")
+    if "cassie_rough" in cases:   # the biped: 2 feet, no_fly, 11 x 11 scan, pelvis termination
+        run_case("cassie_rough", "Cassie", cassie_rough, 16, 24, 6, "cassie_model.json")

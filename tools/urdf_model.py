@@ -18,7 +18,10 @@ Semantics reproduced from the Isaac Gym asset importer as configured by the refe
   * replace_cylinder_with_capsule=True: cylinders become capsules (segment = cylinder
     length along the cylinder axis, radius unchanged).
 
-Only 4-leg x 3-revolute-joint robots are supported (Go1, ANYmal-C: SURVEY.md §8).
+Robots with 12 revolute DOFs in serial leg chains hanging off the base: 4 legs x 3 joints (the
+quadrupeds) or 2 legs x 6 joints (Cassie); `leg_dof` in the JSON.  The root body keeps its root
+link's name ("base" for the quadrupeds, "pelvis" for Cassie), as Isaac Gym names a collapsed body
+after its root link (legged_robot.py:678-680 matches termination bodies by substring of these names).
 
 Usage:  python tools/urdf_model.py <urdf> <out.json> <name>
 """
@@ -150,7 +153,7 @@ def build(urdf_path, name):
 
     bodies.append(dict(name=root_link, members=[], parent=-1, R_pj=np.eye(3), t_pj=np.zeros(3), joint=None))
     visit(root_link, 0, np.eye(3), np.zeros(3))
-    # Isaac Gym names a collapsed body after its root link; the base is reported as "base".
+    # Isaac Gym names a collapsed body after its root link (the quadrupeds: "base", Cassie: "pelvis").
     for b in bodies:
         props = []
         pts = []
@@ -166,15 +169,16 @@ def build(urdf_path, name):
 
     nb = len(bodies)
     assert len(dofs) == 12, f"expected 12 revolute DOFs, got {len(dofs)}"
-    # legs: the 4 children of the base that start a 3-DOF chain, in order
+    # legs: the children of the base that start a serial chain (4 x 3 DOFs or 2 x 6), in order
     leg_roots = [i for i in dofs if bodies[i]["parent"] == 0]
-    assert len(leg_roots) == 4
-    dyn = [0]            # dyn body 0 = base, then per leg hip/thigh/shank
+    assert len(leg_roots) in (2, 4), leg_roots
+    leg_dof = 12 // len(leg_roots)
+    dyn = [0]            # dyn body 0 = base, then per leg its chain's moving bodies
     report_to_dyn = {0: (0, np.eye(3), np.zeros(3))}
     joint_rows = []
     for leg, b0 in enumerate(leg_roots):
         chain = [b0]
-        while len(chain) < 3:
+        while len(chain) < leg_dof:
             nxt = [i for i in dofs if bodies[i]["parent"] == chain[-1]]
             assert len(nxt) == 1
             chain.append(nxt[0])
@@ -183,7 +187,7 @@ def build(urdf_path, name):
             j = bodies[bi]["joint"]
             joint_rows.append(dict(name=j["name"], R=bodies[bi]["R_pj"], t=bodies[bi]["t_pj"], axis=j["axis"],
                                    lower=j["lower"], upper=j["upper"], effort=j["effort"], velocity=j["velocity"]))
-            report_to_dyn[bi] = (1 + 3 * leg + k, np.eye(3), np.zeros(3))
+            report_to_dyn[bi] = (1 + leg_dof * leg + k, np.eye(3), np.zeros(3))
     # fixed (dont_collapse) bodies -> rigidly attached to their moving parent
     for bi, b in enumerate(bodies):
         if bi in report_to_dyn:
@@ -207,9 +211,10 @@ def build(urdf_path, name):
         m, c, I = compose_inertia(dyn_props[d])
         dyn_out.append(dict(name=bodies[dyn[d]]["name"], mass=m, com=c.tolist(),
                             inertia=[I[0, 0], I[1, 1], I[2, 2], I[0, 1], I[0, 2], I[1, 2]]))
-    body_names = ["base"] + [b["name"] for b in bodies[1:]]
+    body_names = [b["name"] for b in bodies]
     out = dict(
         name=name,
+        leg_dof=leg_dof,
         body_names=body_names,
         dof_names=[j["name"] for j in joint_rows],
         joints=[dict(name=j["name"], rot=j["R"].reshape(-1).tolist(), pos=j["t"].tolist(), axis=j["axis"].tolist(),
