@@ -34,6 +34,7 @@ static int launch_check(int rc, const char* what) {
 struct lgx_sim {
   int device;
   bool dense;             // physics on lgx_physics_dense_kernel (leg_dof 6 / LGX_PHYS_DENSE=1)
+  int32_t num_points;     // contact candidates of the model (the dense kernel's LDS sizing)
   lgx_env_params params;  // host copy
   lgx_buffers bufs;
   lgx_dev_model* d_model;
@@ -172,6 +173,7 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   if (!s) return fail(LGX_ENOMEM, "lgx_sim_create: out of host memory");
   s->device = device;
   s->dense = dense;
+  s->num_points = model->num_points;
   s->params = *params;
   s->bufs = *bufs;
   s->draws = nullptr;
@@ -255,7 +257,7 @@ int lgx_sync_aux(lgx_sim* s, void* stream) {
 // the physics launch of a sim: the arrowhead kernel, or the dense one (lgx_sim.dense)
 static int physics(lgx_sim* s, int32_t nsub, int32_t from_actions, const float* actions, hipStream_t st, int32_t frozen) {
   return s->dense ? lgx_launch_physics_dense(s->d_model, s->d_params, s->bufs, s->params.num_envs, nsub, from_actions,
-                                             actions, st, frozen)
+                                             actions, st, frozen, s->num_points)
                   : lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, nsub, from_actions, actions,
                                        st, frozen);
 }

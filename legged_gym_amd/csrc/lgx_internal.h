@@ -14,6 +14,7 @@ struct lgx_dev_model {
   int32_t max_lane_npts;
   int32_t pad;
   int32_t lane_pts[4][LGX_MAX_LANE_PTS];
+  int32_t pad_tail[(4 - (sizeof(lgx_model) / 4 + 6 + 4 * LGX_MAX_LANE_PTS) % 4) % 4];   // 16-byte multiple
 };
 
 int lgx_launch_ground_contact(const lgx_env_params* dp, const lgx_buffers& b, const float* q, int32_t n, float* o,
@@ -27,7 +28,7 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
 // the dense joint-space kernel (lgx_physics.hip): leg_dof == 6 robots, or any with LGX_PHYS_DENSE=1
 int lgx_launch_physics_dense(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                              int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
-                             int32_t frozen);
+                             int32_t frozen, int32_t num_points);
 int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t num_obs,
                             int32_t n_term_rows, int32_t measure_heights, int64_t step, const float* draws,
                             float* extras_snapshot, hipStream_t stream);

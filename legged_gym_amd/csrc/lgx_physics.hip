@@ -3,14 +3,18 @@
 // Replaces Isaac Gym PhysX `gym.simulate` as driven by LeggedRobot.step
 // (legged_robot.py:89-99; model/drive setup legged_robot.py:645-740).  Model: DESIGN.md §3.
 //
-// Mapping (CDNA4, wave64): one env per 4-lane quad, lane = leg.  A wave holds 16 envs.
-// The joint-space mass matrix of a quadruped is "arrowhead": a 6x6 base block A coupled to
-// four independent 3x3 leg blocks D_l through 6x3 blocks B_l.  Each lane builds its leg's
-// B_l/D_l (composite-rigid-body algorithm on a 3-link chain), its leg's bias forces
-// (RNEA) and its leg's contact terms; the base Schur complement A - sum_l B_l D_l^-1 B_l^T
-// is formed with two quad shuffles per entry and solved redundantly in all 4 lanes; the
-// leg back-substitution is lane-local again.  All state stays in VGPRs across substeps;
-// HBM traffic per env-step = state in + state out (+ actuator-net history).
+// Mapping (CDNA4, wave64), lgx_physics_kernel<PP>: one env per 4 PP lanes, lane = leg x PP-way
+// split of the leg's contact candidates (PP = 4 at every size: 16 lanes per env, 4 envs per wave,
+// 16 envs per 256-thread workgroup).  The joint-space mass matrix of a quadruped is "arrowhead": a
+// 6x6 base block A coupled to four independent 3x3 leg blocks D_l through 6x3 blocks B_l.  Each lane
+// builds its leg's B_l/D_l (composite-rigid-body algorithm on a 3-link chain), its leg's bias forces
+// (RNEA) and its share of the leg's contact terms (reduced over the PP lanes with DPP row sums); the
+// base Schur complement A - sum_l B_l D_l^-1 B_l^T is formed with quad shuffles and its 6x6 Cholesky
+// solved redundantly by every lane of the env; the leg back-substitution is lane-local again.
+// Per-substep state stays in VGPRs, leg-uniform values and the heightfield patch in LDS; HBM
+// traffic per env-step = state in + state out (+ actuator-net history).
+// lgx_physics_dense_kernel (end of file): the biped's 2 x 6 chains (and any robot with
+// LGX_PHYS_DENSE=1), one env per wavefront, the oracle's dense algorithm.
 #include <stdlib.h>
 
 #include "lgx_device.h"
@@ -640,6 +644,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   // per-wave queue of the candidates that need the corrected-trimesh query: (cells << 16 | slot << 6 | lane)
   __shared__ uint32_t tm_q[PP][64 * SLOTS];
   {
+    static_assert(sizeof(lgx_dev_model) % 16 == 0, "the model is staged in 16-byte units");
     const int4* src = reinterpret_cast<const int4*>(DMg);
     int4* dst = reinterpret_cast<int4*>(&smodel);
     for (int i = threadIdx.x; i < (int)(sizeof(lgx_dev_model) / 16); i += PHYS_BLOCK) dst[i] = src[i];
@@ -1355,32 +1360,67 @@ int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const 
 // ============================================================================================
 // Dense joint-space physics (lgx_model.leg_dof == 6: Cassie's 2 legs x 6 joints, which the
 // arrowhead kernel's 4-leg x 3-joint lane mapping does not cover; any robot with LGX_PHYS_DENSE=1).
-// One env per wavefront (64-thread workgroup), the same model and algorithm as the oracle
-// (oracle/lgx_oracle.c physics_env: dense 18 x 18 H = sum_b J_b^T I_b J_b, RNEA bias, implicit PD
-// drives and limit springs, compliant contact with the two-pass stick / slide classification,
-// dense Cholesky), the work of every phase spread over the wave's lanes with the per-env arrays in
-// LDS: forward kinematics one lane per leg chain, spatial inertias / body forces one lane per body,
-// H / M one lane per matrix entry, contacts one lane per candidate point (ballot-compacted in point
-// order, so every sum over contacts runs in the oracle's order), the Cholesky columns one lane per
-// row.  Latency-bound like the arrowhead kernel (a serial chain of small dependent steps per env).
+// One env per wavefront (64-thread workgroup), the same physics model as the oracle (implicit PD
+// drives and limit springs, compliant contact with the two-pass stick / slide classification) on the
+// full 18 x 18 joint-space system, the work of every phase spread over the wave's lanes with the
+// per-env arrays in LDS:
+//   * one lane per leg chain: forward kinematics and the RNEA velocities / accelerations on the way
+//     out, then composite inertias IC_k, H's leg rows (S_j . IC_k S_k) and base couplings (IC_k S_k),
+//     and the bias forces S_j . (sum of the subtree's body forces) on the way back (CRBA / RNEA: the
+//     H = sum_b J_b^T I_b J_b of the oracle without its zero blocks);
+//   * one lane per body: spatial inertia and body force; one lane per entry: the base block;
+//   * one lane per contact candidate (ballot-compacted in point order, so the sums over contacts run
+//     in the oracle's order); one lane per matrix entry of M = H + drives + contact terms; one lane
+//     per row in each Cholesky column.
+// Contact storage is sized to the robot's candidate count (dynamic LDS).  Latency-bound like the
+// arrowhead kernel (a serial chain of small dependent steps per env).
 // ============================================================================================
 namespace {
 
 constexpr int DN = 18;                     // generalised velocity [w(3), v(3), qd(12)]
-constexpr int DMAXC = LGX_MAX_POINTS;
+constexpr int DCF = 3 * DN + 3 + 3 + 1 + 1 + 3 + 3;   // floats per contact slot (+ 3 ints)
 
 struct DenseLds {
   float R[LGX_NUM_DYN][9], o[LGX_NUM_DYN][3], S[LGX_NUM_DOF][6], I6[LGX_NUM_DYN][36];
   float H[DN * DN], M[DN * DN];
   float V[LGX_NUM_DYN][6], A[LGX_NUM_DYN][6], F[LGX_NUM_DYN][6];
+  float ICroot[2][36], Froot[2][6];          // per leg: composite inertia and force sum at its root
   float Cb[DN], g[DN], Hu[DN], r[DN], u[DN], u2[DN];
   float th[12], thd[12], tgt[12], tex[12], Dimp[12];
   float root[13];
   int impl[12];
   int nc;
-  float cJ[DMAXC][3 * DN], cP[DMAXC][3], cn[DMAXC][3], cdepth[DMAXC], cmu[DMAXC], cfs[DMAXC][3], cf[DMAXC][3];
-  int cbody[DMAXC], creport[DMAXC], cstat[DMAXC];
 };
+
+// per-contact slots in dynamic LDS: [capacity] arrays
+struct DenseContacts {
+  float (*J)[3 * DN];
+  float (*P)[3];
+  float (*n)[3];
+  float* depth;
+  float* mu;
+  float (*fs)[3];
+  float (*f)[3];
+  int* body;
+  int* report;
+  int* stat;
+};
+
+LGX_DEV DenseContacts dense_contacts(float* base, int cap) {
+  DenseContacts c;
+  c.J = reinterpret_cast<float(*)[3 * DN]>(base);
+  c.P = reinterpret_cast<float(*)[3]>(base + cap * 3 * DN);
+  c.n = reinterpret_cast<float(*)[3]>(base + cap * (3 * DN + 3));
+  c.depth = base + cap * (3 * DN + 6);
+  c.mu = base + cap * (3 * DN + 7);
+  c.fs = reinterpret_cast<float(*)[3]>(base + cap * (3 * DN + 8));
+  c.f = reinterpret_cast<float(*)[3]>(base + cap * (3 * DN + 11));
+  int* ib = reinterpret_cast<int*>(base + cap * DCF);
+  c.body = ib;
+  c.report = ib + cap;
+  c.stat = ib + 2 * cap;
+  return c;
+}
 
 // does dyn body `body`'s chain contain joint `joint` (legs of LD joints)
 LGX_DEV bool d_chain_has(int body, int joint, int LD) {
@@ -1400,8 +1440,6 @@ LGX_DEV void d_body_col(const DenseLds& L, int b, int c, int LD, float* col) {
     for (int i = 0; i < 6; ++i) col[i] = L.S[j][i];
 }
 
-LGX_DEV bool d_col_nonzero(int b, int c, int LD) { return c < 6 || d_chain_has(b, c - 6, LD); }
-
 LGX_DEV void d_crm(const float* V, const float* s, float* o) {   // V x_m s
   const f3 a = cross(mk3(V[0], V[1], V[2]), mk3(s[0], s[1], s[2]));
   const f3 l = cross(mk3(V[0], V[1], V[2]), mk3(s[3], s[4], s[5])) + cross(mk3(V[3], V[4], V[5]), mk3(s[0], s[1], s[2]));
@@ -1418,8 +1456,11 @@ LGX_DEV void d_crf(const float* V, const float* f, float* o) {   // V x_f f
 __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_model* __restrict__ DMg,
                                                                const lgx_env_params* __restrict__ P, lgx_buffers B,
                                                                int32_t nsub, int32_t from_actions,
-                                                               const float* __restrict__ act_src, int32_t frozen) {
+                                                               const float* __restrict__ act_src, int32_t frozen,
+                                                               int32_t cap) {
   __shared__ DenseLds L;
+  extern __shared__ __attribute__((aligned(16))) float dyn_lds[];
+  const DenseContacts Ct = dense_contacts(dyn_lds, cap);
   const lgx_model* __restrict__ M = &DMg->m;
   const int lane = threadIdx.x;
   const int e = blockIdx.x;
@@ -1465,21 +1506,31 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
       }
       L.tex[j] = t;
     }
-    if (lane < 6) {
-      L.u[lane] = lane < 3 ? L.root[10 + lane] : L.root[7 + lane - 3];
-    } else if (lane < DN) {
-      L.u[lane] = L.thd[lane - 6];
-    }
-    // ---- kinematics: one lane per leg chain
+    if (lane < 6) L.u[lane] = lane < 3 ? L.root[10 + lane] : L.root[7 + lane - 3];
+    else if (lane < DN) L.u[lane] = L.thd[lane - 6];
+    for (int q = lane; q < DN * DN; q += 64) L.H[q] = 0.f;
+    // ---- one lane per leg chain: kinematics + RNEA velocities / accelerations (A_0 = (0, -w x v - g))
     const m33 R0 = quat_to_mat(L.root[3], L.root[4], L.root[5], L.root[6]);
+    const float ub[6] = {L.root[10], L.root[11], L.root[12], L.root[7], L.root[8], L.root[9]};
     if (lane == 0) {
 #pragma unroll
       for (int i = 0; i < 9; ++i) L.R[0][i] = R0.a[i];
       L.o[0][0] = L.o[0][1] = L.o[0][2] = 0.f;
+      const f3 wxv = cross(mk3(ub[0], ub[1], ub[2]), mk3(ub[3], ub[4], ub[5]));
+#pragma unroll
+      for (int i = 0; i < 6; ++i) L.V[0][i] = ub[i];
+      L.A[0][0] = L.A[0][1] = L.A[0][2] = 0.f;
+      L.A[0][3] = -wxv.x - M->gravity[0]; L.A[0][4] = -wxv.y - M->gravity[1]; L.A[0][5] = -wxv.z - M->gravity[2];
     }
     if (lane < NL) {
       m33 Rp = R0;
       f3 op = mk3(0.f, 0.f, 0.f);
+      float Vp[6], Ap[6];
+      const f3 wxv = cross(mk3(ub[0], ub[1], ub[2]), mk3(ub[3], ub[4], ub[5]));
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Vp[i] = ub[i];
+      Ap[0] = Ap[1] = Ap[2] = 0.f;
+      Ap[3] = -wxv.x - M->gravity[0]; Ap[4] = -wxv.y - M->gravity[1]; Ap[5] = -wxv.z - M->gravity[2];
       for (int k = 0; k < LD; ++k) {
         const int j = LD * lane + k, b = 1 + j;
         m33 Jr;
@@ -1491,27 +1542,38 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
         const f3 aw = mul(Rjf, ax);
         const m33 Rb = mul(Rjf, axis_angle(ax, L.th[j]));
         const f3 ow = cross(ob, aw);
+        const float Sj[6] = {aw.x, aw.y, aw.z, ow.x, ow.y, ow.z};
+        const float qd = L.thd[j];
+        float c6[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Vp[i] = Vp[i] + Sj[i] * qd;
+        d_crm(Vp, Sj, c6);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          Ap[i] = Ap[i] + c6[i] * qd;
+          L.S[j][i] = Sj[i];
+          L.V[b][i] = Vp[i];
+          L.A[b][i] = Ap[i];
+        }
 #pragma unroll
         for (int i = 0; i < 9; ++i) L.R[b][i] = Rb.a[i];
         L.o[b][0] = ob.x; L.o[b][1] = ob.y; L.o[b][2] = ob.z;
-        L.S[j][0] = aw.x; L.S[j][1] = aw.y; L.S[j][2] = aw.z;
-        L.S[j][3] = ow.x; L.S[j][4] = ow.y; L.S[j][5] = ow.z;
         Rp = Rb;
         op = ob;
       }
     }
     __syncthreads();
-    // ---- spatial inertias at the base origin: one lane per body (oracle spatial_inertia)
+    // ---- one lane per body: spatial inertia at the base origin (oracle spatial_inertia) and the
+    // body force f_b = I_b A_b + V_b x* I_b V_b
     if (lane < LGX_NUM_DYN) {
       const int b = lane;
       const float* in = M->body_inertia[b];
       const float scale = B.body_mass_scale[(int64_t)e * LGX_NUM_DYN + b];
-      m33 R, Ib;
+      m33 R, Ib, RT;
 #pragma unroll
       for (int i = 0; i < 9; ++i) R.a[i] = L.R[b][i];
       Ib.a[0] = in[0]; Ib.a[1] = in[3]; Ib.a[2] = in[4]; Ib.a[3] = in[3]; Ib.a[4] = in[1]; Ib.a[5] = in[5];
       Ib.a[6] = in[4]; Ib.a[7] = in[5]; Ib.a[8] = in[2];
-      m33 RT;
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
@@ -1524,84 +1586,84 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
       for (int i = 0; i < 9; ++i) Iw.a[i] *= scale;
       const float cc = dot(c, c);
       const float cv[3] = {c.x, c.y, c.z};
-      float* I6 = L.I6[b];
+      const float sk[9] = {0.f, -c.z, c.y, c.z, 0.f, -c.x, -c.y, c.x, 0.f};
+      float I6[36];
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           I6[i * 6 + j] = Iw.a[3 * i + j] + mass * ((i == j ? cc : 0.f) - cv[i] * cv[j]);
           I6[(3 + i) * 6 + 3 + j] = i == j ? mass : 0.f;
-        }
-      const float sk[9] = {0.f, -c.z, c.y, c.z, 0.f, -c.x, -c.y, c.x, 0.f};
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
           I6[i * 6 + 3 + j] = mass * sk[3 * i + j];
           I6[(3 + i) * 6 + j] = mass * sk[3 * j + i];
         }
-    } else if (lane >= 32 && lane < 32 + NL) {
-      // ---- RNEA velocities / accelerations along each leg chain (A_0 = (0, -w x v - g))
-      const int leg = lane - 32;
-      float Vp[6], Ap[6];
+      float Vb[6], Ab[6], IA[6], IV[6], vf[6];
 #pragma unroll
-      for (int i = 0; i < 6; ++i) Vp[i] = L.u[i];
-      const f3 wxv = cross(mk3(L.u[0], L.u[1], L.u[2]), mk3(L.u[3], L.u[4], L.u[5]));
-      Ap[0] = Ap[1] = Ap[2] = 0.f;
-      Ap[3] = -wxv.x - M->gravity[0]; Ap[4] = -wxv.y - M->gravity[1]; Ap[5] = -wxv.z - M->gravity[2];
-      if (leg == 0)
-#pragma unroll
-        for (int i = 0; i < 6; ++i) { L.V[0][i] = Vp[i]; L.A[0][i] = Ap[i]; }
-      for (int k = 0; k < LD; ++k) {
-        const int j = LD * leg + k, b = 1 + j;
-        float Sj[6], c6[6];
-#pragma unroll
-        for (int i = 0; i < 6; ++i) { Sj[i] = L.S[j][i]; Vp[i] = Vp[i] + Sj[i] * L.thd[j]; }
-        d_crm(Vp, Sj, c6);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) { Ap[i] = Ap[i] + c6[i] * L.thd[j]; L.V[b][i] = Vp[i]; L.A[b][i] = Ap[i]; }
-      }
-    }
-    __syncthreads();
-    // ---- H = sum_b J_b^T I_b J_b (all 324 entries; the Cholesky reads the lower triangle, H u
-    // the whole matrix) and the body forces f_b = I_b A_b + V_b x* I_b V_b
-    for (int q = lane; q < DN * DN; q += 64) {
-      const int a = q / DN, c = q % DN;
-      float h = 0.f;
-      for (int b = 0; b < LGX_NUM_DYN; ++b) {
-        if (!d_col_nonzero(b, a, LD) || !d_col_nonzero(b, c, LD)) continue;
-        float ca[6], cc[6];
-        d_body_col(L, b, a, LD, ca);
-        d_body_col(L, b, c, LD, cc);
-        float sum = 0.f;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-          float ij = 0.f;
-#pragma unroll
-          for (int m = 0; m < 6; ++m) ij += L.I6[b][k * 6 + m] * cc[m];
-          sum += ca[k] * ij;
-        }
-        h += sum;
-      }
-      L.H[q] = h;
-    }
-    if (lane < LGX_NUM_DYN) {
-      const int b = lane;
-      float IA[6], IV[6], vf[6];
+      for (int i = 0; i < 6; ++i) { Vb[i] = L.V[b][i]; Ab[i] = L.A[b][i]; }
 #pragma unroll
       for (int i = 0; i < 6; ++i) {
         float x = 0.f, y = 0.f;
 #pragma unroll
-        for (int j = 0; j < 6; ++j) { x += L.I6[b][i * 6 + j] * L.A[b][j]; y += L.I6[b][i * 6 + j] * L.V[b][j]; }
+        for (int j = 0; j < 6; ++j) { x += I6[i * 6 + j] * Ab[j]; y += I6[i * 6 + j] * Vb[j]; }
         IA[i] = x; IV[i] = y;
       }
-      d_crf(L.V[b], IV, vf);
+      d_crf(Vb, IV, vf);
 #pragma unroll
       for (int i = 0; i < 6; ++i) L.F[b][i] = IA[i] + vf[i];
+#pragma unroll
+      for (int i = 0; i < 36; ++i) L.I6[b][i] = I6[i];
+    }
+    __syncthreads();
+    // ---- one lane per leg: composite inertias and subtree forces from the tip (CRBA / RNEA):
+    // H[j][k] = S_j . IC_k S_k (k deeper on the chain), H[base][k] = IC_k S_k, C_j = S_j . F_k
+    if (lane < NL) {
+      const int leg = lane;
+      float IC[36], Fs[6];
+#pragma unroll
+      for (int i = 0; i < 36; ++i) IC[i] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) Fs[i] = 0.f;
+      for (int k = LD - 1; k >= 0; --k) {
+        const int j = LD * leg + k, b = 1 + j;
+#pragma unroll
+        for (int i = 0; i < 36; ++i) IC[i] += L.I6[b][i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Fs[i] += L.F[b][i];
+        float Sk[6], Fc[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) Sk[i] = L.S[j][i];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          float x = 0.f;
+#pragma unroll
+          for (int m = 0; m < 6; ++m) x += IC[i * 6 + m] * Sk[m];
+          Fc[i] = x;
+        }
+        float cj = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          L.H[i * DN + 6 + j] = Fc[i];       // base rows / column j (symmetric)
+          L.H[(6 + j) * DN + i] = Fc[i];
+          cj += Sk[i] * Fs[i];
+        }
+        L.Cb[6 + j] = cj;
+        for (int kk = 0; kk <= k; ++kk) {    // joints j' on the chain from the root down to j
+          const int jj = LD * leg + kk;
+          float h = 0.f;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) h += L.S[jj][i] * Fc[i];
+          L.H[(6 + jj) * DN + 6 + j] = h;
+          L.H[(6 + j) * DN + 6 + jj] = h;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 36; ++i) L.ICroot[leg][i] = IC[i];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) L.Froot[leg][i] = Fs[i];
     }
     // ---- drives (implicit PD while within the effort limit) and hard-limit springs
-    if (lane < 12) {
-      const int j = lane;
+    if (lane >= 32 && lane < 44) {
+      const int j = lane - 32;
       float gj = 0.f, dimp = 0.f;
       int impl = 0;
       const float eff = M->dof_effort[j];
@@ -1630,12 +1692,23 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
       L.g[6 + j] = gj;
       L.Dimp[j] = dimp;
       L.impl[j] = impl;
-    } else if (lane < 18) {
-      L.g[lane - 12] = 0.f;
+    } else if (lane >= 44 && lane < 50) {
+      L.g[lane - 44] = 0.f;
+    }
+    if (lane == 63) L.nc = 0;
+    __syncthreads();
+    // base block and base bias: the base body plus every leg's composite at its root
+    if (lane < 36) {
+      float h = L.I6[0][lane];
+      for (int leg = 0; leg < NL; ++leg) h += L.ICroot[leg][lane];
+      L.H[(lane / 6) * DN + lane % 6] = h;
+    } else if (lane < 42) {
+      const int i = lane - 36;
+      float c = L.F[0][i];
+      for (int leg = 0; leg < NL; ++leg) c += L.Froot[leg][i];
+      L.Cb[i] = c;
     }
     // ---- contact candidates: one lane per point, compacted in point order
-    if (lane == 0) L.nc = 0;
-    __syncthreads();
     const int npts = M->num_points;
     for (int i0 = 0; i0 < npts; i0 += 64) {
       const int i = i0 + lane;
@@ -1659,13 +1732,13 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
       const int base = L.nc;
       if (hit) {
         const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
-        L.cbody[slot] = b;
-        L.creport[slot] = M->point_report[i];
-        L.cP[slot][0] = Pc.x; L.cP[slot][1] = Pc.y; L.cP[slot][2] = Pc.z;
-        L.cn[slot][0] = n.x; L.cn[slot][1] = n.y; L.cn[slot][2] = n.z;
-        L.cdepth[slot] = depth;
-        L.cmu[slot] = 0.5f * (mu_env + M->ground_friction);
-        L.cstat[slot] = 1;
+        Ct.body[slot] = b;
+        Ct.report[slot] = M->point_report[i];
+        Ct.P[slot][0] = Pc.x; Ct.P[slot][1] = Pc.y; Ct.P[slot][2] = Pc.z;
+        Ct.n[slot][0] = n.x; Ct.n[slot][1] = n.y; Ct.n[slot][2] = n.z;
+        Ct.depth[slot] = depth;
+        Ct.mu[slot] = 0.5f * (mu_env + M->ground_friction);
+        Ct.stat[slot] = 1;
       }
       __syncthreads();
       if (lane == 0) L.nc = base + __popcll(mask);
@@ -1676,28 +1749,17 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
     for (int q = lane; q < nc * DN; q += 64) {
       const int i = q / DN, c = q % DN;
       float col[6];
-      d_body_col(L, L.cbody[i], c, LD, col);
-      const f3 wxp = cross(mk3(col[0], col[1], col[2]), mk3(L.cP[i][0], L.cP[i][1], L.cP[i][2]));
-      L.cJ[i][c] = col[3] + wxp.x;
-      L.cJ[i][DN + c] = col[4] + wxp.y;
-      L.cJ[i][2 * DN + c] = col[5] + wxp.z;
+      d_body_col(L, Ct.body[i], c, LD, col);
+      const f3 wxp = cross(mk3(col[0], col[1], col[2]), mk3(Ct.P[i][0], Ct.P[i][1], Ct.P[i][2]));
+      Ct.J[i][c] = col[3] + wxp.x;
+      Ct.J[i][DN + c] = col[4] + wxp.y;
+      Ct.J[i][2 * DN + c] = col[5] + wxp.z;
     }
-    __syncthreads();
-    // C (bias) and H u
-    if (lane < DN) {
-      const int c = lane;
-      float cb = 0.f, hu = 0.f;
-      for (int b = 0; b < LGX_NUM_DYN; ++b) {
-        if (!d_col_nonzero(b, c, LD)) continue;
-        float col[6];
-        d_body_col(L, b, c, LD, col);
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) sum += col[i] * L.F[b][i];
-        cb += sum;
-      }
+    // H u
+    if (lane >= 32 && lane < 32 + DN) {
+      const int c = lane - 32;
+      float hu = 0.f;
       for (int k = 0; k < DN; ++k) hu += L.H[c * DN + k] * L.u[k];
-      L.Cb[c] = cb;
       L.Hu[c] = hu;
     }
     __syncthreads();
@@ -1709,33 +1771,28 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
         float m = L.H[q];
         if (a == c && a >= 6) m += L.Dimp[a - 6];
         for (int i = 0; i < nc; ++i) {
-          if (L.cstat[i] == 0) continue;
-          const float wt = (pass == 0 || L.cstat[i] == 1) ? dt * ct : 0.f;
+          if (Ct.stat[i] == 0) continue;
+          const float wt = (pass == 0 || Ct.stat[i] == 1) ? dt * ct : 0.f;
           const float wn = dt * (cn + dt * kn);
-          const float* J = L.cJ[i];
-          const float nv[3] = {L.cn[i][0], L.cn[i][1], L.cn[i][2]};
-          float WJ[3];
-#pragma unroll
-          for (int rr = 0; rr < 3; ++rr) {
-            float w0 = (wn - wt) * nv[rr] * nv[0] + (rr == 0 ? wt : 0.f);
-            float w1 = (wn - wt) * nv[rr] * nv[1] + (rr == 1 ? wt : 0.f);
-            float w2 = (wn - wt) * nv[rr] * nv[2] + (rr == 2 ? wt : 0.f);
-            WJ[rr] = w0 * J[c] + w1 * J[DN + c] + w2 * J[2 * DN + c];
-          }
-          m += J[a] * WJ[0] + J[DN + a] * WJ[1] + J[2 * DN + a] * WJ[2];
+          const float* J = Ct.J[i];
+          const float nv[3] = {Ct.n[i][0], Ct.n[i][1], Ct.n[i][2]};
+          const float jc[3] = {J[c], J[DN + c], J[2 * DN + c]};
+          const float ndc = (wn - wt) * (nv[0] * jc[0] + nv[1] * jc[1] + nv[2] * jc[2]);
+          m += J[a] * (wt * jc[0] + ndc * nv[0]) + J[DN + a] * (wt * jc[1] + ndc * nv[1]) +
+               J[2 * DN + a] * (wt * jc[2] + ndc * nv[2]);
         }
         L.M[q] = m;
       }
-      if (lane < DN) {
-        const int a = lane;
+      if (lane >= 32 && lane < 32 + DN) {
+        const int a = lane - 32;
         float rv = L.Hu[a] + dt * (L.g[a] - L.Cb[a]);
         for (int i = 0; i < nc; ++i) {
-          if (L.cstat[i] == 0) continue;
-          const float* J = L.cJ[i];
-          const float jn = J[a] * L.cn[i][0] + J[DN + a] * L.cn[i][1] + J[2 * DN + a] * L.cn[i][2];
-          rv += dt * kn * L.cdepth[i] * jn;
-          if (pass == 1 && L.cstat[i] == 2)
-            rv += dt * (J[a] * L.cfs[i][0] + J[DN + a] * L.cfs[i][1] + J[2 * DN + a] * L.cfs[i][2]);
+          if (Ct.stat[i] == 0) continue;
+          const float* J = Ct.J[i];
+          const float jn = J[a] * Ct.n[i][0] + J[DN + a] * Ct.n[i][1] + J[2 * DN + a] * Ct.n[i][2];
+          rv += dt * kn * Ct.depth[i] * jn;
+          if (pass == 1 && Ct.stat[i] == 2)
+            rv += dt * (J[a] * Ct.fs[i][0] + J[DN + a] * Ct.fs[i][1] + J[2 * DN + a] * Ct.fs[i][2]);
         }
         L.r[a] = rv;
       }
@@ -1756,24 +1813,22 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
         if (i > j && i < DN) L.M[i * DN + j] = t / d;
         __syncthreads();
       }
-      if (lane == 0) {
-        float x[DN];
-        for (int i = 0; i < DN; ++i) {
-          float t = L.r[i];
-          for (int k = 0; k < i; ++k) t -= L.M[i * DN + k] * x[k];
-          x[i] = t / L.M[i * DN + i];
-        }
-        for (int i = DN - 1; i >= 0; --i) {
-          float t = x[i];
-          for (int k = i + 1; k < DN; ++k) t -= L.M[k * DN + i] * x[k];
-          x[i] = t / L.M[i * DN + i];
-        }
-        for (int i = 0; i < DN; ++i) L.u2[i] = x[i];
+      // substitutions: the solution entries in LDS, one lane per row updating after each pivot
+      for (int i = 0; i < DN; ++i) {
+        if (lane == 0) L.u2[i] = L.r[i] / L.M[i * DN + i];
+        __syncthreads();
+        if (lane > i && lane < DN) L.r[lane] -= L.M[lane * DN + i] * L.u2[i];
+        __syncthreads();
       }
-      __syncthreads();
+      for (int i = DN - 1; i >= 0; --i) {
+        if (lane == 0) L.u2[i] = L.u2[i] / L.M[i * DN + i];
+        __syncthreads();
+        if (lane < i) L.u2[lane] -= L.M[i * DN + lane] * L.u2[i];
+        __syncthreads();
+      }
       if (pass == 0) {   // classify: separating, sliding (Coulomb cone), sticking
         for (int i = lane; i < nc; i += 64) {
-          const float* J = L.cJ[i];
+          const float* J = Ct.J[i];
           float vp[3];
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
@@ -1781,51 +1836,53 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
             for (int a = 0; a < DN; ++a) sv += J[k * DN + a] * L.u2[a];
             vp[k] = sv;
           }
-          const f3 nn = mk3(L.cn[i][0], L.cn[i][1], L.cn[i][2]);
+          const f3 nn = mk3(Ct.n[i][0], Ct.n[i][1], Ct.n[i][2]);
           const float vn = vp[0] * nn.x + vp[1] * nn.y + vp[2] * nn.z;
-          const float fn = kn * L.cdepth[i] - (cn + dt * kn) * vn;
+          const float fn = kn * Ct.depth[i] - (cn + dt * kn) * vn;
           const float vt[3] = {vp[0] - vn * nn.x, vp[1] - vn * nn.y, vp[2] - vn * nn.z};
           const float vtn = sqrtf(vt[0] * vt[0] + vt[1] * vt[1] + vt[2] * vt[2]);
-          if (fn <= 0.f) L.cstat[i] = 0;
-          else if (ct * vtn > L.cmu[i] * fn) {
-            L.cstat[i] = 2;
-            const float sc = -L.cmu[i] * fn / vtn;
-            L.cfs[i][0] = sc * vt[0]; L.cfs[i][1] = sc * vt[1]; L.cfs[i][2] = sc * vt[2];
-          } else L.cstat[i] = 1;
+          if (fn <= 0.f) Ct.stat[i] = 0;
+          else if (ct * vtn > Ct.mu[i] * fn) {
+            Ct.stat[i] = 2;
+            const float sc = -Ct.mu[i] * fn / vtn;
+            Ct.fs[i][0] = sc * vt[0]; Ct.fs[i][1] = sc * vt[1]; Ct.fs[i][2] = sc * vt[2];
+          } else Ct.stat[i] = 1;
         }
         __syncthreads();
       }
     }
     // ---- reported contact forces (net force per reporting body, the last substep's)
-    for (int i = lane; i < nc; i += 64) {
-      float f[3] = {0.f, 0.f, 0.f};
-      if (L.cstat[i] != 0) {
-        const float* J = L.cJ[i];
-        float vp[3];
+    if (s == nsub - 1) {
+      for (int i = lane; i < nc; i += 64) {
+        float f[3] = {0.f, 0.f, 0.f};
+        if (Ct.stat[i] != 0) {
+          const float* J = Ct.J[i];
+          float vp[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          float sv = 0.f;
-          for (int a = 0; a < DN; ++a) sv += J[k * DN + a] * L.u2[a];
-          vp[k] = sv;
-        }
-        const float vn = vp[0] * L.cn[i][0] + vp[1] * L.cn[i][1] + vp[2] * L.cn[i][2];
-        float fn = kn * L.cdepth[i] - (cn + dt * kn) * vn;
-        if (fn < 0.f) fn = 0.f;
+          for (int k = 0; k < 3; ++k) {
+            float sv = 0.f;
+            for (int a = 0; a < DN; ++a) sv += J[k * DN + a] * L.u2[a];
+            vp[k] = sv;
+          }
+          const float vn = vp[0] * Ct.n[i][0] + vp[1] * Ct.n[i][1] + vp[2] * Ct.n[i][2];
+          float fn = kn * Ct.depth[i] - (cn + dt * kn) * vn;
+          if (fn < 0.f) fn = 0.f;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float ft = L.cstat[i] == 1 ? -ct * (vp[k] - vn * L.cn[i][k]) : L.cfs[i][k];
-          f[k] = fn * L.cn[i][k] + ft;
+          for (int k = 0; k < 3; ++k) {
+            const float ft = Ct.stat[i] == 1 ? -ct * (vp[k] - vn * Ct.n[i][k]) : Ct.fs[i][k];
+            f[k] = fn * Ct.n[i][k] + ft;
+          }
         }
+        Ct.f[i][0] = f[0]; Ct.f[i][1] = f[1]; Ct.f[i][2] = f[2];
       }
-      L.cf[i][0] = f[0]; L.cf[i][1] = f[1]; L.cf[i][2] = f[2];
-    }
-    __syncthreads();
-    if (s == nsub - 1 && lane < LGX_MAX_BODIES) {   // (every substep's would be overwritten)
-      float f[3] = {0.f, 0.f, 0.f};
-      for (int i = 0; i < nc; ++i)
-        if (L.creport[i] == lane) { f[0] += L.cf[i][0]; f[1] += L.cf[i][1]; f[2] += L.cf[i][2]; }
-      float* cfo = B.contact_forces + ((int64_t)e * LGX_MAX_BODIES + lane) * 3;
-      cfo[0] = f[0]; cfo[1] = f[1]; cfo[2] = f[2];
+      __syncthreads();
+      if (lane < LGX_MAX_BODIES) {
+        float f[3] = {0.f, 0.f, 0.f};
+        for (int i = 0; i < nc; ++i)
+          if (Ct.report[i] == lane) { f[0] += Ct.f[i][0]; f[1] += Ct.f[i][1]; f[2] += Ct.f[i][2]; }
+        float* cfo = B.contact_forces + ((int64_t)e * LGX_MAX_BODIES + lane) * 3;
+        cfo[0] = f[0]; cfo[1] = f[1]; cfo[2] = f[2];
+      }
     }
     // ---- joint outputs and the root (semi-implicit Euler, quaternion renormalised)
     if (lane < 12) {
@@ -1866,14 +1923,18 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
   if (lane < 13) B.root_states[(int64_t)e * 13 + lane] = L.root[lane];
 }
 
+// dynamic LDS bytes of the dense kernel's contact slots for `num_points` candidates
+static int lgx_physics_dense_lds(int32_t num_points) { return num_points * (DCF + 3) * 4; }
+
 int lgx_launch_physics_dense(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                              int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
-                             int32_t frozen) {
+                             int32_t frozen, int32_t num_points) {
   if (!act_src) act_src = b.actions;
-  LGX_LAUNCH(lgx_physics_dense_kernel, dim3(n_envs), dim3(64), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);
+  const int cap = num_points > 0 ? num_points : 1;
+  LGX_LAUNCH(lgx_physics_dense_kernel, dim3(n_envs), dim3(64), lgx_physics_dense_lds(cap), stream, dm, dp, b, nsub,
+             from_actions, act_src, frozen, cap);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
-
 
 #ifdef LGX_PHASE_CLOCK_BUF
 // instrumented builds only (tools/phase_clock.sh): the per-workgroup clock table of the last physics launch
