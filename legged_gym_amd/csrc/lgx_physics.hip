@@ -87,6 +87,15 @@ LGX_DEV float sv_get(const sv& v, int i) {
   return i == 0 ? v.a.x : i == 1 ? v.a.y : i == 2 ? v.a.z : i == 3 ? v.l.x : i == 4 ? v.l.y : v.l.z;
 }
 
+// Transcendentals on the per-substep critical path (the 6x6 Cholesky's pivots, the leg blocks'
+// inverse determinant, the joint rotations): the hardware v_rsq_f32 / v_rcp_f32 / v_sin_f32 /
+// v_cos_f32 (~1 ulp; 1 instruction each) instead of the correctly rounded sequences (~8-40
+// dependent instructions each: a chain of 8 arrow solves x 6 pivots per launch at one wave per
+// SIMD).  -DLGX_PHYS_FAST_TRANSC=0 restores the correctly rounded forms (A/B; the oracle uses them).
+#ifndef LGX_PHYS_FAST_TRANSC
+#define LGX_PHYS_FAST_TRANSC 1
+#endif
+
 // 6x6 SPD solve (packed sym), in registers
 // (the substitutions multiply by the factorisation's reciprocal diagonal: 12 of the 18 correctly
 // rounded divisions of the textbook form, ~10 instructions each, on the per-substep critical path)
@@ -97,9 +106,15 @@ LGX_DEV void chol6_solve(float* A, float* b) {
     float s = A[sidx(j, j)];
 #pragma unroll
     for (int k = 0; k < j; ++k) s -= L[sidx(j, k)] * L[sidx(j, k)];
+#if LGX_PHYS_FAST_TRANSC
+    const float sc = fmaxf(s, 1e-20f);
+    const float inv = __builtin_amdgcn_rsqf(sc);   // pivot 1 / sqrt(s) and sqrt(s) = s / sqrt(s)
+    const float d = sc * inv;
+#else
     float d = sqrtf(fmaxf(s, 1e-20f));
-    L[sidx(j, j)] = d;
     const float inv = 1.0f / d;
+#endif
+    L[sidx(j, j)] = d;
     Li[j] = inv;
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
@@ -125,13 +140,28 @@ LGX_DEV void chol6_solve(float* A, float* b) {
   }
 }
 
+// Rodrigues rotation with the hardware sine / cosine (v_sin_f32 / v_cos_f32 on th / 2 pi)
+LGX_DEV m33 axis_angle_hw(f3 a, float th) {
+  const float s = __sinf(th), c = __cosf(th);
+  const float t = 1 - c;
+  m33 R;
+  R.a[0] = t * a.x * a.x + c;       R.a[1] = t * a.x * a.y - s * a.z; R.a[2] = t * a.x * a.z + s * a.y;
+  R.a[3] = t * a.x * a.y + s * a.z; R.a[4] = t * a.y * a.y + c;       R.a[5] = t * a.y * a.z - s * a.x;
+  R.a[6] = t * a.x * a.z - s * a.y; R.a[7] = t * a.y * a.z + s * a.x; R.a[8] = t * a.z * a.z + c;
+  return R;
+}
+
 // inverse of a symmetric positive-definite 3x3 (packed d00 d11 d22 d01 d02 d12)
 LGX_DEV void inv3sym(const float* D, float* Di) {
   float c00 = D[1] * D[2] - D[5] * D[5];
   float c01 = D[4] * D[5] - D[3] * D[2];
   float c02 = D[3] * D[5] - D[4] * D[1];
   float det = D[0] * c00 + D[3] * c01 + D[4] * c02;
+#if LGX_PHYS_FAST_TRANSC
+  float id = __builtin_amdgcn_rcpf(det);
+#else
   float id = 1.0f / det;
+#endif
   Di[0] = c00 * id;
   Di[3] = c01 * id;
   Di[4] = c02 * id;
@@ -854,7 +884,11 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         f3 oj = op + mul(Rp, mk3(M->joint_pos[j][0], M->joint_pos[j][1], M->joint_pos[j][2]));
         f3 ax = mk3(M->joint_axis[j][0], M->joint_axis[j][1], M->joint_axis[j][2]);
         f3 aw = mul(Rjf, ax);
+#if LGX_PHYS_FAST_TRANSC
+        Rb[k] = mul(Rjf, axis_angle_hw(ax, th[k]));
+#else
         Rb[k] = mul(Rjf, axis_angle(ax, th[k]));
+#endif
         ob[k] = oj;
 #pragma unroll
         for (int i = 0; i < 9; ++i) kin[k * 12 + i] = Rb[k].a[i];
@@ -1384,7 +1418,7 @@ struct DenseLds {
   float R[LGX_NUM_DYN][9], o[LGX_NUM_DYN][3], S[LGX_NUM_DOF][6], I6[LGX_NUM_DYN][36];
   float H[DN * DN], M[DN * DN];
   float V[LGX_NUM_DYN][6], A[LGX_NUM_DYN][6], F[LGX_NUM_DYN][6];
-  float ICroot[2][36], Froot[2][6];          // per leg: composite inertia and force sum at its root
+  float ICroot[4][36], Froot[4][6];          // per leg: composite inertia and force sum at its root
   float Cb[DN], g[DN], Hu[DN], r[DN], u[DN], u2[DN];
   float th[12], thd[12], tgt[12], tex[12], Dimp[12];
   float root[13];

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round-4 GPU session C: physics A/B (hardware transcendentals vs correctly rounded), phase clocks,
+# then the physics / env parity tests (derived tolerances) on the product build.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
+mkdir -p gpurun_out
+for r in 1 2; do
+  for v in default exact; do
+    if [ $v = default ]; then unset LGX_LIB_PATH; else export LGX_LIB_PATH=$PWD/build/ab/$v/liblgx.so; fi
+    timeout -k 10 200 python tools/phys_bench.py go1_rough 4096 50 > gpurun_out/r04c_phys_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/r04c_phys_$v.log; exit 1; }
+    echo "$v: $(grep physics gpurun_out/r04c_phys_$v.log)"
+  done
+done
+unset LGX_LIB_PATH
+LGX_LIB_PATH=build/clock/liblgx.so timeout -k 10 200 python tools/phys_bench.py go1_rough 4096 3 > gpurun_out/r04c_phys_clock.log 2>&1 || { echo "clock bench failed"; tail -5 gpurun_out/r04c_phys_clock.log; exit 1; }
+grep "physics cycles" gpurun_out/r04c_phys_clock.log | tail -2
+timeout -k 10 900 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fullsize.py \
+  > gpurun_out/r04c_tests.log 2>&1
+rc=$?
+grep -E "FAIL|Error|passed|failed" gpurun_out/r04c_tests.log | tail -30
