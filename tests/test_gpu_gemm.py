@@ -280,6 +280,15 @@ def test_gemm_tn_weight_gradients(gpu, M, S, R, Cc, ldb):
     _run_tn(M, S, R, Cc, 2, ldb=ldb, seed=M + S)
 
 
+@pytest.mark.parametrize("M,S,R,Cc,ldb", [(1024, 2, 128, 128, None), (2048, 4, 256, 235, 256), (96, 3, 128, 384, None),
+                                          (24576, 8, 512, 235, 256)])
+def test_gemm_tn_exact_f32_variant(gpu, monkeypatch, M, S, R, Cc, ldb):
+    """The exact-f32 MFMA dW kernel (LGX_GEMM_TN_F32=1, the A/B alternative to the split-bf16
+    products) under the same float64 bound."""
+    monkeypatch.setenv("LGX_GEMM_TN_F32", "1")
+    _run_tn(M, S, R, Cc, 2, ldb=ldb, seed=M + S + 1)
+
+
 def test_gemm_tn_rejects_bad_shapes(gpu):
     a = abi.LgxGemmTnArgs()
     x = torch.zeros(4096, device="cuda:0")
