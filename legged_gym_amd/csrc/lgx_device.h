@@ -34,10 +34,11 @@ static __device__ unsigned long long lgx_clk_buf[LGX_CLK_MAXB][14];
 #define LGX_CLK_START
 #define LGX_CLK_PRINT(name, n)                                                                        \
   if (LGX_CLK_WHO) {   /* one printf per line (lines of concurrent workgroups do not interleave) */   \
-    unsigned long long _v[8] = {};                                                                    \
-    for (int _i = 0; _i < n && _i < 8; ++_i) _v[_i] = lgx_clk_acc[_i];                                \
-    printf("%s cycles: b=%d 0=%llu 1=%llu 2=%llu 3=%llu 4=%llu 5=%llu 6=%llu 7=%llu\n", name,         \
-           (int)blockIdx.x, _v[0], _v[1], _v[2], _v[3], _v[4], _v[5], _v[6], _v[7]);                  \
+    unsigned long long _v[12] = {};                                                                   \
+    for (int _i = 0; _i < n && _i < 12; ++_i) _v[_i] = lgx_clk_acc[_i];                               \
+    printf("%s cycles: b=%d 0=%llu 1=%llu 2=%llu 3=%llu 4=%llu 5=%llu 6=%llu 7=%llu 8=%llu 9=%llu "   \
+           "10=%llu 11=%llu\n", name, (int)blockIdx.x, _v[0], _v[1], _v[2], _v[3], _v[4], _v[5], _v[6],  \
+           _v[7], _v[8], _v[9], _v[10], _v[11]);                                                       \
   }
 #endif
 #else
@@ -179,7 +180,9 @@ LGX_DEV float row_quads_sum(float v) {
 // triangulated heightfield (diagonal (i,j)-(i+1,j+1), isaacgym terrain_utils trimesh).
 // Optional LDS patch: samples (i, j) with 0 <= i - pi0, j - pj0 < LGX_HF_PATCH are read from
 // `patch` (a copy of the same int16 samples), others from H: identical values either way.
+#ifndef LGX_HF_PATCH
 #define LGX_HF_PATCH 24
+#endif
 LGX_DEV float ground_height(const lgx_env_params* __restrict__ P, const int16_t* __restrict__ H, int rows, int cols,
                             float x, float y, f3* n, const int16_t* patch = nullptr, int pi0 = 0, int pj0 = 0) {
   if (P->terrain_kind == 0 || H == nullptr) { *n = mk3(0.f, 0.f, 1.f); return 0.0f; }

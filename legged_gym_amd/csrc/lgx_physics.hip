@@ -151,6 +151,30 @@ LGX_DEV m33 axis_angle_hw(f3 a, float th) {
   return R;
 }
 
+// reciprocal / reciprocal square root / quotient of the contact queries (per candidate and substep):
+// v_rcp_f32 / v_rsq_f32 (~1 ulp) under LGX_PHYS_FAST_TRANSC, the correctly rounded forms otherwise
+LGX_DEV float ph_rcp(float x) {
+#if LGX_PHYS_FAST_TRANSC
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
+LGX_DEV float ph_rsqrt(float x) {
+#if LGX_PHYS_FAST_TRANSC
+  return __builtin_amdgcn_rsqf(x);
+#else
+  return 1.0f / sqrtf(x);
+#endif
+}
+LGX_DEV float ph_div(float a, float b) {
+#if LGX_PHYS_FAST_TRANSC
+  return a * __builtin_amdgcn_rcpf(b);
+#else
+  return a / b;
+#endif
+}
+
 // inverse of a symmetric positive-definite 3x3 (packed d00 d11 d22 d01 d02 d12)
 LGX_DEV void inv3sym(const float* D, float* Di) {
   float c00 = D[1] * D[2] - D[5] * D[5];
@@ -325,15 +349,15 @@ LGX_DEV f3 closest_on_tri(f3 p, f3 a, f3 b, f3 c) {
   const float d3 = dot(ab, bp), d4 = dot(ac, bp);
   if (d3 >= 0.f && d4 <= d3) return b;
   const float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + (d1 / (d1 - d3)) * ab;
+  if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) return a + ph_div(d1, d1 - d3) * ab;
   const f3 cq = p - c;
   const float d5 = dot(ab, cq), d6 = dot(ac, cq);
   if (d6 >= 0.f && d5 <= d6) return c;
   const float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + (d2 / (d2 - d6)) * ac;
+  if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) return a + ph_div(d2, d2 - d6) * ac;
   const float va = d3 * d6 - d5 * d4;
-  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + ((d4 - d3) / ((d4 - d3) + (d5 - d6))) * (c - b);
-  const float den = 1.f / (va + vb + vc);
+  if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) return b + ph_div(d4 - d3, (d4 - d3) + (d5 - d6)) * (c - b);
+  const float den = ph_rcp(va + vb + vc);
   return a + (vb * den) * ab + (vc * den) * ac;
 }
 
@@ -349,7 +373,7 @@ LGX_DEV void tm_tri(TmQuery& q, f3 p, f3 a, f3 b, f3 c) {
   if (d2 < q.d2) { q.d2 = d2; q.cp = cp; q.cn = cross(e1, e2); }
   const float den = e1.x * e2.y - e1.y * e2.x;      // 2 x signed xy area (0 for vertical faces)
   if (fabsf(den) > 1e-9f) {
-    const float id = 1.f / den;
+    const float id = ph_rcp(den);
     const float px = p.x - a.x, py = p.y - a.y;
     const float s = (px * e2.y - py * e2.x) * id, t = (e1.x * py - e1.y * px) * id;
     if (s >= -1e-6f && t >= -1e-6f && s + t <= 1.f + 1e-6f) {
@@ -455,7 +479,7 @@ LGX_DEV float tm_finish(const TmQuery& q, f3 p, float r, f3* n) {
   const bool inside = p.z < q.top;
   const float d = sqrtf(q.d2);
   if (d > 1e-7f) {
-    const float inv = 1.f / d;
+    const float inv = ph_rcp(d);
     *n = inside ? inv * (q.cp - p) : inv * (p - q.cp);
   } else {
     f3 c = q.top > -1e30f ? q.tn : q.cn;
@@ -599,7 +623,7 @@ LGX_DEV float ground_cell(const lgx_env_params* __restrict__ P, const lgx_buffer
   float gx, gy, h;
   if (fu >= fv) { gx = (h10 - h00) * ihs; gy = (h11 - h10) * ihs; h = h00 + fu * (h10 - h00) + fv * (h11 - h10); }
   else          { gx = (h11 - h01) * ihs; gy = (h01 - h00) * ihs; h = h00 + fv * (h01 - h00) + fu * (h11 - h01); }
-  const float inv = 1.0f / sqrtf(gx * gx + gy * gy + 1.0f);
+  const float inv = ph_rsqrt(gx * gx + gy * gy + 1.0f);
   *n = mk3(-gx * inv, -gy * inv, inv);
   return (h - p.z) * n->z + r;
 }
@@ -753,7 +777,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
     // every thread copies PER samples, in batches of up to 12 whose global loads are all issued
     // before the first LDS store (the copy is latency-bound otherwise: one HBM round trip per sample)
     constexpr int AREA = LGX_HF_PATCH * LGX_HF_PATCH, PER = ENVS * AREA / PHYS_BLOCK;
-    constexpr int BATCH = PER % 12 == 0 ? 12 : (PER % 9 == 0 ? 9 : 6);
+    constexpr int BATCH = PER % 12 == 0 ? 12 : PER % 9 == 0 ? 9 : PER % 8 == 0 ? 8 : PER % 6 == 0 ? 6 : 4;
     static_assert(ENVS * AREA % PHYS_BLOCK == 0 && PER % BATCH == 0, "patch copy layout");
     const int8_t* T = B.hf_trimesh;
     for (int q0 = 0; q0 < PER; q0 += BATCH) {

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
 mkdir -p gpurun_out
 for r in 1 2; do
-  for v in default exact; do
+  for v in default exact patch16; do
     if [ $v = default ]; then unset LGX_LIB_PATH; else export LGX_LIB_PATH=$PWD/build/ab/$v/liblgx.so; fi
     timeout -k 10 200 python tools/phys_bench.py go1_rough 4096 50 > gpurun_out/r04c_phys_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/r04c_phys_$v.log; exit 1; }
     echo "$v: $(grep physics gpurun_out/r04c_phys_$v.log)"
