@@ -181,7 +181,7 @@ LGX_DEV float row_quads_sum(float v) {
 // Optional LDS patch: samples (i, j) with 0 <= i - pi0, j - pj0 < LGX_HF_PATCH are read from
 // `patch` (a copy of the same int16 samples), others from H: identical values either way.
 #ifndef LGX_HF_PATCH
-#define LGX_HF_PATCH 24
+#define LGX_HF_PATCH 16
 #endif
 LGX_DEV float ground_height(const lgx_env_params* __restrict__ P, const int16_t* __restrict__ H, int rows, int cols,
                             float x, float y, f3* n, const int16_t* patch = nullptr, int pi0 = 0, int pj0 = 0) {
