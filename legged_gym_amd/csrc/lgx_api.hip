@@ -166,6 +166,10 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
     dm.lane_pts[lane][dm.lane_npts[lane]++] = i;
   }
   for (int l = 0; l < 4; ++l) dm.max_lane_npts = dm.lane_npts[l] > dm.max_lane_npts ? dm.lane_npts[l] : dm.max_lane_npts;
+  dm.joint_rot_eye = 1;
+  for (int j = 0; j < LGX_NUM_DOF; ++j)
+    for (int i = 0; i < 9; ++i)
+      if (model->joint_rot[j][i] != (i % 4 == 0 ? 1.f : 0.f)) dm.joint_rot_eye = 0;
 
   int rc = hip_check(hipSetDevice(device), "hipSetDevice");
   if (rc) return rc;

@@ -323,6 +323,9 @@ __device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pe
     v.y = elu_f(v.y + bq.y);
     v.z = elu_f(v.z + bq.z);
     v.w = elu_f(v.w + bq.w);
+    // keep the bias read and the ELU ahead of the row test: sunk into the branch, the read waited
+    // on its own LDS round trip inside it
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
   }
   if (row < g.M) *reinterpret_cast<float4*>(g.C + T.z * g.sc + row * g.ldc + T.nt * PN + cn) = v;
 }

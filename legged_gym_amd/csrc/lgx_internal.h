@@ -12,7 +12,7 @@ struct lgx_dev_model {
   lgx_model m;
   int32_t lane_npts[4];
   int32_t max_lane_npts;
-  int32_t pad;
+  int32_t joint_rot_eye;   // every joint frame rotation is the identity (URDF rpy = 0: the quadrupeds but ANYmal C)
   int32_t lane_pts[4][LGX_MAX_LANE_PTS];
   int32_t pad_tail[(4 - (sizeof(lgx_model) / 4 + 6 + 4 * LGX_MAX_LANE_PTS) % 4) % 4];   // 16-byte multiple
 };

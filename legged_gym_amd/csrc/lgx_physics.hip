@@ -260,20 +260,23 @@ LGX_DEV void arrow_solve(LegSys& L, const float* Acommon, const float* rbcommon,
 #pragma unroll
   for (int i = 0; i < 6; ++i) Y[i] = sym3_mul(Di, mk3(L.B[i][0], L.B[i][1], L.B[i][2]));
   f3 Dr = sym3_mul(Di, mk3(L.rl[0], L.rl[1], L.rl[2]));
+  // the env's common base block enters on the leg-0 lane: every lane reads it (one broadcast LDS
+  // address) and selects the sum - a read under `if (lane0)` compiles to a branch with its own
+  // lgkmcnt(0) wait, 27 serial LDS round trips per solve
   float A[21], rb[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i)
 #pragma unroll
     for (int j = i; j < 6; ++j) {
-      float v = L.Ap[sidx(i, j)] - (L.B[i][0] * Y[j].x + L.B[i][1] * Y[j].y + L.B[i][2] * Y[j].z);
-      if (lane0) v += Acommon[sidx(i, j)];
-      A[sidx(i, j)] = quad_sum(v);
+      const float ac = Acommon[sidx(i, j)];
+      const float v = L.Ap[sidx(i, j)] - (L.B[i][0] * Y[j].x + L.B[i][1] * Y[j].y + L.B[i][2] * Y[j].z);
+      A[sidx(i, j)] = quad_sum(lane0 ? v + ac : v);
     }
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    float v = L.rb[i] - (L.B[i][0] * Dr.x + L.B[i][1] * Dr.y + L.B[i][2] * Dr.z);
-    if (lane0) v += rbcommon[i];
-    rb[i] = quad_sum(v);
+    const float rc = rbcommon[i];
+    const float v = L.rb[i] - (L.B[i][0] * Dr.x + L.B[i][1] * Dr.y + L.B[i][2] * Dr.z);
+    rb[i] = quad_sum(lane0 ? v + rc : v);
   }
   chol6_solve(A, rb);
 #pragma unroll
@@ -803,6 +806,7 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
   const int pi0 = use_patch ? hf_org[eb][0] : 0, pj0 = use_patch ? hf_org[eb][1] : 0;
   const int npts = DM->lane_npts[leg];
   const int maxpts = DM->max_lane_npts;
+  const bool rot_eye = __builtin_amdgcn_readfirstlane(DM->joint_rot_eye) != 0;   // uniform
   // this lane's candidates (point index, dynamic body) per slot, fixed for the launch: the geometry
   // loop's model reads then no longer wait on one another
   int slot_pt[SLOTS], slot_db[SLOTS];
@@ -901,10 +905,13 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         int j = 3 * leg + k;
-        m33 E;
+        m33 Rjf = Rp;   // identity joint frames (every quadruped but ANYmal C): no R_p E product
+        if (!rot_eye) {
+          m33 E;
 #pragma unroll
-        for (int i = 0; i < 9; ++i) E.a[i] = M->joint_rot[j][i];
-        m33 Rjf = mul(Rp, E);
+          for (int i = 0; i < 9; ++i) E.a[i] = M->joint_rot[j][i];
+          Rjf = mul(Rp, E);
+        }
         f3 oj = op + mul(Rp, mk3(M->joint_pos[j][0], M->joint_pos[j][1], M->joint_pos[j][2]));
         f3 ax = mk3(M->joint_axis[j][0], M->joint_axis[j][1], M->joint_axis[j][2]);
         f3 aw = mul(Rjf, ax);
@@ -1000,24 +1007,25 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       int j = 3 * leg + k;
+      // model reads first (LDS): a read inside a lane-dependent branch waits on its own round trip
+      const float kp = M->kp[j], kd = M->kd[j], eff = M->dof_effort[j];
+      const float lo = M->dof_lower[j], hi = M->dof_upper[j], lk = M->limit_k, lc = M->limit_c;
       float g = 0.f;
       if (ctrl == LGX_CTRL_POS_DRIVE) {
-        float eff = M->dof_effort[j];
-        float te = M->kp[j] * (tgt[k] - th[k]) - M->kd[j] * thd[k];
+        float te = kp * (tgt[k] - th[k]) - kd * thd[k];
         if (fabsf(te) <= eff) {
           impl[k] = true;
-          Dimp[k] += dt * (M->kd[j] + dt * M->kp[j]);
-          g += M->kp[j] * (tgt[k] - th[k]);
+          Dimp[k] += dt * (kd + dt * kp);
+          g += kp * (tgt[k] - th[k]);
         } else {
           g += te > 0.f ? eff : -eff;
         }
       } else {
         g += tex[k];
       }
-      float lo = M->dof_lower[j], hi = M->dof_upper[j];
       if (lo < hi) {
-        if (th[k] < lo) { Dimp[k] += dt * (M->limit_c + dt * M->limit_k); g += M->limit_k * (lo - th[k]); }
-        else if (th[k] > hi) { Dimp[k] += dt * (M->limit_c + dt * M->limit_k); g -= M->limit_k * (th[k] - hi); }
+        if (th[k] < lo) { Dimp[k] += dt * (lc + dt * lk); g += lk * (lo - th[k]); }
+        else if (th[k] > hi) { Dimp[k] += dt * (lc + dt * lk); g -= lk * (th[k] - hi); }
       }
       rl0[k] += dt * g;
     }
