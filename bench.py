@@ -27,8 +27,9 @@ MI355X_F32_PEAK_TFLOPS = 157.3      # vector FP32 == f32 MFMA peak (MI355X_MICRO
 MI355X_HBM_PEAK_GBS = 8000.0
 # HBM bytes per launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts
 # half of wide reads), from the rocprofv3 --pmc passes of the same build (tools/pmc_round.sh ->
-# profiles/r03_pmc_env_kernels.json); the actuator net from the passes that launch it on its own
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_env_kernels.json")
+# profiles/r04_pmc_env_kernels.json); the actuator net from the passes that launch it on its own.
+# LGX_BENCH_PMC_ENV / LGX_BENCH_PMC_PPO point at a fresh pair (tools/gpu_r04e.sh: same GPU session)
+PMC_FILE = os.environ.get("LGX_BENCH_PMC_ENV") or os.path.join(ROOT, "profiles", "r04_pmc_env_kernels.json")
 
 
 def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
@@ -40,7 +41,7 @@ def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
 
 
 PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
-PPO_PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc_ppo_kernels.json")
+PPO_PMC_FILE = os.environ.get("LGX_BENCH_PMC_PPO") or os.path.join(ROOT, "profiles", "r04_pmc_ppo_kernels.json")
 MI355X_BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PRODUCTS = 6                  # split-bf16: six bf16 limb products per f32 product (lgx_gemm_split.hip)
 
@@ -444,7 +445,7 @@ def main():
             "algorithmic_per_launch": phys_flop,
             "note": ("compute roof = FP32 peak (vector FP32 = f32 MFMA = 157.3 TF on gfx950); algorithmic FLOP "
                      "from legged_gym_amd/sim/flops.py x envs x substeps; traffic = FETCH_SIZE*2 + WRITE_SIZE "
-                     "per launch from profiles/r03_pmc_env_kernels.json (tools/pmc_round.sh); latency-bound, see DESIGN.md 4.1")}
+                     "per launch from " + os.path.relpath(PMC_FILE, ROOT) + " (tools/gpu_r04e.sh); latency-bound, see DESIGN.md 4.1")}
     act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
     roof2 = {"kernel": "lgx_actuator_ws_kernel", "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
              "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None,

@@ -27,6 +27,7 @@ OUT=gpurun_out/pmc04_ppo
 rm -rf $OUT; mkdir -p $OUT
 run fetch bench FETCH_SIZE && run write bench WRITE_SIZE || exit 1
 python tools/pmc_summary.py $OUT gpurun_out/r04_pmc_ppo_kernels.json "rocprofv3 --kernel-trace --pmc, per-dispatch means over bench.py --steps 1 --warmup 1 (go1_rough, 4096 envs: 2 PPO iterations); FETCH_SIZE/WRITE_SIZE in KB (gfx950: FETCH_SIZE reads half of wide coalesced bytes)" > /dev/null || exit 1
+export LGX_BENCH_PMC_ENV=$PWD/gpurun_out/r04_pmc_env_kernels.json LGX_BENCH_PMC_PPO=$PWD/gpurun_out/r04_pmc_ppo_kernels.json
 timeout -k 10 600 python bench.py > gpurun_out/r04_bench.json 2> gpurun_out/r04_bench.err || { echo "bench failed"; tail -20 gpurun_out/r04_bench.err; exit 1; }
 cat gpurun_out/r04_bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof04 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no_cpu_baseline > gpurun_out/r04_prof_bench.json 2> gpurun_out/r04_prof.err || { echo "prof failed"; tail -20 gpurun_out/r04_prof.err; exit 1; }
