@@ -313,7 +313,7 @@ def data_parallel_check(runner, fused, comm_t, world, backend, device, dist):
     flat = fused.flat_p if fused is not None else torch.cat([p.detach().reshape(-1) for p in alg.actor_critic.parameters()])
     fp = param_fingerprint(flat, torch).view(1)
     out = {"world": world, "backend": backend, "param_fingerprint": int(fp.item())}
-    if world > 1:
+    if dist is not None:
         hi, lo, ranks = fp.clone(), fp.clone(), torch.ones(1, dtype=torch.int64, device=device)
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
@@ -347,7 +347,11 @@ def main():
     ngpu = torch.cuda.device_count() if backend != "nccl" else 0
     if ngpu:
         local = local % ngpu
-    if world > 1:
+    # LGX_DIST_REHEARSAL=1 (under torch.distributed.run, one rank): the data-parallel path - process
+    # group, parameter broadcast, bucketed gradient all-reduce, the self-check - over a one-rank
+    # communicator, on the one GPU of a test box
+    distributed = world > 1 or os.environ.get("LGX_DIST_REHEARSAL") == "1"
+    if distributed:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -387,13 +391,13 @@ def main():
     fused = getattr(runner.alg, "_fused", None)
     if fused is not None:   # HIP events around the PPO-update GEMM launches of every k-th minibatch
         fused.time_gemms(int(os.environ.get("LGX_BENCH_GEMM_TIMING", "7")))
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     runner.learn(args.steps)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     gc.enable()
@@ -405,11 +409,12 @@ def main():
     ms = (C.c_double * 3)()
     cnt = (C.c_int64 * 3)()
     lgxlib.check(lib.lgx_profile_collect(handle, ms, cnt), "lgx_profile_collect")
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
-    data_parallel = data_parallel_check(runner, fused, comm_t, world, backend if world > 1 else None, device, dist)
+    data_parallel = data_parallel_check(runner, fused, comm_t, world, backend if distributed else None, device,
+                                        dist if distributed else None)
     N = args.num_envs
     steps_per_iter = runner.num_steps_per_env
     value = steps_per_iter * N * world * args.steps / elapsed
@@ -533,7 +538,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out))
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -24,8 +24,13 @@ from .storage import RolloutStorage
 
 
 def _dist():
+    """torch.distributed when the job runs data-parallel (world > 1).  LGX_DIST_REHEARSAL=1 takes the
+    data-parallel path at world 1 too (every collective over a one-rank RCCL communicator): the
+    single-GPU rehearsal of the multi-GPU code path (bench.py, tests/test_gpu_ddp.py)."""
+    import os
     import torch.distributed as dist
-    return dist if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1 else None
+    least = 1 if os.environ.get("LGX_DIST_REHEARSAL") == "1" else 2
+    return dist if dist.is_available() and dist.is_initialized() and dist.get_world_size() >= least else None
 
 
 class PPO:

@@ -145,3 +145,32 @@ def test_bench_two_ranks_self_check(gpu, tmp_path):
     assert dp["params_identical_across_ranks"] and dp["param_fingerprint_spread"] == 0
     assert dp["bucketed_allreduce"] is True
     assert dp["allreduce"]["collectives_timed"] >= 2 and dp["allreduce"]["ms_per_iteration"] > 0
+
+
+@pytest.mark.timeout(280)
+def test_bench_rccl_rehearsal_one_rank(gpu, tmp_path):
+    """The RCCL data-parallel path on the test box's one GPU: bench.py under torch.distributed.run
+    with ONE rank, backend nccl (= RCCL), LGX_DIST_REHEARSAL=1 so the PPO takes its multi-GPU code
+    (parameter broadcast, the two-bucket gradient all-reduce from the side stream while dW1 runs,
+    the advantage-statistics and KL all-reduces) over a one-rank communicator - the launch, stream
+    and event plumbing the driver's 8-GPU run depends on, which two ranks on one device cannot
+    exercise (RCCL refuses duplicate devices)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LGX_DIST_BACKEND="nccl", LGX_DIST_REHEARSAL="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               LGX_BENCH_GEMM_TIMING="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--task", "go1_flat_bench", "--num_envs", "1024",
+           "--no_cpu_baseline"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    dp = d["data_parallel"]
+    assert dp["world"] == 1 and dp["backend"] == "nccl" and dp["ranks_seen"] == 1
+    assert dp["params_identical_across_ranks"] and dp["param_fingerprint_spread"] == 0
+    assert dp["bucketed_allreduce"] is True
+    assert dp["allreduce"]["collectives_timed"] >= 2 and dp["allreduce"]["ms_per_iteration"] > 0
