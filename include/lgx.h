@@ -383,6 +383,16 @@ int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* descs, int32_t count, void* stream
 int lgx_profile_enable(lgx_sim* sim, int32_t period);
 int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
 
+/* Cross-stream ordering events of the PPO update (the dW GEMMs on a second stream next to the dA
+ * GEMMs): hipEventDisableTiming | hipEventDisableSystemFence - the release / acquire stay at device
+ * scope (every consumer is a kernel on the same GPU; an RCCL send is a kernel on it too), so a
+ * record does not write back and invalidate the caches to system scope the way a default event
+ * does (measured ~6 us of idle GPU at every cross-stream join).  `*ev` receives a hipEvent_t. */
+int lgx_event_create(void** ev);
+int lgx_event_destroy(void* ev);
+int lgx_event_record(void* ev, void* stream);
+int lgx_stream_wait_event(void* stream, void* ev);
+
 /* Generalised advantage estimation (rsl_rl RolloutStorage.compute_returns, before the
  * advantage normalisation): rewards/values/dones [T,N] (dones uint8), last_values [N] ->
  * returns, advantages (= returns - values) [T,N]. */

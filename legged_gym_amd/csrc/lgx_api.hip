@@ -436,3 +436,30 @@ int lgx_gae_norm(const float* rewards, const float* values, const uint8_t* dones
 }
 
 }  // extern "C"
+
+// ---- device-scope cross-stream events (lgx.h: lgx_event_create)
+extern "C" int lgx_event_create(void** ev) {
+  if (!ev) return lgx_fail(LGX_EINVAL, "lgx_event_create: null out pointer");
+  hipEvent_t e = nullptr;
+  if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+    return lgx_fail(LGX_EHIP, "lgx_event_create: hipEventCreateWithFlags failed");
+  *ev = reinterpret_cast<void*>(e);
+  return LGX_OK;
+}
+extern "C" int lgx_event_destroy(void* ev) {
+  if (!ev) return LGX_OK;
+  return hipEventDestroy(reinterpret_cast<hipEvent_t>(ev)) == hipSuccess ? LGX_OK
+                                                                         : lgx_fail(LGX_EHIP, "lgx_event_destroy failed");
+}
+extern "C" int lgx_event_record(void* ev, void* stream) {
+  if (!ev) return lgx_fail(LGX_EINVAL, "lgx_event_record: null event");
+  return hipEventRecord(reinterpret_cast<hipEvent_t>(ev), reinterpret_cast<hipStream_t>(stream)) == hipSuccess
+             ? LGX_OK
+             : lgx_fail(LGX_EHIP, "lgx_event_record: hipEventRecord failed");
+}
+extern "C" int lgx_stream_wait_event(void* stream, void* ev) {
+  if (!ev) return lgx_fail(LGX_EINVAL, "lgx_stream_wait_event: null event");
+  return hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(ev), 0) == hipSuccess
+             ? LGX_OK
+             : lgx_fail(LGX_EHIP, "lgx_stream_wait_event: hipStreamWaitEvent failed");
+}

@@ -711,6 +711,33 @@ class FusedPPOUpdate:
             k = self.k_alg.get(id(g), g.K)
             self._t_events.append((g.epi, 2.0 * g.M * g.N * k * g.batch, e0, e1))
 
+    def _join(self, src, dst, slot):
+        """Order `dst` after the work issued so far on `src` (slot: 0..L-1 the side stream's inputs,
+        L its output).  Device-scope events (lgx_event_*: no system-scope cache write-back and
+        invalidate at the record, ~6 us of idle GPU per join with default events) unless
+        LGX_PPO_DEV_EVENTS=0 (torch events; read per call for same-process A/B runs)."""
+        if os.environ.get("LGX_PPO_DEV_EVENTS", "1") != "0":
+            if getattr(self, "_dev_ev", None) is None:
+                self._dev_ev = []
+                for _ in range(self.L + 1):
+                    e = C.c_void_p()
+                    self.check(self.lib.lgx_event_create(C.byref(e)), "event_create")
+                    self._dev_ev.append(e)
+            e = self._dev_ev[slot]
+            self.check(self.lib.lgx_event_record(e, C.c_void_p(src.cuda_stream)), "event_record")
+            self.check(self.lib.lgx_stream_wait_event(C.c_void_p(dst.cuda_stream), e), "stream_wait_event")
+        else:
+            e = self._ev_in[slot] if slot < self.L else self._ev_out
+            e.record(src)
+            dst.wait_event(e)
+
+    def __del__(self):
+        for e in getattr(self, "_dev_ev", None) or []:
+            try:
+                self.lib.lgx_event_destroy(e)
+            except Exception:
+                pass
+
     def _gemm_tn(self, t, stream, torch_stream=None):
         rec = getattr(self, "_t_period", 0) and self._t_count % self._t_period == 0   # (as _gemm)
         if rec:   # (events on the stream the kernel runs on)
@@ -831,8 +858,7 @@ class FusedPPOUpdate:
                     self._ev_in = [torch.cuda.Event() for _ in range(L)]
                     self._ev_out = torch.cuda.Event()
                 main = torch.cuda.current_stream(self.dev)
-                self._ev_in[k].record(main)
-                self._side.wait_event(self._ev_in[k])
+                self._join(main, self._side, k)
                 for t in self.gemm_dw[k]:
                     self._gemm_tn(t, C.c_void_p(self._side.cuda_stream), self._side)
                 side_used = True
@@ -855,8 +881,7 @@ class FusedPPOUpdate:
             # every gradient block but dW1's is complete once dA_1 (this stream) and the side
             # stream's dW GEMMs are: reduce them (+ the loss finalize) on the side stream while dW1
             # runs here - the memory-bound reduction next to the MFMA-bound GEMM
-            self._ev_in[0].record(torch.cuda.current_stream(self.dev))
-            self._side.wait_event(self._ev_in[0])
+            self._join(torch.cuda.current_stream(self.dev), self._side, 0)
             chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
                                                C.c_void_p(self._side.cuda_stream)), "reduce")
         bucketed = early and apply and ppo.dist is not None
@@ -883,14 +908,12 @@ class FusedPPOUpdate:
             torch.bmm(dZ[0].view(S, M // S, h[0]).transpose(1, 2), X.unflatten(0, (S, M // S)), out=self.P[0][0])
             torch.bmm(dZ[1].view(S, M // S, h[0]).transpose(1, 2), Xc.unflatten(0, (S, M // S)), out=self.P[0][1])
         if side_used and not early:   # the weight gradients are complete before the reduction reads them
-            self._ev_out.record(self._side)
-            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
+            self._join(self._side, torch.cuda.current_stream(self.dev), L)
         if early:   # (dW1's partials come from this stream; the side stream's blocks are joined below)
             chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
             if bucketed:
                 self._all_reduce(self.g_comm[:self.nW1], torch.cuda.current_stream(self.dev))
-            self._ev_out.record(self._side)
-            torch.cuda.current_stream(self.dev).wait_event(self._ev_out)
+            self._join(self._side, torch.cuda.current_stream(self.dev), L)
         elif self.loss_bwd:
             chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
         else:

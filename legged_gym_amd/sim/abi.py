@@ -226,6 +226,10 @@ def declare(lib, prefix="lgx"):
                                     C.c_float, C.c_float, vp]),
             "adam_clip_mirror": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
                                            C.c_float, C.c_float, C.POINTER(LgxCopy2dJob), i32, vp]),
+            "event_create": (C.c_int, [C.POINTER(vp)]),
+            "event_destroy": (C.c_int, [vp]),
+            "event_record": (C.c_int, [vp, vp]),
+            "stream_wait_event": (C.c_int, [vp, vp]),
         })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}")
@@ -243,7 +247,8 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trim
             "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store", "lgx_ppo_act_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
-            "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward"]
+            "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward",
+            "lgx_event_create", "lgx_event_destroy", "lgx_event_record", "lgx_stream_wait_event"]
 
 
 def check_layout(sizes_fn, n=12):
