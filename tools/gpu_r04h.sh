@@ -16,6 +16,6 @@ done
 unset LGX_LIB_PATH
 LGX_LIB_PATH=build/clock/liblgx.so timeout -k 10 200 python tools/phys_bench.py go1_rough 4096 3 > gpurun_out/r04h_phys_clock.log 2>&1 || { echo "clock bench failed"; tail -5 gpurun_out/r04h_phys_clock.log; exit 1; }
 grep "physics cycles" gpurun_out/r04h_phys_clock.log | tail -2
-timeout -k 10 900 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_terrain.py tests/test_gpu_golden.py \
+env ${TEST_LIB:+LGX_LIB_PATH=$TEST_LIB} timeout -k 10 900 python -u -m pytest -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_terrain.py tests/test_gpu_golden.py \
   > gpurun_out/r04h_tests.log 2>&1
 grep -E "FAIL|Error|passed|failed" gpurun_out/r04h_tests.log | tail -30
