@@ -95,10 +95,6 @@ LGX_DEV float sv_get(const sv& v, int i) {
 #ifndef LGX_PHYS_FAST_TRANSC
 #define LGX_PHYS_FAST_TRANSC 1
 #endif
-// contact-term reduction as one lane fetch when every leg's terms sit on one PP lane; 0 for A/B
-#ifndef LGX_PHYS_SINGLE_LANE_SUM
-#define LGX_PHYS_SINGLE_LANE_SUM 0
-#endif
 
 // 6x6 SPD solve (packed sym), in registers
 // (the substitutions multiply by the factorisation's reciprocal diagonal: 12 of the 18 correctly
@@ -1209,12 +1205,10 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
 #pragma unroll
       for (int i = 0; i < 6; ++i) L.D[i] = 0.f;
       L.rl[0] = L.rl[1] = L.rl[2] = 0.f;
-      bool any_c = false;   // this lane added a contact term
       for (int c = pl, sl = 0; c < maxpts; c += PP, ++sl) {
         if (c >= npts) break;
         const float4 st = slot_state[sl][tid];
         if (st.x == 0.f) continue;  // separated (pass 1: in pass 0's classification)
-        any_c = true;
         const float4 gp = geo_p[sl][tid], gn = geo_n[sl][tid];
         const f3 Pc = mk3(gp.x, gp.y, gp.z);
         const float depth = gp.w;
@@ -1226,48 +1220,18 @@ lgx_physics_kernel(const lgx_dev_model* __restrict__ DMg, const lgx_env_params* 
         if (pass == 1 && st.x == 2.f) f = f + dt * mk3(st.y, st.z, st.w);
         add_contact(L, Pc, n, wn, wt, f, k, S);
       }
-      // reduce the contact terms over the PP lanes of the leg, add the contact-free system.  When
-      // no leg of the wave has contact terms on more than one of its PP lanes (the common case: a
-      // foot sphere), the sum is that lane's value plus exact zeros - the same bits - so it is
-      // fetched with one ds_bpermute per term instead of the DPP reduction (5 VALU per term)
-      int src = -1;
-#if LGX_PHYS_SINGLE_LANE_SUM
-      if (PP == 4) {
-        const int wl = tid & 63;
-        const uint64_t cm = __ballot(any_c);
-        const uint32_t gm = (uint32_t)(cm >> (wl & ~12)) & 0x1111u;   // this leg's 4 PP lanes (bits 0, 4, 8, 12)
-        if (__ballot((gm & (gm - 1u)) != 0u) == 0ull)                  // wave-uniform: at most one per leg
-          src = gm ? (wl & ~12) + __builtin_ctz(gm) : wl;
+      // reduce the contact terms over the PP lanes of the leg, add the contact-free system
+#pragma unroll
+      for (int i = 0; i < 21; ++i) L.Ap[i] = psum<PP>(L.Ap[i]);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        L.rb[i] = psum<PP>(L.rb[i]) + lsys[24 + i];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) L.B[i][k] = psum<PP>(L.B[i][k]) + lsys[3 * i + k];
+        L.D[i] = psum<PP>(L.D[i]) + lsys[18 + i];
       }
-#endif
-#ifdef LGX_PHASE_CLOCK
-      lgx_clk_acc[9] += src >= 0 ? 1 : 1000;   // tuning builds: single-lane fetches / DPP reductions
-#endif
-      if (src >= 0) {
 #pragma unroll
-        for (int i = 0; i < 21; ++i) L.Ap[i] = __shfl(L.Ap[i], src);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          L.rb[i] = __shfl(L.rb[i], src) + lsys[24 + i];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) L.B[i][k] = __shfl(L.B[i][k], src) + lsys[3 * i + k];
-          L.D[i] = __shfl(L.D[i], src) + lsys[18 + i];
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) L.rl[k] = __shfl(L.rl[k], src) + lsys[30 + k];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 21; ++i) L.Ap[i] = psum<PP>(L.Ap[i]);
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          L.rb[i] = psum<PP>(L.rb[i]) + lsys[24 + i];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) L.B[i][k] = psum<PP>(L.B[i][k]) + lsys[3 * i + k];
-          L.D[i] = psum<PP>(L.D[i]) + lsys[18 + i];
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + lsys[30 + k];
-      }
+      for (int k = 0; k < 3; ++k) L.rl[k] = psum<PP>(L.rl[k]) + lsys[30 + k];
       if (pass == 0) LGX_CLK(3); else LGX_CLK(7);
       arrow_solve(L, ecom, ecom + 21, lane0, xb, xl);
       LGX_CLK(4);
