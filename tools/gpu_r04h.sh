@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" 2>/dev/null || true
 mkdir -p gpurun_out
 for task in "go1_rough 4096" "anymal_c_rough 8192"; do
   for r in 1 2; do
-    for v in single default; do
+    for v in head default; do
       if [ $v = default ]; then unset LGX_LIB_PATH; else export LGX_LIB_PATH=$PWD/build/ab/$v/liblgx.so; fi
       timeout -k 10 200 python tools/phys_bench.py $task 50 > gpurun_out/r04h_phys_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/r04h_phys_$v.log; exit 1; }
       echo "$v: $(grep physics gpurun_out/r04h_phys_$v.log)"
