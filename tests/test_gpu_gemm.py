@@ -363,3 +363,27 @@ def test_elu_near_zero_bound(gpu):
     # and where the cancellation is mild (|x| >= 2^-8) the relative error is f32-level
     mild = x.abs() >= 2 ** -8
     assert rel[mild].max().item() <= 6e-5, rel[mild].max().item()
+
+
+def test_device_scope_events_order_two_streams(gpu):
+    """lgx_event_create / lgx_event_record / lgx_stream_wait_event (the PPO update's cross-stream
+    joins, device-scope release): a consumer stream ordered after a producer stream's long chain
+    of launches reads the producer's final values; destroy accepts the handle."""
+    lib = _lib()
+    dev = "cuda:0"
+    prod, cons = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    ev = C.c_void_p()
+    lgxlib.check(lib.lgx_event_create(C.byref(ev)), "event_create")
+    x = torch.zeros(4096, 4096, device=dev)
+    w = torch.eye(4096, device=dev)
+    with torch.cuda.stream(prod):
+        for i in range(8):                     # long enough that an unordered reader would race it
+            x = x @ w + 1.0
+    lgxlib.check(lib.lgx_event_record(ev, C.c_void_p(prod.cuda_stream)), "event_record")
+    lgxlib.check(lib.lgx_stream_wait_event(C.c_void_p(cons.cuda_stream), ev), "stream_wait_event")
+    with torch.cuda.stream(cons):
+        y = x.sum()
+    torch.cuda.synchronize()
+    assert y.item() == pytest.approx(8.0 * 4096 * 4096)
+    assert lib.lgx_event_destroy(ev) == 0
+    assert lib.lgx_event_record(None, None) != 0      # null event: error status, no crash
