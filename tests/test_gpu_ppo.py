@@ -120,6 +120,26 @@ def test_fused_update_single_stream(gpu, monkeypatch):
     assert getattr(fus._fused, "_side", None) is None
 
 
+@pytest.mark.parametrize("var,val", [("LGX_GEMM_TN_F32", "1"), ("LGX_PPO_DEV_EVENTS", "0")])
+def test_fused_update_ab_variants(gpu, monkeypatch, var, val):
+    """The update's A/B variants against autograd: the exact-f32 MFMA weight-gradient kernel
+    (LGX_GEMM_TN_F32=1) and torch events for the cross-stream joins (LGX_PPO_DEV_EVENTS=0)."""
+    monkeypatch.setenv(var, val)
+    ref, fus = make_pair()
+    torch.manual_seed(11)
+    vl_r, sl_r = ref.update()
+    torch.manual_seed(11)
+    vl_f, sl_f = fus.update()
+    assert fus.learning_rate == ref.learning_rate
+    assert abs(vl_f - vl_r) <= 1e-4 * abs(vl_r) + 1e-6 and abs(sl_f - sl_r) <= 1e-4 * abs(sl_r) + 1e-6
+    big = total = 0   # (the criterion of test_fused_update_matches_autograd_update below)
+    for (n, a), b in zip(fus.actor_critic.named_parameters(), ref.actor_critic.parameters()):
+        d = (a - b).abs()
+        big += (d > 1e-5).sum().item()
+        total += d.numel()
+    assert big <= 1e-3 * total, (big, total)
+
+
 def test_fused_minibatch_gradient_separate_loss_and_head(gpu, monkeypatch):
     """lgx_ppo_loss + lgx_head_bwd_finalize as two launches (LGX_PPO_LOSS_BWD=0) instead of
     lgx_ppo_loss_bwd: minibatch gradient and a full update against autograd."""
