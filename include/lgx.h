@@ -387,7 +387,8 @@ int lgx_profile_collect(lgx_sim* sim, double* ms, int64_t* count);
  * GEMMs): hipEventDisableTiming | hipEventDisableSystemFence - the release / acquire stay at device
  * scope (every consumer is a kernel on the same GPU; an RCCL send is a kernel on it too), so a
  * record does not write back and invalidate the caches to system scope the way a default event
- * does (measured ~6 us of idle GPU at every cross-stream join).  `*ev` receives a hipEvent_t. */
+ * does.  The PPO update uses them in single-process runs; data-parallel runs keep system-scope
+ * events (their joins also order buffers that RCCL peers write).  `*ev` receives a hipEvent_t. */
 int lgx_event_create(void** ev);
 int lgx_event_destroy(void* ev);
 int lgx_event_record(void* ev, void* stream);

@@ -714,9 +714,10 @@ class FusedPPOUpdate:
     def _join(self, src, dst, slot):
         """Order `dst` after the work issued so far on `src` (slot: 0..L-1 the side stream's inputs,
         L its output).  Device-scope events (lgx_event_*: no system-scope cache write-back and
-        invalidate at the record, ~6 us of idle GPU per join with default events) unless
-        LGX_PPO_DEV_EVENTS=0 (torch events; read per call for same-process A/B runs)."""
-        if os.environ.get("LGX_PPO_DEV_EVENTS", "1") != "0":
+        invalidate at the record) in single-process runs unless LGX_PPO_DEV_EVENTS=0 (torch events;
+        read per call for same-process A/B runs).  Data-parallel runs keep the system-scope events:
+        the joins there also order the collectives' buffers, which peers write over xGMI."""
+        if os.environ.get("LGX_PPO_DEV_EVENTS", "1") != "0" and self.ppo.dist is None:
             if getattr(self, "_dev_ev", None) is None:
                 self._dev_ev = []
                 for _ in range(self.L + 1):
