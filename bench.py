@@ -6,8 +6,10 @@ One "step" = one PPO iteration: 24 x (policy act on the fused MFMA MLP + lgx_ste
 5 epochs x 4 minibatches of PPO (fused f32-MFMA update, RCCL gradient all-reduce when N>1).
 value = 24 * envs_per_gpu * world * K / max-over-ranks wall time of K iterations.
 
-Launch: python bench.py [--gpus 1 --steps K --warmup W]; for N>1 the driver uses
-torch.distributed.run (one rank per GPU, env vars RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*).
+Launch: python bench.py [--gpus N --steps K --warmup W].  Under torch.distributed.run (one rank
+per GPU, env vars RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*) WORLD_SIZE must equal --gpus; without a
+launcher, --gpus N > 1 starts the N ranks itself (torch.distributed.run as a child process, before
+anything touches the GPU), passes rank 0's JSON line through and exits with the launcher's code.
 """
 import argparse
 import ctypes as C
@@ -322,6 +324,7 @@ def data_parallel_check(runner, fused, comm_t, world, backend, device, dist):
                    params_identical_across_ranks=bool((hi == lo).item()))
     if fused is not None:
         out["bucketed_allreduce"] = bool(fused.bucketed)
+        out["join_events"] = fused.join_events   # cross-stream joins: "system" whenever data-parallel
         n, ms, nbytes, mbs = comm_t
         mb_per_iter = alg.num_learning_epochs * alg.num_mini_batches
         out["allreduce"] = {"collectives_timed": n, "bytes_per_minibatch": (nbytes / mbs) if mbs else 0,
@@ -331,8 +334,38 @@ def data_parallel_check(runner, fused, comm_t, world, backend, device, dist):
     return out
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """--gpus n > 1 without a launcher: run this script as n ranks under torch.distributed.run in a
+    child process (never exec: nothing here has touched the GPU, and the child owns the ranks),
+    stdout passed through (rank 0 prints the JSON line); returns the launcher's exit code, non-zero
+    when any rank failed."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least one GPU")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}: "
+                         "one rank per GPU, the two must agree")
     if args.actuator_net_torques and not args.task.startswith("anymal"):
         raise SystemExit("--actuator_net_torques: the SEA actuator network is ANYmal's (anymal.py:71-78); "
                          f"task {args.task} has no actuator-net torque source")

@@ -411,6 +411,18 @@ int lgx_gae_norm(const float* rewards, const float* values, const uint8_t* dones
                  float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam, double* scratch,
                  void* stream);
 
+/* The data-parallel form of lgx_gae_norm (global statistics over every rank's advantages, as one
+ * process holding all ranks' envs would normalise): lgx_gae_parts runs the GAE and writes this
+ * rank's per-workgroup (count, mean, M2) summaries, lgx_gae_norm_scratch(N) doubles, to `parts`;
+ * the host gathers every rank's parts (torch.distributed all_gather, rank order) and
+ * lgx_adv_norm normalises this rank's n = T*N advantages in place with the statistics of the
+ * `nparts` gathered summaries (combined in order, so every rank applies the same mean / std; at
+ * world 1 the result is bitwise lgx_gae_norm's). */
+int lgx_gae_parts(const float* rewards, const float* values, const uint8_t* dones, const float* last_values,
+                  float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam, double* parts,
+                  void* stream);
+int lgx_adv_norm(float* advantages, int64_t n, const double* parts, int32_t nparts, void* stream);
+
 /* ---- PPO update (rsl_rl PPO.update, legged_robot_config.py:226-239): the non-GEMM work of a
  * minibatch step.  Activations are net-major [2 (actor, critic), M, H]; the GEMMs between
  * these calls are library GEMMs issued by the host.  All pointers are device pointers. */

@@ -144,6 +144,14 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   const bool dense = leg_dof == 6 || (force_dense && atoi(force_dense) == 1);
   if (dense && (params->control_type == LGX_CTRL_SEA || params->use_actuator_history))
     return fail(LGX_EINVAL, "lgx_sim_create: the dense physics kernel has no SEA / actuator-history drive inputs");
+  // every contact candidate's dynamic body and reporting body index into fixed tables (LDS in both
+  // physics kernels): checked for every point, whichever kernel runs
+  for (int i = 0; i < model->num_points; ++i) {
+    if (model->point_dyn[i] < 0 || model->point_dyn[i] >= LGX_NUM_DYN)
+      return fail(LGX_EINVAL, "lgx_sim_create: bad point_dyn");
+    if (model->point_report[i] < 0 || model->point_report[i] >= LGX_MAX_BODIES)
+      return fail(LGX_EINVAL, "lgx_sim_create: bad point_report");
+  }
   // per-lane contact candidate tables: leg points to their leg's lane, base points round-robin
   lgx_dev_model dm;
   memset(&dm, 0, sizeof dm);
@@ -433,6 +441,22 @@ int lgx_gae_norm(const float* rewards, const float* values, const uint8_t* dones
   return launch_check(lgx_launch_gae_norm(rewards, values, dones, last_values, returns, advantages, T, N, gamma, lam,
                                           scratch, (hipStream_t)stream),
                       "lgx_gae_norm: launch (T, N must be > 0)");
+}
+
+int lgx_gae_parts(const float* rewards, const float* values, const uint8_t* dones, const float* last_values,
+                  float* returns, float* advantages, int32_t T, int32_t N, float gamma, float lam, double* parts,
+                  void* stream) {
+  if (!rewards || !values || !dones || !last_values || !returns || !advantages || !parts)
+    return fail(LGX_EINVAL, "lgx_gae_parts: null argument");
+  return launch_check(lgx_launch_gae_parts(rewards, values, dones, last_values, returns, advantages, T, N, gamma, lam,
+                                           parts, (hipStream_t)stream),
+                      "lgx_gae_parts: launch (T, N must be > 0)");
+}
+
+int lgx_adv_norm(float* advantages, int64_t n, const double* parts, int32_t nparts, void* stream) {
+  if (!advantages || !parts) return fail(LGX_EINVAL, "lgx_adv_norm: null argument");
+  return launch_check(lgx_launch_adv_norm(advantages, n, parts, nparts, (hipStream_t)stream),
+                      "lgx_adv_norm: launch (n, nparts must be > 0)");
 }
 
 }  // extern "C"

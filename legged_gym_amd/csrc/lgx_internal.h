@@ -51,6 +51,9 @@ int lgx_launch_mlp_forward(const float* x, float* y, int64_t rows, int32_t nl, c
 int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t stream);
 int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                    float* adv, int32_t T, int32_t N, float gamma, float lam, hipStream_t stream);
+int lgx_launch_gae_parts(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
+                         float* adv, int32_t T, int32_t N, float gamma, float lam, double* parts, hipStream_t stream);
+int lgx_launch_adv_norm(float* adv, int64_t n, const double* parts, int32_t nparts, hipStream_t stream);
 int lgx_launch_gae_norm(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
                         float* adv, int32_t T, int32_t N, float gamma, float lam, double* scratch, hipStream_t stream);
 

@@ -1774,6 +1774,8 @@ __global__ void __launch_bounds__(64) lgx_physics_dense_kernel(const lgx_dev_mod
       for (int leg = 0; leg < NL; ++leg) c += L.Froot[leg][i];
       L.Cb[i] = c;
     }
+    // (H's base block and Cb are read by other lanes below, also when no candidate loop runs)
+    __syncthreads();
     // ---- contact candidates: one lane per point, compacted in point order
     const int npts = M->num_points;
     for (int i0 = 0; i0 < npts; i0 += 64) {

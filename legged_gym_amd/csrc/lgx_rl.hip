@@ -65,14 +65,15 @@ __global__ void __launch_bounds__(256) lgx_gae_kernel(const float* __restrict__ 
 
 // rsl_rl's advantage normalisation, (adv - adv.mean()) / (adv.std() + 1e-8) with the unbiased
 // std, in place: every workgroup re-combines the GAE summaries in the same order (double), then
-// normalises its slice in f32 as torch does from the f32 mean / std
+// normalises its slice in f32 as torch does from the f32 mean / std.  The summaries may cover more
+// samples than the n normalised here (data-parallel: every rank's summaries, in rank order)
 __global__ void __launch_bounds__(256) lgx_adv_norm_kernel(float* __restrict__ adv, int64_t n,
                                                            const double* __restrict__ part, int32_t nparts) {
   __shared__ float ms[2];
   if (threadIdx.x == 0) {
     MomentSummary s = {0.0, 0.0, 0.0};
     for (int i = 0; i < nparts; ++i) s = moments_combine(s, {part[3 * i], part[3 * i + 1], part[3 * i + 2]});
-    const double var = n > 1 ? s.m2 / (double)(n - 1) : 0.0;
+    const double var = s.n > 1.0 ? s.m2 / (s.n - 1.0) : 0.0;
     ms[0] = (float)s.mean;
     ms[1] = (float)sqrt(var) + 1e-8f;
   }
@@ -87,6 +88,21 @@ int lgx_launch_gae(const float* rew, const float* val, const uint8_t* dones, con
   if (T <= 0 || N <= 0) return -1;
   hipLaunchKernelGGL(lgx_gae_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, rew, val, dones, last_val, ret, adv, T,
                      N, gamma, lam, (double*)nullptr);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int lgx_launch_gae_parts(const float* rew, const float* val, const uint8_t* dones, const float* last_val, float* ret,
+                         float* adv, int32_t T, int32_t N, float gamma, float lam, double* parts, hipStream_t stream) {
+  if (T <= 0 || N <= 0) return -1;
+  hipLaunchKernelGGL(lgx_gae_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, rew, val, dones, last_val, ret, adv, T,
+                     N, gamma, lam, parts);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int lgx_launch_adv_norm(float* adv, int64_t n, const double* parts, int32_t nparts, hipStream_t stream) {
+  if (n <= 0 || nparts <= 0) return -1;
+  const int blocks = (int)std::min<int64_t>((n + 1023) / 1024, 256);
+  hipLaunchKernelGGL(lgx_adv_norm_kernel, dim3(blocks), dim3(256), 0, stream, adv, n, parts, nparts);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -711,13 +711,18 @@ class FusedPPOUpdate:
             k = self.k_alg.get(id(g), g.K)
             self._t_events.append((g.epi, 2.0 * g.M * g.N * k * g.batch, e0, e1))
 
+    @property
+    def join_events(self):
+        """"device" (lgx_event_*) or "system" (torch events): the event kind _join uses."""
+        return "device" if (os.environ.get("LGX_PPO_DEV_EVENTS", "1") != "0" and self.ppo.dist is None) else "system"
+
     def _join(self, src, dst, slot):
         """Order `dst` after the work issued so far on `src` (slot: 0..L-1 the side stream's inputs,
         L its output).  Device-scope events (lgx_event_*: no system-scope cache write-back and
         invalidate at the record) in single-process runs unless LGX_PPO_DEV_EVENTS=0 (torch events;
         read per call for same-process A/B runs).  Data-parallel runs keep the system-scope events:
         the joins there also order the collectives' buffers, which peers write over xGMI."""
-        if os.environ.get("LGX_PPO_DEV_EVENTS", "1") != "0" and self.ppo.dist is None:
+        if self.join_events == "device":
             if getattr(self, "_dev_ev", None) is None:
                 self._dev_ev = []
                 for _ in range(self.L + 1):

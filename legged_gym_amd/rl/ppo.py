@@ -216,21 +216,21 @@ class PPO:
         self._fused.check(self._fused.lib.lgx_ppo_store(C.byref(pend[0]), C.c_void_p(
             torch.cuda.current_stream(pend[1].device).cuda_stream)), "lgx_ppo_store")
 
-    def _adv_stats(self, adv):
+    def _gather_moments(self, parts):
+        """Every rank's flat float64 (count, mean, M2) advantage summaries, concatenated in rank order
+        (all_gather: identical on every rank, so every rank normalises with the same statistics)."""
+        parts = parts.contiguous()
         if self.dist is None:
-            return adv.mean(), adv.std()
-        s = torch.stack([adv.sum(), (adv * adv).sum(), torch.tensor(float(adv.numel()), device=adv.device)])
-        self.dist.all_reduce(s)
-        n = s[2]
-        mean = s[0] / n
-        var = (s[1] - n * mean * mean) / (n - 1)
-        return mean, var.clamp(min=0).sqrt()
+            return parts
+        out = [torch.empty_like(parts) for _ in range(self.dist.get_world_size())]
+        self.dist.all_gather(out, parts)
+        return torch.cat(out)
 
     def compute_returns(self, last_critic_obs):
         self.flush_store()
         last_values = self.actor_critic.evaluate(last_critic_obs).detach()
         self.storage.compute_returns(last_values, self.gamma, self.lam,
-                                     reduce_stats=self._adv_stats if self.dist is not None else None)
+                                     reduce_stats=self._gather_moments if self.dist is not None else None)
 
     # ---------------------------------------------------------------- update
     def _allreduce_grads(self):

@@ -81,6 +81,7 @@ class OnPolicyRunner:
         # launch (LGX_DEFER_STORE=0: its own launch, as before)
         self.alg.defer_store = os.environ.get("LGX_DEFER_STORE", "1") != "0"
         tot_iter = self.current_learning_iteration + num_learning_iterations
+        completed = False
         try:
             for it in range(self.current_learning_iteration, tot_iter):
                 start = time.time()
@@ -116,8 +117,8 @@ class OnPolicyRunner:
                     self.alg.flush_store()           # (the last step's storage row: no act follows it)
                     self.alg.compute_returns(critic_obs)
                 if pending is not None:
-                    self._finish_deferred(pending)
-                    pending = None
+                    p, pending = pending, None
+                    self._finish_deferred(p)
                 if defer:
                     self.alg.update(defer=True)
                     ev[2].record()
@@ -140,15 +141,24 @@ class OnPolicyRunner:
                     if it % self.save_interval == 0:
                         self.save(os.path.join(self.log_dir, f"model_{it}.pt"))
                 ep_infos.clear()
+            completed = True
         finally:
             # also on an exception: no deferred storage row may outlive learn() holding pointers to
             # the env's reward / reset / time-out buffers (the env has not stepped since that row's
             # process_env_step: every env.step follows an act, which takes the pending row), and no
-            # update readback stays pending
-            self.alg.flush_store()
+            # update readback stays pending.  While an exception propagates (possibly a GPU error,
+            # which the cleanup's launches and synchronisation would raise again) the cleanup is
+            # best-effort and the original exception is the one reported.
             self.alg.defer_store = False
-            if pending is not None:
-                self._finish_deferred(pending)
+            p, pending = pending, None
+            try:
+                self.alg.flush_store()
+                if p is not None:
+                    self._finish_deferred(p)
+            except Exception:
+                if completed:
+                    raise
+                self.alg._pending_store = None
         self.current_learning_iteration += num_learning_iterations
         if self.log_dir is not None:
             self.save(os.path.join(self.log_dir, f"model_{self.current_learning_iteration}.pt"))

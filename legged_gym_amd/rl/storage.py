@@ -2,10 +2,40 @@
 
 GAE (rsl_rl compute_returns: gamma/lam recursion with done masking, then advantage
 normalisation) runs as ONE HIP kernel (lgx GAE, one thread per env over the T steps) on the
-GPU; the normalisation statistics are optionally all-reduced across ranks so that N ranks x B
-envs normalise exactly like 1 rank x N*B envs.
+GPU; in a data-parallel run the normalisation statistics are global: every rank's (count, mean,
+M2) summaries of its advantages (float64) are gathered in rank order and combined with Chan's
+pairwise formula, so N ranks x B envs normalise like 1 rank x N*B envs (no sum / sum-of-squares
+cancellation when |mean| >> std).
 """
+import math
+
 import torch
+
+
+def moments_combine(a, b):
+    """Chan et al.'s pairwise combination of (count, mean, M2) summaries (lgx_rl.hip)."""
+    n = a[0] + b[0]
+    if n == 0.0:
+        return a
+    d = b[1] - a[1]
+    return (n, a[1] + d * (b[0] / n), a[2] + b[2] + d * d * (a[0] * b[0] / n))
+
+
+def local_moments(x):
+    """(count, mean, M2) of x as a float64 [3] tensor (two passes)."""
+    xd = x.double().reshape(-1)
+    mean = xd.mean()
+    return torch.stack([torch.tensor(float(xd.numel()), dtype=torch.float64, device=x.device), mean,
+                        ((xd - mean) ** 2).sum()])
+
+
+def combined_mean_std(parts):
+    """(mean, unbiased std) as Python floats from a flat [3 k] tensor of summaries, combined in order."""
+    s = (0.0, 0.0, 0.0)
+    for n, m, m2 in parts.detach().double().cpu().view(-1, 3).tolist():
+        s = moments_combine(s, (n, m, m2))
+    var = s[2] / (s[0] - 1.0) if s[0] > 1.0 else 0.0
+    return s[1], math.sqrt(var)
 
 
 class RolloutStorage:
@@ -70,14 +100,21 @@ class RolloutStorage:
         self.step = 0
 
     def compute_returns(self, last_values, gamma, lam, reduce_stats=None):
-        """rsl_rl RolloutStorage.compute_returns (+ optional cross-rank statistics)."""
+        """rsl_rl RolloutStorage.compute_returns.  reduce_stats (data-parallel): a callable taking this
+        rank's flat float64 (count, mean, M2) summaries and returning every rank's, concatenated in
+        rank order (PPO._gather_moments)."""
         if self.returns.is_cuda:
             from legged_gym_amd.rl import fused
             if reduce_stats is None:   # one process: the normalisation rides on the GAE launch pair
                 fused.gae_norm(self.rewards, self.values, self.dones, last_values.contiguous(), self.returns,
                                self.advantages, gamma, lam)
                 return
-            fused.gae(self.rewards, self.values, self.dones, last_values, self.returns, self.advantages, gamma, lam)
+            # data-parallel: the same per-workgroup summaries, every rank's combined in rank order
+            # (at world 1 bitwise lgx_gae_norm)
+            parts = fused.gae_parts(self.rewards, self.values, self.dones, last_values.contiguous(), self.returns,
+                                    self.advantages, gamma, lam)
+            fused.adv_norm(self.advantages, reduce_stats(parts))
+            return
         else:
             advantage = 0
             for step in reversed(range(self.num_transitions_per_env)):
@@ -90,9 +127,11 @@ class RolloutStorage:
         adv = self.advantages
         if reduce_stats is None:
             mean, std = adv.mean(), adv.std()
-        else:
-            mean, std = reduce_stats(adv)
-        self.advantages = (adv - mean) / (std + 1e-8)
+            self.advantages = (adv - mean) / (std + 1e-8)
+        else:   # f32 mean / std from the float64 global statistics, as lgx_adv_norm
+            mean, std = combined_mean_std(reduce_stats(local_moments(adv)))
+            self.advantages = (adv - torch.tensor(mean, dtype=adv.dtype)) / (
+                torch.tensor(std, dtype=adv.dtype) + 1e-8)
 
     def get_statistics(self):
         done = self.dones.clone()

@@ -179,6 +179,8 @@ def declare(lib, prefix="lgx"):
         "gae": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp]),
         "gae_norm_scratch": (i64, [i32]),
         "gae_norm": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp]),
+        "gae_parts": (C.c_int, [vp, vp, vp, vp, vp, vp, i32, i32, C.c_float, C.c_float, vp, vp]),
+        "adv_norm": (C.c_int, [vp, i64, vp, i32, vp]),
         "profile_enable": (C.c_int, [vp, i32]),
         "mlp_forward_batch": (C.c_int, [C.POINTER(LgxMlpDesc), i32, vp]),
         "profile_collect": (C.c_int, [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64)]),
@@ -240,7 +242,7 @@ def declare(lib, prefix="lgx"):
 
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trimesh_build", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
             "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_step_from", "lgx_drive_inputs", "lgx_ground_contact", "lgx_sync_aux",
-            "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae", "lgx_gae_norm_scratch", "lgx_gae_norm",
+            "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae", "lgx_gae_norm_scratch", "lgx_gae_norm", "lgx_gae_parts", "lgx_adv_norm",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",

@@ -139,3 +139,35 @@ def test_philox_stream_is_uniform_and_deterministic():
     assert 0 <= u.min() and u.max() < 1 and abs(u.mean() - 0.5) < 0.02
     assert lib.lgxo_uniform(1, 3, 7, 5, 0) == lib.lgxo_uniform(1, 3, 7, 5, 0)
     assert lib.lgxo_uniform(1, 3, 7, 5, 0) != lib.lgxo_uniform(1, 3, 7, 6, 0)
+
+
+@pytest.mark.parametrize("robot", ["go1", "cassie"])
+@pytest.mark.parametrize("field,value,msg", [("point_dyn", 13, "point_dyn"), ("point_dyn", -1, "point_dyn"),
+                                             ("point_report", 17, "point_report")])
+def test_sim_create_rejects_bad_contact_tables(robot, field, value, msg):
+    """lgx_sim_create validates every contact candidate's dyn / report body index for BOTH physics
+    kernels (the dense kernel's path skipped the check and would read LDS out of bounds).
+    The validation precedes any device call, so it runs here without a GPU."""
+    import types
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim.model import RobotAsset, build_model
+    from legged_gym_amd.utils.task_registry import task_registry
+    import legged_gym_amd.envs  # noqa: F401
+    task = {"go1": "go1_flat_bench", "cassie": "cassie"}[robot]
+    env_cfg, _ = task_registry.get_cfgs(task)
+    asset = RobotAsset(os.path.join(ROOT, "legged_gym_amd", "resources", f"{robot}_model.json"))
+    model = build_model(asset, env_cfg, types.SimpleNamespace(gravity=[0.0, 0.0, -9.81], dt=0.005))
+    getattr(model, field)[model.num_points - 1] = value
+    p = abi.LgxEnvParams()
+    p.num_envs, p.num_obs, p.decimation, p.resample_interval = 16, 48, 4, 100
+    b = abi.LgxBuffers()
+    for name, typ in b._fields_:
+        if typ is C.c_void_p or (isinstance(typ, type) and issubclass(typ, C._Pointer)):
+            setattr(b, name, C.cast(C.c_void_p(0x1000), typ) if typ is not C.c_void_p else 0x1000)
+    import torch  # noqa: F401  (HIP runtime first)
+    lib = C.CDLL(os.path.join(ROOT, "legged_gym_amd", "liblgx.so"))
+    abi.declare(lib)
+    h = C.c_void_p()
+    rc = lib.lgx_sim_create(C.byref(model), C.byref(p), C.byref(b), 0, C.byref(h))
+    assert rc == -1 and not h.value
+    assert msg in lib.lgx_last_error().decode()

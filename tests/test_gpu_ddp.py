@@ -42,7 +42,7 @@ def _make(n_envs, sl):
                       ("values", "val"), ("actions_log_prob", "logp"), ("mu", "mu"), ("sigma", "sigma")):
         getattr(st, name).copy_(d[key][:, sl])
     st.step = T
-    st.compute_returns(d["last"][sl].cuda(), 0.99, 0.95, reduce_stats=ppo._adv_stats)
+    st.compute_returns(d["last"][sl].cuda(), 0.99, 0.95, reduce_stats=ppo._gather_moments)
     return ppo
 
 
@@ -61,6 +61,7 @@ def _worker(rank, world, port, q, early):
         # early reduction on: two gradient buckets, the first all-reduced from the side stream
         # while dW1 runs; off: one collective after the whole backward
         assert ppo._fused.bucketed == (early == "1")
+        assert ppo._fused.join_events == "system"   # peers write the collectives' buffers
         if rank == 0:
             # numpy (pickled by value): CPU tensors would go through shared-memory file descriptors
             # that die with this process
@@ -145,6 +146,31 @@ def test_bench_two_ranks_self_check(gpu, tmp_path):
     assert dp["params_identical_across_ranks"] and dp["param_fingerprint_spread"] == 0
     assert dp["bucketed_allreduce"] is True
     assert dp["allreduce"]["collectives_timed"] >= 2 and dp["allreduce"]["ms_per_iteration"] > 0
+    assert dp["join_events"] == "system"   # data-parallel joins keep system-scope events
+
+
+@pytest.mark.timeout(280)
+def test_bench_plain_gpus2_launches_ranks(gpu, tmp_path):
+    """`python bench.py --gpus 2` with no launcher: bench.py starts the two ranks
+    itself (torch.distributed.run as a child process; gloo so both can share the one test GPU), and
+    rank 0's line reports n_gpus 2, both ranks seen and bitwise identical parameters."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(LGX_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0", LGX_BENCH_GEMM_TIMING="1")
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--task", "go1_flat_bench", "--num_envs", "256", "--no_cpu_baseline"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]     # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    dp = d["data_parallel"]
+    assert dp["world"] == 2 and dp["ranks_seen"] == 2 and dp["param_fingerprint_spread"] == 0
+    assert dp["bucketed_allreduce"] is True
 
 
 @pytest.mark.timeout(280)
@@ -172,5 +198,6 @@ def test_bench_rccl_rehearsal_one_rank(gpu, tmp_path):
     dp = d["data_parallel"]
     assert dp["world"] == 1 and dp["backend"] == "nccl" and dp["ranks_seen"] == 1
     assert dp["params_identical_across_ranks"] and dp["param_fingerprint_spread"] == 0
+    assert dp["join_events"] == "system"
     assert dp["bucketed_allreduce"] is True
     assert dp["allreduce"]["collectives_timed"] >= 2 and dp["allreduce"]["ms_per_iteration"] > 0

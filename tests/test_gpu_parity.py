@@ -486,6 +486,40 @@ def test_gae_norm_large_mean_advantages(gpu):
     assert abs(got.std().item() - 1.0) < 1e-3
 
 
+@pytest.mark.parametrize("mean", [0.0, 3e3])
+def test_dp_advantage_statistics_match_gae_norm(gpu, mean):
+    """The data-parallel normalisation (lgx_gae_parts -> gathered summaries -> lgx_adv_norm) at
+    world 1 is bitwise lgx_gae_norm's, and over two shards it equals the one-process statistics of
+    the whole batch (the DP path keeps Chan's float64 moments, also when |mean| >> std)."""
+    from legged_gym_amd.rl.storage import RolloutStorage
+    T, N = 24, 4096
+    gen = torch.Generator().manual_seed(3)
+    rew = mean + torch.randn(T, N, 1, generator=gen) * (1e-2 if mean else 1.0)
+    val = torch.randn(T, N, 1, generator=gen) * (1e-3 if mean else 1.0)
+    dones = (torch.rand(T, N, 1, generator=gen) < 0.05).byte()
+    last = torch.randn(N, 1, generator=gen)
+
+    def mk(sl):
+        st = RolloutStorage(sl.stop - sl.start, T, [4], [None], [2], str(gpu))
+        st.rewards.copy_(rew[:, sl]), st.values.copy_(val[:, sl]), st.dones.copy_(dones[:, sl])
+        return st
+    full = slice(0, N)
+    one, dp1 = mk(full), mk(full)
+    one.compute_returns(last.to(gpu), 0.99, 0.95)
+    dp1.compute_returns(last.to(gpu), 0.99, 0.95, reduce_stats=lambda p: p)
+    assert torch.equal(one.advantages, dp1.advantages) and torch.equal(one.returns, dp1.returns)
+    # two "ranks" of N/2 envs: gather both ranks' GAE summaries in rank order, normalise each shard
+    from legged_gym_amd.rl import fused
+    shards = [mk(slice(0, N // 2)), mk(slice(N // 2, N))]
+    parts = [fused.gae_parts(s.rewards, s.values, s.dones, last[sl].to(gpu).contiguous(), s.returns, s.advantages,
+                             0.99, 0.95) for s, sl in zip(shards, (slice(0, N // 2), slice(N // 2, N)))]
+    allp = torch.cat(parts)
+    for s in shards:
+        fused.adv_norm(s.advantages, allp)
+    got = torch.cat([s.advantages for s in shards], dim=1)
+    assert (got - one.advantages).abs().max().item() <= 1e-5 * max(1.0, one.advantages.abs().max().item())
+
+
 def test_splitk_linear_gradients_match_torch(gpu):
     from legged_gym_amd.rl.actor_critic import LgxLinear
     torch.manual_seed(0)

@@ -193,12 +193,35 @@ def _ddp_worker(rank, world, port, out_q):
     alg = make_alg(B)
     fill(alg.storage, None, B, offset=rank * B)
     last = torch.randn(2 * B, 1, generator=torch.Generator().manual_seed(9))[rank * B:(rank + 1) * B]
-    alg.storage.compute_returns(last, 0.99, 0.95, reduce_stats=alg._adv_stats)
+    alg.storage.compute_returns(last, 0.99, 0.95, reduce_stats=alg._gather_moments)
     alg.update()
     if rank == 0:
         out_q.put([p.detach().numpy().copy() for p in alg.actor_critic.parameters()] + [alg.learning_rate])
     dist.barrier()
     dist.destroy_process_group()
+
+
+def test_dp_advantage_statistics_are_chan_moments():
+    """The data-parallel advantage statistics: per-rank float64 (count, mean, M2)
+    summaries combined in rank order == the float64 mean / unbiased std of all samples, also when
+    |mean| >> std (where sum / sum-of-squares in f32 collapses the variance)."""
+    from legged_gym_amd.rl.storage import combined_mean_std, local_moments
+    g = torch.Generator().manual_seed(5)
+    for offset, scale in ((0.0, 1.0), (1.0e4, 1.0e-3), (-3.0e3, 0.5)):
+        x = (offset + scale * torch.randn(4, 3000, 1, generator=g)).float()
+        ranks = [x[:, :1000], x[:, 1000:1700], x[:, 1700:]]          # ragged shards
+        mean, std = combined_mean_std(torch.cat([local_moments(r) for r in ranks]))
+        xd = x.double().numpy().reshape(-1)
+        assert mean == pytest.approx(xd.mean(), rel=1e-12, abs=1e-12)
+        assert std == pytest.approx(xd.std(ddof=1), rel=1e-9)
+    # the f32 sum / sum-of-squares form it replaces loses the large-mean case entirely
+    xf = (1.0e4 + 1.0e-3 * torch.randn(12000, generator=g)).float()
+    n = xf.numel()
+    var_naive = float(((xf * xf).sum() - n * xf.mean() ** 2) / (n - 1))
+    std_true = float(xf.double().std())
+    assert abs(max(var_naive, 0.0) ** 0.5 - std_true) > 0.5 * std_true
+    _, std = combined_mean_std(local_moments(xf))
+    assert std == pytest.approx(std_true, rel=1e-9)
 
 
 def test_data_parallel_equals_single_process_gloo():
@@ -244,6 +267,37 @@ def test_runner_learns_on_oracle_env_and_checkpoints(tmp_path):
     with torch.inference_mode():
         a = pol(env.get_observations())
     assert a.shape == (8, 12) and torch.isfinite(a).all()
+
+
+def test_runner_reports_the_original_error(tmp_path):
+    """when learn() unwinds from an error, a failing cleanup (flush of the deferred
+    storage row) must not replace the original exception, and no deferred row survives."""
+    from oracle_backend import make_env
+    from legged_gym_amd.rl.runner import OnPolicyRunner
+    from legged_gym_amd.utils.helpers import class_to_dict
+    from legged_gym_amd.envs.go1.go1_config import Go1RoughCfgPPO
+    env = make_env("go1_flat_bench", num_envs=4, device="cpu", backend="oracle")
+    cfg = class_to_dict(Go1RoughCfgPPO())
+    cfg["runner"]["num_steps_per_env"] = 2
+    runner = OnPolicyRunner(env, cfg, None, device="cpu")
+    calls = {"n": 0}
+    orig = env.step
+
+    def failing_step(actions):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            runner.alg._pending_store = ("stale",)        # a deferred row whose flush will fail
+            raise ValueError("env step failed")
+        return orig(actions)
+
+    def bad_flush():
+        if runner.alg._pending_store is not None:
+            raise RuntimeError("cleanup failed")
+    env.step = failing_step
+    runner.alg.flush_store = bad_flush
+    with pytest.raises(ValueError, match="env step failed"):
+        runner.learn(1)
+    assert runner.alg._pending_store is None and runner.alg.defer_store is False
 
 
 def test_policy_export_is_plain_torchscript(tmp_path):
