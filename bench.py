@@ -27,25 +27,43 @@ sys.path.insert(0, ROOT)
 ACT_MLP_FLOP_PER_ENV_STEP = 4 * 4 * 2 * (30 * 128 + 128 * 128 * 2 + 128 * 3)
 MI355X_F32_PEAK_TFLOPS = 157.3      # vector FP32 == f32 MFMA peak (MI355X_MICROARCH.md)
 MI355X_HBM_PEAK_GBS = 8000.0
-# HBM bytes per launch, go1_rough 4096 envs: 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts
-# half of wide reads), from the rocprofv3 --pmc passes of the same build (tools/pmc_round.sh ->
-# profiles/r04_pmc_env_kernels.json); the actuator net from the passes that launch it on its own.
-# LGX_BENCH_PMC_ENV / LGX_BENCH_PMC_PPO point at a fresh pair (tools/gpu_r04e.sh: same GPU session)
-PMC_FILE = os.environ.get("LGX_BENCH_PMC_ENV") or os.path.join(ROOT, "profiles", "r04_pmc_env_kernels.json")
+# PMC figures (rocprofv3 --pmc passes of the same build, tools/gpu_profile.sh): HBM bytes per launch
+# = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of wide reads) and MFMA utilisation.
+# Default: the newest committed profiles/r*_pmc_{env,ppo}_kernels.json; LGX_BENCH_PMC_ENV /
+# LGX_BENCH_PMC_PPO point at a fresh pair from the same GPU session.  A file is used only for the
+# workload it was collected on (its "workload" entry; files without one are go1_rough, 4096 envs).
+import glob  # noqa: E402
 
 
-def pmc_traffic_bytes(kernel, fetch_pass="fetch", write_pass="write"):
-    try:
-        p = json.load(open(PMC_FILE))["passes"]
-        return int((2 * p[fetch_pass][kernel]["FETCH_SIZE"] + p[write_pass][kernel]["WRITE_SIZE"]) * 1024)
-    except (OSError, KeyError, ValueError):
-        return None
+def _newest(kind):
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{kind}_kernels.json")))
+    return files[-1] if files else ""
 
 
-PHYS_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_physics_kernel<4>")
-PPO_PMC_FILE = os.environ.get("LGX_BENCH_PMC_PPO") or os.path.join(ROOT, "profiles", "r04_pmc_ppo_kernels.json")
+PMC_FILE = os.environ.get("LGX_BENCH_PMC_ENV") or _newest("env")
+PPO_PMC_FILE = os.environ.get("LGX_BENCH_PMC_PPO") or _newest("ppo")
 MI355X_BF16_PEAK_TFLOPS = 2500.0    # dense bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PRODUCTS = 6                  # split-bf16: six bf16 limb products per f32 product (lgx_gemm_split.hip)
+MI355X_SIMDS = 256 * 4              # MfmaUtil's SIMD_NUM (counter_defs.yaml): 256 CUs x 4 SIMDs
+MI355X_XCDS = 8                     # GRBM_GUI_ACTIVE arrives summed over the 8 XCDs
+
+
+def _pmc_passes(path, task, n_envs):
+    """The passes of a PMC summary file if it was collected on (task, n_envs), else None."""
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    wl = d.get("workload", {"task": "go1_rough", "num_envs": 4096})
+    return d.get("passes") if (wl.get("task"), int(wl.get("num_envs", 0))) == (task, n_envs) else None
+
+
+def pmc_traffic_bytes(kernel, task, n_envs, fetch_pass="fetch", write_pass="write"):
+    p = _pmc_passes(PMC_FILE, task, n_envs)
+    try:
+        return int((2 * p[fetch_pass][kernel]["FETCH_SIZE"] + p[write_pass][kernel]["WRITE_SIZE"]) * 1024)
+    except (TypeError, KeyError):
+        return None
 
 
 def gemm_kernel_info(key, split):
@@ -66,23 +84,57 @@ GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor 
                     "(512x235, 256x512, 128x256 per network)"}
 
 
-def pmc_ppo_traffic_bytes(kernel):
-    """HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KB) of a PPO-update kernel from the PMC
-    passes over one bench iteration (tools/pmc_ppo.sh); `kernel` may hold '*' wildcards (e.g. the
-    K-specialised instantiations of one epilogue): dispatch-weighted mean over the matches."""
+# the MFMA kernels of one iteration whose utilisation the bench line reports (PMC pass "mfma")
+MFMA_KERNELS = ["gemm_tn_x3_kernel<*>", "gemm_nt_x3p_kernel<1, *>", "gemm_nt_x3p_kernel<2, *>", "lgx_mlp_x3_kernel*",
+                "lgx_post_physics_act_kernel*"]
+
+
+def _ppo_matches(p, kernel, passname):
     import fnmatch
-    try:
-        p = json.load(open(PPO_PMC_FILE))["passes"]
-        tot = n = 0.0
-        for name in p["fetch"]:
-            if fnmatch.fnmatchcase(name, kernel) and name in p["write"]:
-                d = p["fetch"][name].get("dispatches", 1)
-                tot += d * (2 * p["fetch"][name]["FETCH_SIZE"] + p["write"][name]["WRITE_SIZE"]) * 1024
-                n += d
-        return int(tot / n) if n else None
-    except (OSError, KeyError, ValueError):
+    return [(name, v) for name, v in p.get(passname, {}).items() if fnmatch.fnmatchcase(name, kernel)]
+
+
+def pmc_ppo_traffic_bytes(kernel, task, n_envs):
+    """HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, KB) of a PPO-update kernel from the PMC
+    passes over one bench iteration of (task, n_envs); `kernel` may hold '*' wildcards (e.g. the
+    K-specialised instantiations of one epilogue): dispatch-weighted mean over the matches."""
+    p = _pmc_passes(PPO_PMC_FILE, task, n_envs)
+    if not p:
         return None
-ACT_PMC_TRAFFIC_BYTES = pmc_traffic_bytes("lgx_actuator_ws_kernel", "fetch_sep", "write_sep")
+    tot = n = 0.0
+    for name, f in _ppo_matches(p, kernel, "fetch"):
+        w = p.get("write", {}).get(name)
+        if w is None or "FETCH_SIZE" not in f or "WRITE_SIZE" not in w:
+            continue
+        d = f.get("dispatches", 1)
+        tot += d * (2 * f["FETCH_SIZE"] + w["WRITE_SIZE"]) * 1024
+        n += d
+    return int(tot / n) if n else None
+
+
+def pmc_mfma_busy(kernel, task, n_envs):
+    """MFMA utilisation of the kernels matching `kernel` in the PMC pass "mfma" of (task, n_envs):
+    SQ_VALU_MFMA_BUSY_CYCLES (summed over SIMDs) / (SIMDs x kernel cycles), kernel cycles =
+    GRBM_GUI_ACTIVE / XCDs (rocprofv3's MfmaUtil), summed over the dispatches of every match; None
+    when the file has no such pass.  rocprofv3 serialises dispatches under --pmc, so second-stream
+    kernels are measured alone there."""
+    p = _pmc_passes(PPO_PMC_FILE, task, n_envs)
+    if not p:
+        return None
+    busy = cyc = insts = disp = 0.0
+    for _, c in _ppo_matches(p, kernel, "mfma"):
+        if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or not c.get("GRBM_GUI_ACTIVE"):
+            continue
+        d = c.get("dispatches", 1)
+        busy += d * c["SQ_VALU_MFMA_BUSY_CYCLES"]
+        cyc += d * c["GRBM_GUI_ACTIVE"] / MI355X_XCDS
+        insts += d * c.get("SQ_INSTS_MFMA", 0.0)
+        disp += d
+    if not cyc:
+        return None
+    return {"mfma_busy": busy / (MI355X_SIMDS * cyc), "mfma_insts_per_launch": insts / disp,
+            "kernel_cycles_per_launch": cyc / disp, "dispatches": int(disp),
+            "source": os.path.relpath(PPO_PMC_FILE, ROOT) + " pass mfma"}
 
 
 from legged_gym_amd.sim.flops import physics_flop_per_env_substep, policy_flop_per_sample  # noqa: E402
@@ -479,15 +531,16 @@ def main():
     roof = {"kernel": names[0], "bound": "valu", "compute_pipe": "fp32 VALU",
             "achieved": (phys_flop / (avg[0] * 1e-3) / 1e12) if avg[0] else None,
             "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "traffic": PHYS_PMC_TRAFFIC_BYTES if (N == 4096 and args.task == "go1_rough") else None,
+            "traffic": pmc_traffic_bytes(f"lgx_physics_kernel<{lib.lgx_physics_lane_split(N)}>", args.task, N),
             "algorithmic_per_launch": phys_flop,
             "note": ("compute roof = FP32 peak (vector FP32 = f32 MFMA = 157.3 TF on gfx950); algorithmic FLOP "
                      "from legged_gym_amd/sim/flops.py x envs x substeps; traffic = FETCH_SIZE*2 + WRITE_SIZE "
-                     "per launch from " + os.path.relpath(PMC_FILE, ROOT) + " (tools/gpu_r04e.sh); latency-bound, see DESIGN.md 4.1")}
+                     "per launch from " + os.path.relpath(PMC_FILE, ROOT) + " (tools/gpu_profile.sh; null when that file was "
+                     "collected on another workload); latency-bound, see DESIGN.md 4.1")}
     act_flop = ACT_MLP_FLOP_PER_ENV_STEP * N
     roof2 = {"kernel": "lgx_actuator_ws_kernel", "bound": "mfma", "peak": MI355X_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
              "achieved": (act_flop / (avg[1] * 1e-3) / 1e12) if avg[1] else None,
-             "traffic": ACT_PMC_TRAFFIC_BYTES if (N == 4096 and args.task == "go1_rough") else None,
+             "traffic": pmc_traffic_bytes("lgx_actuator_ws_kernel", args.task, N, "fetch_sep", "write_sep"),
              "algorithmic_per_launch": act_flop}
     if act_note:
         roof2["note"] = act_note
@@ -511,7 +564,8 @@ def main():
             "kernel": kname, "bound": "mfma", "compute_pipe": pipe,
             "achieved": flop / (t_ms * 1e-3) / 1e12, "peak": peak, "unit": "TFLOP/s",
             "frac": flop / (t_ms * 1e-3) / 1e12 / peak,
-            "traffic": pmc_ppo_traffic_bytes(kname), "algorithmic_per_launch": flop / n, "avg_ms": t_ms / n,
+            "traffic": pmc_ppo_traffic_bytes(kname, args.task, N), "algorithmic_per_launch": flop / n,
+            "avg_ms": t_ms / n, "mfma": pmc_mfma_busy(kname, args.task, N),
             "launches_timed": n, "share_of_iteration": (t_ms / mbs) * mb_per_iter / it_ms,
             "note": GEMM_NOTES.get(epi, "") + "; algorithmic FLOP = 2 M N K x {actor, critic} with the unpadded K / Cc "
                     "(f32 products; the split-bf16 peak is the bf16 dense MFMA peak / 6 limb products); HIP events "
@@ -542,6 +596,8 @@ def main():
     cands = [roof] + gemm_roofs
     cands.sort(key=lambda r: -r.get("share_of_iteration", 0.0))
     roof, others = cands[0], cands[1:]
+    if roof.get("mfma"):
+        roof["mfma_busy"] = roof["mfma"]["mfma_busy"]
     roof["selection"] = ("largest GPU-time share of the iteration among the physics kernel and the PPO-update GEMM "
                          "families (second-stream launches included)")
     out = {
@@ -561,6 +617,7 @@ def main():
         "iteration_roofline": iteration_roofline(runner, env, N, it_ms),
         "dominant_lgx_kernel": roof["kernel"],
         "lgx_kernels": kernels,
+        "mfma_utilisation": {k: pmc_mfma_busy(k, args.task, N) for k in MFMA_KERNELS},
         "last_iteration": runner.last_iteration_stats,
         "data_parallel": data_parallel,
     }

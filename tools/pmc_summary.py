@@ -16,6 +16,9 @@ out = {"what": what or "rocprofv3 --kernel-trace --pmc, per-dispatch means over 
                "coalesced bytes); SQ_* = wave-instruction totals per dispatch; passes *_sep ran with "
                "LGX_ACT_OVERLAP=0 (actuator net as its own launch)",
        "passes": {}}
+# the workload the passes ran (bench.py uses a file's traffic / MFMA figures only for that workload)
+out["workload"] = {"task": os.environ.get("LGX_PMC_TASK", "go1_rough"),
+                   "num_envs": int(os.environ.get("LGX_PMC_ENVS", "4096"))}
 for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv"))):
     name = os.path.basename(os.path.dirname(f))
     acc = defaultdict(lambda: defaultdict(list))
