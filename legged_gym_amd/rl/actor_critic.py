@@ -297,3 +297,109 @@ class ActorCritic(nn.Module):
         if self._fused_ok(critic_observations, self._fused_critic):
             return self._fused_critic(critic_observations)
         return self.critic(critic_observations)
+
+
+# ---------------------------------------------------------------------------------------------
+# Recurrent policy (rsl_rl v1.0.x `ActorCriticRecurrent` / `Memory`; legged_robot_config.py:221-224
+# names its options rnn_type / rnn_hidden_size / rnn_num_layers).  The LSTM / GRU runs on torch
+# (MIOpen); the MLP heads behind it keep the fused rollout kernels of ActorCritic.
+
+def split_and_pad_trajectories(tensor, dones):
+    """[T, N, ...] -> ([T, n_traj, ...] zero-padded trajectories, [T, n_traj] masks): the rollout cut
+    at every done (and at the end), env-major (rsl_rl utils.split_and_pad_trajectories)."""
+    dones = dones.clone()
+    dones[-1] = 1
+    flat_dones = dones.transpose(1, 0).reshape(-1, 1)
+    done_indices = torch.cat((flat_dones.new_tensor([-1], dtype=torch.int64), flat_dones.nonzero()[:, 0]))
+    lengths = done_indices[1:] - done_indices[:-1]
+    trajectories = torch.split(tensor.transpose(1, 0).flatten(0, 1), lengths.tolist())
+    # one full-length dummy so the padding always reaches T, removed afterwards
+    trajectories = trajectories + (torch.zeros(tensor.shape[0], *tensor.shape[2:], device=tensor.device,
+                                               dtype=tensor.dtype),)
+    padded = torch.nn.utils.rnn.pad_sequence(trajectories)[:, :-1]
+    masks = lengths > torch.arange(0, tensor.shape[0], device=tensor.device).unsqueeze(1)
+    return padded, masks
+
+
+def unpad_trajectories(trajectories, masks):
+    """Inverse of split_and_pad_trajectories: [T, n_traj, H] -> [T, N, H]."""
+    return trajectories.transpose(1, 0)[masks.transpose(1, 0)].view(
+        -1, trajectories.shape[0], trajectories.shape[-1]).transpose(1, 0)
+
+
+class Memory(nn.Module):
+    """rsl_rl Memory: one LSTM (or GRU) over the observation stream.  Rollout (masks None): one time
+    step from the stored hidden state; update (masks given): whole padded trajectories from the
+    hidden states saved at their first step, unpadded back to [T, envs, H]."""
+
+    def __init__(self, input_size, type="lstm", num_layers=1, hidden_size=256):
+        super().__init__()
+        rnn_cls = nn.GRU if type.lower() == "gru" else nn.LSTM
+        self.rnn = rnn_cls(input_size=input_size, hidden_size=hidden_size, num_layers=num_layers)
+        self.hidden_states = None
+
+    def forward(self, input, masks=None, hidden_states=None):
+        if masks is not None:
+            if hidden_states is None:
+                raise ValueError("Hidden states not passed to memory module during policy update")
+            out, _ = self.rnn(input, hidden_states)
+            return unpad_trajectories(out, masks)
+        out, self.hidden_states = self.rnn(input.unsqueeze(0), self.hidden_states)
+        return out
+
+    def reset(self, dones=None):
+        if self.hidden_states is None:
+            return
+        # LSTM: (h, c); GRU: one tensor whose layers are iterated - both [.., envs, hidden]
+        for hidden_state in self.hidden_states:
+            hidden_state[..., dones, :] = 0.0
+
+
+class ActorCriticRecurrent(ActorCritic):
+    is_recurrent = True
+
+    def __init__(self, num_actor_obs, num_critic_obs, num_actions, actor_hidden_dims=(256, 256, 256),
+                 critic_hidden_dims=(256, 256, 256), activation="elu", rnn_type="lstm", rnn_hidden_size=256,
+                 rnn_num_layers=1, init_noise_std=1.0, **kwargs):
+        if kwargs:
+            print("ActorCriticRecurrent.__init__ got unexpected arguments, which will be ignored: "
+                  + str(kwargs.keys()))
+        super().__init__(num_actor_obs=rnn_hidden_size, num_critic_obs=rnn_hidden_size, num_actions=num_actions,
+                         actor_hidden_dims=actor_hidden_dims, critic_hidden_dims=critic_hidden_dims,
+                         activation=activation, init_noise_std=init_noise_std)
+        self.memory_a = Memory(num_actor_obs, type=rnn_type, num_layers=rnn_num_layers, hidden_size=rnn_hidden_size)
+        self.memory_c = Memory(num_critic_obs, type=rnn_type, num_layers=rnn_num_layers, hidden_size=rnn_hidden_size)
+        print(f"Actor RNN: {self.memory_a}")
+        print(f"Critic RNN: {self.memory_c}")
+
+    def reset(self, dones=None):
+        self.memory_a.reset(dones)
+        self.memory_c.reset(dones)
+
+    def act(self, observations, masks=None, hidden_states=None):
+        input_a = self.memory_a(observations, masks, hidden_states)
+        return super().act(input_a.squeeze(0))
+
+    def act_inference(self, observations):
+        input_a = self.memory_a(observations)
+        return super().act_inference(input_a.squeeze(0))
+
+    def evaluate(self, critic_observations, masks=None, hidden_states=None):
+        input_c = self.memory_c(critic_observations, masks, hidden_states)
+        return super().evaluate(input_c.squeeze(0))
+
+    def act_and_evaluate(self, observations, critic_observations):
+        """act + evaluate (both memories advance one step); the two MLP heads in one fused launch."""
+        input_a = self.memory_a(observations).squeeze(0)
+        input_c = self.memory_c(critic_observations).squeeze(0)
+        if self._fused_ok(input_a, self._fused_actor) and self._fused_critic.ok:
+            mean, value = run_fused([(self._fused_actor, input_a), (self._fused_critic, input_c)])
+            self.distribution = Normal(mean, mean * 0.0 + self.std)
+            return self.distribution.sample(), value
+        return ActorCritic.act(self, input_a), ActorCritic.evaluate(self, input_c)
+
+    # the fused rollout path of PPO._act_fused feeds observations straight into the actor MLP
+    rollout_forward = None
+
+    def get_hidden_states(self):
+        return self.memory_a.hidden_states, self.memory_c.hidden_states

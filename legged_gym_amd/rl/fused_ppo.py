@@ -156,6 +156,8 @@ class FusedPPOUpdate:
     def supported(ac):
         def lin(seq):
             return [m for m in seq if isinstance(m, nn.Linear)], [m for m in seq if not isinstance(m, nn.Linear)]
+        if getattr(ac, "is_recurrent", False):    # (the memories' update runs on the autograd path)
+            return False
         try:
             la, aa = lin(ac.actor)
             lc, acr = lin(ac.critic)

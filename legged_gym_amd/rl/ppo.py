@@ -88,7 +88,8 @@ class PPO:
     # ---------------------------------------------------------------- rollout
     def _rollout_kernels_ok(self, obs):
         ac = self.actor_critic
-        return (self._fused is not None and obs.is_cuda and self.storage is not None and hasattr(ac, "rollout_forward")
+        return (self._fused is not None and obs.is_cuda and self.storage is not None
+                and getattr(ac, "rollout_forward", None) is not None and not ac.is_recurrent
                 and self.storage.step < self.storage.num_transitions_per_env)
 
     def _act_fused(self, obs, critic_obs):
@@ -158,6 +159,8 @@ class PPO:
             if actions is not None:
                 return actions
         self.flush_store()   # (a deferred store reads the env's buffers before the next env.step)
+        if self.actor_critic.is_recurrent:   # the memories' state before this step (rsl_rl PPO.act)
+            t.hidden_states = self.actor_critic.get_hidden_states()
         if hasattr(self.actor_critic, "act_and_evaluate"):
             actions, values = self.actor_critic.act_and_evaluate(obs, critic_obs)
             t.actions, t.values = actions.detach(), values.detach()
@@ -256,11 +259,14 @@ class PPO:
             return out
         mean_value_loss = 0.0
         mean_surrogate_loss = 0.0
-        gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
-        for (obs_b, cobs_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b, old_sigma_b, _hid, _mask) in gen:
-            self.actor_critic.act(obs_b)
+        if self.actor_critic.is_recurrent:
+            gen = self.storage.reccurent_mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        else:
+            gen = self.storage.mini_batch_generator(self.num_mini_batches, self.num_learning_epochs)
+        for (obs_b, cobs_b, act_b, target_v_b, adv_b, ret_b, old_logp_b, old_mu_b, old_sigma_b, hid_b, masks_b) in gen:
+            self.actor_critic.act(obs_b, masks=masks_b, hidden_states=hid_b[0])
             logp_b = self.actor_critic.get_actions_log_prob(act_b)
-            value_b = self.actor_critic.evaluate(cobs_b)
+            value_b = self.actor_critic.evaluate(cobs_b, masks=masks_b, hidden_states=hid_b[1])
             mu_b = self.actor_critic.action_mean
             sigma_b = self.actor_critic.action_std
             entropy_b = self.actor_critic.entropy

@@ -15,7 +15,7 @@ from collections import deque
 
 import torch
 
-from .actor_critic import ActorCritic  # noqa: F401  (resolved by name from the cfg)
+from .actor_critic import ActorCritic, ActorCriticRecurrent  # noqa: F401  (resolved by name from the cfg)
 from .ppo import PPO  # noqa: F401
 
 
@@ -27,7 +27,8 @@ class OnPolicyRunner:
         self.device = device
         self.env = env
         num_critic_obs = self.env.num_privileged_obs if self.env.num_privileged_obs is not None else self.env.num_obs
-        ac_class = {"ActorCritic": ActorCritic}[self.cfg["policy_class_name"]]
+        ac_class = {"ActorCritic": ActorCritic,
+                    "ActorCriticRecurrent": ActorCriticRecurrent}[self.cfg["policy_class_name"]]
         actor_critic = ac_class(self.env.num_obs, num_critic_obs, self.env.num_actions, **self.policy_cfg).to(self.device)
         alg_class = {"PPO": PPO}[self.cfg["algorithm_class_name"]]
         self.alg = alg_class(actor_critic, device=self.device, **self.alg_cfg)

@@ -79,6 +79,8 @@ class RolloutStorage:
         self.num_transitions_per_env = T
         self.num_envs = N
         self.step = 0
+        self.saved_hidden_states_a = None   # recurrent policies: memory state before each step
+        self.saved_hidden_states_c = None
 
     def add_transitions(self, t: "RolloutStorage.Transition"):
         if self.step >= self.num_transitions_per_env:
@@ -94,7 +96,23 @@ class RolloutStorage:
         self.actions_log_prob[s].copy_(t.actions_log_prob.view(-1, 1))
         self.mu[s].copy_(t.action_mean)
         self.sigma[s].copy_(t.action_sigma)
+        self._save_hidden_states(t.hidden_states)
         self.step += 1
+
+    def _save_hidden_states(self, hidden_states):
+        """rsl_rl RolloutStorage._save_hidden_states: [T, layers, envs, hidden] per state tensor
+        (LSTM: h and c; GRU: one), zero until the memory has run once."""
+        if hidden_states is None or hidden_states == (None, None):
+            return
+        hid_a = hidden_states[0] if isinstance(hidden_states[0], tuple) else (hidden_states[0],)
+        hid_c = hidden_states[1] if isinstance(hidden_states[1], tuple) else (hidden_states[1],)
+        if self.saved_hidden_states_a is None:
+            T = self.observations.shape[0]
+            self.saved_hidden_states_a = [torch.zeros(T, *h.shape, device=self.device) for h in hid_a]
+            self.saved_hidden_states_c = [torch.zeros(T, *h.shape, device=self.device) for h in hid_c]
+        for i in range(len(hid_a)):
+            self.saved_hidden_states_a[i][self.step].copy_(hid_a[i])
+            self.saved_hidden_states_c[i][self.step].copy_(hid_c[i])
 
     def clear(self):
         self.step = 0
@@ -159,3 +177,40 @@ class RolloutStorage:
                 b = indices[i * mb:(i + 1) * mb]
                 yield obs[b], cobs[b], actions[b], values[b], adv[b], returns[b], old_logp[b], mu[b], sigma[b], \
                     (None, None), None
+
+    def reccurent_mini_batch_generator(self, num_mini_batches, num_epochs=8):
+        """rsl_rl RolloutStorage.reccurent_mini_batch_generator (upstream's spelling): minibatches of
+        whole envs; observations as zero-padded trajectories with their masks, the memories' hidden
+        states at each trajectory's first step.  As upstream v1.0.x, an LSTM's critic batch receives
+        the ACTOR's saved states (`hid_c_batch = ... else hid_a_batch`), kept for parity."""
+        from .actor_critic import split_and_pad_trajectories
+        padded_obs, traj_masks = split_and_pad_trajectories(self.observations, self.dones)
+        if self.privileged_observations is not None:
+            padded_cobs, _ = split_and_pad_trajectories(self.privileged_observations, self.dones)
+        else:
+            padded_cobs = padded_obs
+        mb = self.num_envs // num_mini_batches
+        for _ in range(num_epochs):
+            first_traj = 0
+            for i in range(num_mini_batches):
+                start, stop = i * mb, (i + 1) * mb
+                dones = self.dones.squeeze(-1)
+                last_was_done = torch.zeros_like(dones, dtype=torch.bool)
+                last_was_done[1:] = dones[:-1]
+                last_was_done[0] = True
+                last_traj = first_traj + int(torch.sum(last_was_done[:, start:stop]))
+                masks_b = traj_masks[:, first_traj:last_traj]
+                obs_b = padded_obs[:, first_traj:last_traj]
+                cobs_b = padded_cobs[:, first_traj:last_traj]
+                lwd = last_was_done.permute(1, 0)
+                hid_a = [h.permute(2, 0, 1, 3)[lwd][first_traj:last_traj].transpose(1, 0).contiguous()
+                         for h in self.saved_hidden_states_a]
+                hid_c = [h.permute(2, 0, 1, 3)[lwd][first_traj:last_traj].transpose(1, 0).contiguous()
+                         for h in self.saved_hidden_states_c]
+                hid_a = hid_a[0] if len(hid_a) == 1 else hid_a
+                hid_c = hid_c[0] if len(hid_c) == 1 else hid_a
+                yield (obs_b, cobs_b, self.actions[:, start:stop], self.values[:, start:stop],
+                       self.advantages[:, start:stop], self.returns[:, start:stop],
+                       self.actions_log_prob[:, start:stop], self.mu[:, start:stop], self.sigma[:, start:stop],
+                       (hid_a, hid_c), masks_b)
+                first_traj = last_traj

@@ -170,14 +170,13 @@ def get_args(argv=None):
     return args
 
 
-def export_policy_as_jit(actor_critic, path):
-    """helpers.py:180-190: TorchScript export of the actor MLP (as plain nn.Linear layers, so the
-    exported module has no dependency on this package)."""
+def _plain_actor(actor):
+    """The actor MLP rebuilt from plain nn.Linear layers on the CPU (no dependency on this package
+    in the exported module)."""
     import torch
     import torch.nn as nn
-    os.makedirs(path, exist_ok=True)
     layers = []
-    for m in actor_critic.actor:
+    for m in actor:
         if isinstance(m, nn.Linear):
             lin = nn.Linear(m.in_features, m.out_features)
             with torch.no_grad():
@@ -186,4 +185,55 @@ def export_policy_as_jit(actor_critic, path):
             layers.append(lin)
         else:
             layers.append(copy.deepcopy(m).to("cpu"))
-    torch.jit.script(nn.Sequential(*layers)).save(os.path.join(path, "policy_1.pt"))
+    return nn.Sequential(*layers)
+
+
+def export_policy_as_jit(actor_critic, path):
+    """helpers.py:180-190: TorchScript export of the actor MLP as policy_1.pt, or, for a recurrent
+    policy (one with `memory_a`), of memory + actor as policy_lstm_1.pt (PolicyExporterLSTM)."""
+    import torch
+    if hasattr(actor_critic, "memory_a"):
+        PolicyExporterLSTM(actor_critic).export(path)
+        return
+    os.makedirs(path, exist_ok=True)
+    torch.jit.script(_plain_actor(actor_critic.actor)).save(os.path.join(path, "policy_1.pt"))
+
+
+def _policy_exporter_lstm_cls():
+    import torch
+
+    class PolicyExporterLSTM(torch.nn.Module):
+        """helpers.py:193-219: the actor's LSTM + MLP as one TorchScript module that carries its
+        (layers, 1, hidden) h / c state across calls; reset_memory() zeroes it."""
+
+        def __init__(self, actor_critic):
+            super().__init__()
+            self.actor = _plain_actor(actor_critic.actor)
+            self.is_recurrent = actor_critic.is_recurrent
+            self.memory = copy.deepcopy(actor_critic.memory_a.rnn).cpu()
+            self.register_buffer("hidden_state", torch.zeros(self.memory.num_layers, 1, self.memory.hidden_size))
+            self.register_buffer("cell_state", torch.zeros(self.memory.num_layers, 1, self.memory.hidden_size))
+
+        def forward(self, x):
+            out, (h, c) = self.memory(x.unsqueeze(0), (self.hidden_state, self.cell_state))
+            self.hidden_state[:] = h
+            self.cell_state[:] = c
+            return self.actor(out.squeeze(0))
+
+        @torch.jit.export
+        def reset_memory(self):
+            self.hidden_state[:] = 0.
+            self.cell_state[:] = 0.
+
+        def export(self, path):
+            os.makedirs(path, exist_ok=True)
+            self.to("cpu")
+            torch.jit.script(self).save(os.path.join(path, "policy_lstm_1.pt"))
+
+    return PolicyExporterLSTM
+
+
+def PolicyExporterLSTM(actor_critic):  # noqa: N802  (the reference's class name; torch imported lazily)
+    return _policy_exporter_lstm_cls()(actor_critic)
+
+
