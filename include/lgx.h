@@ -578,6 +578,9 @@ int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* part
  *   LGX_GEMM_BIAS_ELU     epi(x) = ELU(x + bias[z*N + n])
  *   LGX_GEMM_DELU_COLSUM  C = x * ELU'(Y) with Y (same layout as C) the ELU output, and
  *                         partials[t][z*N + n] = sum of C over rows 128t .. 128t+127
+ *   LGX_GEMM_DELU         C = x * ELU'(Y) (no column sums: lgx_gemm_tn's colsum of the next
+ *                         weight-gradient product gives them); split-bf16 with a pre-split B and
+ *                         K % 32 == 0 only
  * Requirements: N % 128 == 0, K % 4 == 0, A/B 16-byte aligned with lda, ldb, sa, sb % 4 == 0
  * (pad K with zero columns).  sa may be 0 (one input shared by the batch). */
 /* algo: LGX_GEMM_ALGO_DEFAULT = the process default (env LGX_GEMM_ALGO = "split" | "f32",
@@ -591,6 +594,7 @@ int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, float* part
 #define LGX_GEMM_PLAIN 0
 #define LGX_GEMM_BIAS_ELU 1
 #define LGX_GEMM_DELU_COLSUM 2
+#define LGX_GEMM_DELU 3
 typedef struct lgx_gemm_args {
   int64_t M;
   int32_t N, K, batch, epi;
@@ -618,7 +622,10 @@ int lgx_gemm_nt(const lgx_gemm_args* args, void* stream);
  *   C[((z * slices + s) * R + n) * ldc + c] = sum_{m = s Ms}^{(s+1) Ms - 1} A[z*sa + m*lda + n] * B[z*sb + m*ldb + c]
  * for z < batch, s < slices, n < R, c < Cc, Ms = M / slices.  Requirements: Ms % 32 == 0,
  * R % 128 == 0, ldb >= Cc rounded up to 128 (the padding columns are read, not stored), A/B
- * 16-byte aligned with lda, ldb, sa, sb % 4 == 0.  lgx_reduce_slices then sums the slices. */
+ * 16-byte aligned with lda, ldb, sa, sb % 4 == 0.  lgx_reduce_slices then sums the slices.
+ * colsum (optional, NULL to skip): colsum[(z * slices + s) * R + n] = sum over the same rows of
+ * A[z*sa + m*lda + n] - the per-slice column sums of A, i.e. with A = dZ_k the bias gradient's
+ * partials (rsl_rl's db_k), computed from the f32 rows the kernel stages anyway. */
 typedef struct lgx_gemm_tn_args {
   int64_t M;                    /* rows per batch entry */
   int32_t R, Cc, slices, batch;
@@ -628,6 +635,7 @@ typedef struct lgx_gemm_tn_args {
   int64_t ldb, sb;
   float* C;
   int64_t ldc;
+  float* colsum;                /* [batch][slices][R] or NULL */
 } lgx_gemm_tn_args;
 int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream);
 

@@ -287,8 +287,8 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
                        (presplit || (((uintptr_t)a.B & 15) == 0 && a.ldb % 4 == 0 && a.sb % 4 == 0));
   if (!a.A || (!a.B && !presplit) || !a.C || a.M <= 0 || a.N <= 0 || a.N % BN || a.K <= 0 || a.K % 4 ||
       a.batch <= 0 || a.batch > 65535 || !aligned || a.lda < a.K || (!presplit && a.ldb < a.K) || a.ldc < a.N ||
-      a.ldc > (1 << 22) || a.epi < 0 || a.epi > 2 || (a.epi == LGX_GEMM_BIAS_ELU && !a.bias) ||
-      (a.epi == LGX_GEMM_DELU_COLSUM && (!a.Y || !a.partials)))
+      a.ldc > (1 << 22) || a.epi < 0 || a.epi > 3 || (a.epi == LGX_GEMM_BIAS_ELU && !a.bias) ||
+      (a.epi == LGX_GEMM_DELU_COLSUM && (!a.Y || !a.partials)) || (a.epi == LGX_GEMM_DELU && !a.Y))
     return lgx_fail(LGX_EINVAL,
                     "lgx_gemm_nt: bad args (N % 128, K % 4, 16-byte aligned A/B rows, epilogue operands)");
   if (a.M * a.lda >= (1ll << 30) || (!presplit && (int64_t)a.N * a.ldb >= (1ll << 30)))
@@ -309,6 +309,7 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   if (algo == LGX_GEMM_ALGO_SPLIT_BF16) return lgx_gemm_nt_split(a, cus, stream);
+  if (a.epi == LGX_GEMM_DELU) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: LGX_GEMM_DELU needs the split-bf16 algo");
   // persistent: 2 workgroups per CU (LDS-bound), a multiple of 8 (XCD tile ranges)
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, 2 * cus / 8));
   const dim3 grid((unsigned)wgs);

@@ -421,6 +421,8 @@ int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream_) {
   const bool x3p_delu = ed ? ed[0] != '0' : X3P_DELU_DEFAULT;
   if (a.Bs && a.K % BK == 0 && pipelined && (a.epi != LGX_GEMM_DELU_COLSUM || x3p_delu))
     return lgx_gemm_nt_x3p(a, cus, stream_);
+  if (a.epi == LGX_GEMM_DELU)
+    return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: LGX_GEMM_DELU needs a pre-split B (Bs) and K % 32 == 0");
   const hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
              a.partials, 0, a.Bs};

@@ -50,11 +50,12 @@ struct TC {
   static constexpr int IMGA = 3 * TK * RA * 2;       // A limb image per stage (24 | 48 KB)
   static constexpr int IMGB = 3 * TK * TT * 2;       // B limb image (24 KB)
   static constexpr int STAGE = IMGA + IMGB;
-  static constexpr int LDS = 2 * STAGE;              // two buffers (96 | 144 KB)
   static constexpr int AQ = RA / 4;                  // A column quads per row
   static constexpr int AR = TK * AQ / PT;            // staged A rows per thread (4)
   static constexpr int BR = TK * (TT / 4) / PT;      // staged B rows per thread (4 | 2)
   static constexpr int AROW = TK / AR;               // thread row groups (8 | 8)
+  static constexpr int CS = AROW * AQ * 16;          // column-sum scratch: [row group][column quad] float4
+  static constexpr int LDS = 2 * STAGE + CS;         // two buffers (96 | 144 KB) + 4 | 8 KB
   static_assert(AR == 4 && (BR == 4 || BR == 2), "staging layout");
 };
 
@@ -67,6 +68,7 @@ struct TnArgs {
   int64_t ldb, sb;
   float* C;
   int64_t ldc;
+  float* colsum;         // [batch][S][R] per-slice column sums of A, or null
   int32_t rt, ct, tiles;
 };
 
@@ -161,7 +163,19 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_tn_x3_kernel(TnArgs g) {
     for (int i = 0; i < 4; ++i) sa[i] = *reinterpret_cast<const float4*>(Ab + oa + i * sta);
 #pragma unroll
     for (int i = 0; i < X::BR; ++i) sb[i] = *reinterpret_cast<const float4*>(Bb + ob + i * stb);
+    // column sums of this thread's staged A rows (column quad aq), for the first column tile of an
+    // (n, s, z) only; cw = 1 while the staged stage is a real one (the last stages re-load)
+    const bool csum = g.colsum != nullptr && ctile == 0;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto cs_add = [&](const float4& v, float w) {
+      cs.x = fmaf(v.x, w, cs.x);
+      cs.y = fmaf(v.y, w, cs.y);
+      cs.z = fmaf(v.z, w, cs.z);
+      cs.w = fmaf(v.w, w, cs.w);
+    };
     __syncthreads();   // (previous tile's last reads of buffer 0 are done)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cs_add(sa[i], 1.f);
 #pragma unroll
     for (int i = 0; i < 4; ++i) tn_store_row<RA>(tlds, sa[i], aq, 4 * am + i);
 #pragma unroll
@@ -195,11 +209,13 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_tn_x3_kernel(TnArgs g) {
       char* nb = tlds + ((k + 1) & 1) * X::STAGE;
       const int kl = min(k + 2, nst - 1);
       const uint32_t la = oa + kl * TK * sta, lb = ob + kl * TK * stb;
+      const float cw = k + 1 < nst ? 1.f : 0.f;   // (stage k+1 exists)
       auto side = [&](int u) {
 #ifdef TN_NO_SIDE
         return;
 #endif
         if (u < 4) {
+          cs_add(sa[u], cw);
           tn_store_row<RA>(nb, sa[u], aq, 4 * am + u);
           sa[u] = *reinterpret_cast<const float4*>(Ab + la + u * sta);
         } else if (u - 4 < X::BR) {
@@ -246,113 +262,22 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_tn_x3_kernel(TnArgs g) {
       TN_STAMP(3);
       __syncthreads();
     }
+    if (csum) {   // the 8 row groups' partial column sums, combined in a fixed order
+      float4* scr = reinterpret_cast<float4*>(tlds + 2 * X::STAGE);
+      scr[am * X::AQ + aq] = cs;
+      __syncthreads();
+      if (tid < X::AQ) {
+        float4 t = scr[tid];
+#pragma unroll
+        for (int i = 1; i < X::AROW; ++i) {
+          const float4 u = scr[i * X::AQ + tid];
+          t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        *reinterpret_cast<float4*>(g.colsum + (int64_t)(z * g.S + s) * g.R + ntile * RA + 4 * tid) = t;
+      }
+    }
     // acc[i][j][e] = C[n0 + 32i + 8(e >> 2) + 4h + (e & 3)][c0 + 32j + r]: 32 lanes store one
     // 128-byte row segment per element
-    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * RA + wm * 64) * g.ldc;
-    const int c0 = ctile * TT + wn * 64 + r;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int c = c0 + 32 * j;
-      if (c >= g.Cc) continue;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int n = 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
-          Cb[(int64_t)n * g.ldc + c] = acc[i][j][e];
-        }
-    }
-  }
-}
-
-// ---- exact-f32 alternative (A/B: LGX_GEMM_TN_F32=1): the same tiles on v_mfma_f32_32x32x2_f32, one
-// product per MAC instead of six limb products (the f32 MFMA rate is 1/16 of bf16: the split path
-// wins while it runs above 6/16 of its own peak per CU).  f32 tiles staged through registers into
-// LDS rows padded by 32 floats (the two rows of one MFMA step land in disjoint bank halves); lane
-// (r, h) of k-step kk reads A[2kk + h][n0 + r] and B[2kk + h][c0 + r] with one ds_read_b32 each.
-template <int RA>
-struct TF {
-  static constexpr int NWV = RA / 32;            // waves: RA / 64 rows x 2 columns of 64 x 64
-  static constexpr int PT = 64 * NWV;
-  static constexpr int SA = RA + 32, SB = TT + 32;   // padded row strides (floats)
-  static constexpr int STAGE = TK * (SA + SB) * 4;
-  static constexpr int LDS = 2 * STAGE;              // 112 KB (RA 256) | 80 KB (RA 128)
-  static constexpr int AR = TK * (RA / 4) / PT;      // staged A rows per thread (4)
-  static constexpr int BR = TK * (TT / 4) / PT;      // staged B rows per thread (2 | 4)
-  static_assert(AR == 4 && (BR == 2 || BR == 4), "staging layout");
-};
-
-template <int RA>
-__global__ void __launch_bounds__(2 * RA, 1) gemm_tn_f32_kernel(TnArgs g) {
-  using X = TF<RA>;
-  extern __shared__ __attribute__((aligned(16))) char tlds[];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int aq = tid % (RA / 4), am = tid / (RA / 4);
-  const int bq = tid & 31, bm = tid >> 5;
-  const int xcd = blockIdx.x & 7;
-  const int32_t stride = gridDim.x >> 3;
-  const int32_t lo = (int32_t)((int64_t)xcd * g.tiles / 8), hi = (int32_t)((int64_t)(xcd + 1) * g.tiles / 8);
-  const int nst = (int)(g.Ms / TK);
-  const uint32_t sta = (uint32_t)(g.lda * 4), stb = (uint32_t)(g.ldb * 4);
-  for (int32_t tile = lo + (blockIdx.x >> 3); tile < hi; tile += stride) {
-    int32_t t = tile;
-    const int ctile = t % g.ct;
-    t /= g.ct;
-    const int ntile = t % g.rt;
-    t /= g.rt;
-    const int s = t % g.S;
-    const int z = t / g.S;
-    const int64_t m0 = (int64_t)s * g.Ms;
-    const char* Ab = reinterpret_cast<const char*>(g.A + z * g.sa + m0 * g.lda + ntile * RA);
-    const char* Bb = reinterpret_cast<const char*>(g.B + z * g.sb + m0 * g.ldb + ctile * TT);
-    const uint32_t oa = (4 * am) * sta + aq * 16, ob = (X::BR * bm) * stb + bq * 16;
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    float4 sa[4], sb[X::BR];
-    auto put = [&](char* buf) {
-      float* fa = reinterpret_cast<float*>(buf);
-      float* fb = fa + TK * X::SA;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) *reinterpret_cast<float4*>(fa + (4 * am + i) * X::SA + 4 * aq) = sa[i];
-#pragma unroll
-      for (int i = 0; i < X::BR; ++i) *reinterpret_cast<float4*>(fb + (X::BR * bm + i) * X::SB + 4 * bq) = sb[i];
-    };
-    auto fetch = [&](int k) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sa[i] = *reinterpret_cast<const float4*>(Ab + oa + k * TK * sta + i * sta);
-#pragma unroll
-      for (int i = 0; i < X::BR; ++i) sb[i] = *reinterpret_cast<const float4*>(Bb + ob + k * TK * stb + i * stb);
-    };
-    fetch(0);
-    __syncthreads();   // (previous tile's last reads of buffer 0 are done)
-    put(tlds);
-    fetch(min(1, nst - 1));
-    __syncthreads();
-    for (int k = 0; k < nst; ++k) {
-      const float* fa = reinterpret_cast<const float*>(tlds + (k & 1) * X::STAGE) + h * X::SA + wm * 64 + r;
-      const float* fb = reinterpret_cast<const float*>(tlds + (k & 1) * X::STAGE) + TK * X::SA + h * X::SB + wn * 64 + r;
-#pragma unroll
-      for (int kk = 0; kk < TK / 2; ++kk) {
-        const float a0 = fa[2 * kk * X::SA], a1 = fa[2 * kk * X::SA + 32];
-        const float b0 = fb[2 * kk * X::SB], b1 = fb[2 * kk * X::SB + 32];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-        if (kk == 7) {   // stage k+1 into the other buffer, stage k+2's loads in flight behind the MFMAs
-          put(tlds + ((k + 1) & 1) * X::STAGE);
-          fetch(min(k + 2, nst - 1));
-        }
-      }
-      __syncthreads();
-    }
     float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * RA + wm * 64) * g.ldc;
     const int c0 = ctile * TT + wn * 64 + r;
 #pragma unroll
@@ -397,13 +322,13 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   g.sb = a.sb;
   g.C = a.C;
   g.ldc = a.ldc;
+  g.colsum = a.colsum;
+  if (a.colsum && ((uintptr_t)a.colsum & 15)) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: colsum must be 16-byte aligned");
   // 256-row tiles (8 waves) when R allows; LGX_GEMM_TN_WAVES=4 forces the 128-row tiles
   static const int force4 = [] {
     const char* e = getenv("LGX_GEMM_TN_WAVES");
     return e && atoi(e) == 4;
   }();
-  const char* fe = getenv("LGX_GEMM_TN_F32");   // read per call: tests switch it within one process
-  const bool f32 = fe && atoi(fe) == 1;
   const int nwv = (a.R % 256 == 0 && !force4) ? 8 : 4;
   const int RA = nwv == 8 ? 256 : 128;
   g.rt = a.R / RA;
@@ -421,19 +346,6 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
-  if (f32) {
-    static const bool fattrs =
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<128>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, TF<128>::LDS) == hipSuccess &&
-        hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_f32_kernel<256>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, TF<256>::LDS) == hipSuccess;
-    if (!fattrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
-    if (nwv == 8)
-      LGX_LAUNCH(gemm_tn_f32_kernel<256>, dim3((unsigned)wgs), dim3(512), TF<256>::LDS, reinterpret_cast<hipStream_t>(stream), g);
-    else
-      LGX_LAUNCH(gemm_tn_f32_kernel<128>, dim3((unsigned)wgs), dim3(256), TF<128>::LDS, reinterpret_cast<hipStream_t>(stream), g);
-    return lgx_hip_status("lgx_gemm_tn");
-  }
   if (nwv == 8)
     LGX_LAUNCH(gemm_tn_x3_kernel<8>, dim3((unsigned)wgs), dim3(512), TC<8>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else

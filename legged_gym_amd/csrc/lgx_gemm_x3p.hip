@@ -327,7 +327,62 @@ __device__ __forceinline__ void p_store_group(const PArgs& g, const f32x16v (&pe
     // on its own LDS round trip inside it
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
   }
+  // (LGX_GEMM_DELU: the run was multiplied by ELU'(Y) in place before - delu_apply)
   if (row < g.M) *reinterpret_cast<float4*>(g.C + T.z * g.sc + row * g.ldc + T.nt * PN + cn) = v;
+}
+
+// LGX_GEMM_DELU on transposed accumulators (lane = row, runs of 4 columns, as p_store_group): the
+// Y run of output run gi (16-byte load from a clamped row: unconditional), and the run multiplied
+// by ELU'(Y) in place
+template <int NWV, int PM>
+__device__ __forceinline__ const float* delu_addr(const PArgs& g, const PTile& T, int wm, int wn, int r, int h, int gi) {
+  constexpr int WI = XC<NWV, PM>::WI, WJ = XC<NWV, PM>::WJ;
+  const int q = gi & 3, j = (gi >> 2) % WJ, i = (gi >> 2) / WJ;
+  const int64_t row = min((int64_t)T.mt * PM + wm * 32 * WI + 32 * i + r, g.M - 1);
+  const int cn = wn * 32 * WJ + 32 * j + 8 * q + 4 * h;
+  return g.Y + T.z * g.sc + row * g.ldc + T.nt * PN + cn;
+}
+
+template <int NWV, int PM>
+__device__ __forceinline__ float4 delu_load(const PArgs& g, const PTile& T, int wm, int wn, int r, int h, int gi) {
+  return *reinterpret_cast<const float4*>(delu_addr<NWV, PM>(g, T, wm, wn, r, h, gi));
+}
+
+// The deferred epilogue's Y runs are loaded one slot ahead by an inline-asm load: the compiler's
+// own wait for a visible load would be counted without the (inline-asm) LDS-DMA loads issued
+// after it and drain them; the slot-top vmcnt wait covers these loads (issued before the slot's
+// B stage), and y_pin() after it orders every use behind that wait (the registers are named).
+__device__ __forceinline__ float4 y_load_asm(const float* p) {
+  float4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ void y_pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
+template <int NWV, int PM>
+__device__ __forceinline__ void delu_apply(int gi, const float4& y, f32x16v (&pend)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ]) {
+  constexpr int WJ = XC<NWV, PM>::WJ;
+  const int q = gi & 3, j = (gi >> 2) % WJ, i = (gi >> 2) / WJ;
+  pend[i][j][4 * q] *= elu_grad_from_out(y.x);
+  pend[i][j][4 * q + 1] *= elu_grad_from_out(y.y);
+  pend[i][j][4 * q + 2] *= elu_grad_from_out(y.z);
+  pend[i][j][4 * q + 3] *= elu_grad_from_out(y.w);
+}
+
+// every run of a tile at once (the last tile, or the runtime-K kernels): all Y loads in flight,
+// then multiply and store
+template <int NWV, int PM>
+__device__ __forceinline__ void delu_tile(const PArgs& g, f32x16v (&acc)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ],
+                                          const PTile& T, int wm, int wn, int r, int h) {
+  constexpr int GROUPS = XC<NWV, PM>::GROUPS;
+  float4 y[GROUPS];
+#pragma unroll
+  for (int gi = 0; gi < GROUPS; ++gi) y[gi] = delu_load<NWV, PM>(g, T, wm, wn, r, h, gi);
+#pragma unroll
+  for (int gi = 0; gi < GROUPS; ++gi) {
+    delu_apply<NWV, PM>(gi, y[gi], acc);
+    p_store_group<LGX_GEMM_DELU, NWV, PM>(g, acc, T, wm, wn, r, h, nullptr, gi);
+  }
 }
 
 // ELU' + bias-gradient column sums at a tile's end (non-transposed accumulators: lane = column
@@ -423,6 +478,10 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   constexpr int A_ST = X::A_ST, OFF_B = X::OFF_B, OFF_BIAS = X::OFF_BIAS;
   extern __shared__ __attribute__((aligned(16))) char plds[];
   constexpr bool DELU = EPI == LGX_GEMM_DELU_COLSUM;
+  // LGX_GEMM_DELU: transposed accumulators like the forward, the output deferred into the next
+  // tile's slots; the Y runs of a slot's stores are loaded one slot ahead (before that slot's
+  // B stage, so the pipeline's vmcnt counts are unchanged) and multiplied in after its barrier
+  constexpr bool DELU_T = EPI == LGX_GEMM_DELU;
   constexpr bool DEFER = KBT > 0 && !DELU;             // (ELU' + column sums: at the tile's end)
   // deferred store runs per slot (slots k with k * GPS < GROUPS store GPS runs each)
   constexpr int GPS = DEFER ? (X::GROUPS >= KBT ? X::GROUPS / KBT : 1) : 0;
@@ -483,6 +542,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = pend[i][j][e] = 0.f;
   PTile Tp{0, 0, 0};           // tile whose output is pending (DEFER)
+  float4 ynext[DELU_T && DEFER ? GPS : 1];   // (DELU) the Y runs of the next slot's stores
   bool pending = false, pend_full = false;
   int32_t q = 0;
   bool waited = false;         // (!DEFER) the epilogue already waited for the next slot's stages
@@ -537,6 +597,27 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       }
       X3P_STAMP(3);
       const bool st_now = DEFER && pending && k * GPS < X::GROUPS;
+      if constexpr (DELU_T && DEFER) {
+        if (st_now) {   // this slot's runs of the pending tile: Y loaded in the previous slot
+#pragma unroll
+          for (int u = 0; u < GPS; ++u)
+            if (k * GPS + u < X::GROUPS) {
+              y_pin(ynext[u]);
+              delu_apply<NWV, PM>(k * GPS + u, ynext[u], pend);
+            }
+        }
+        // the next slot's runs: of the pending tile within this tile, of this tile (pending from the
+        // next tile on) in its last slot
+        const bool last = k + 1 == KBT;
+        const bool ld = last ? tj + 1 < ntiles : (pending && (k + 1) * GPS < X::GROUPS);
+        if (ld) {
+#pragma unroll
+          for (int u = 0; u < GPS; ++u) {
+            const int gi = (last ? 0 : (k + 1) * GPS) + u;
+            if (gi < X::GROUPS) ynext[u] = y_load_asm(delu_addr<NWV, PM>(g, last ? T : Tp, wm, wn, r, h, gi));
+          }
+        }
+      }
       stores = DEFER && st_now && pend_full;
       const float* bias_prev = reinterpret_cast<const float*>(plds + OFF_BIAS + ((tj + 2) % 3) * 1024);
       constexpr int BG = X::B_GL;
@@ -591,6 +672,8 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 #ifndef X3P_NO_EPI
       if constexpr (DELU) {
         delu_epilogue<NWV, PM>(g, acc, T, wave, wm, wn, r, h, reinterpret_cast<float*>(plds + OFF_BIAS));
+      } else if constexpr (DELU_T) {
+        delu_tile<NWV, PM>(g, acc, T, wm, wn, r, h);
       } else {
 #pragma unroll
         for (int gi = 0; gi < X::GROUPS; ++gi)
@@ -614,10 +697,14 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   }
   if constexpr (DEFER) {   // the last tile's output (no further slots to spread it over)
 #ifndef X3P_NO_EPI
+    if constexpr (DELU_T) {
+      delu_tile<NWV, PM>(g, pend, Tp, wm, wn, r, h);
+    } else {
 #pragma unroll
-    for (int gi = 0; gi < X::GROUPS; ++gi)
-      p_store_group<EPI, NWV, PM>(g, pend, Tp, wm, wn, r, h,
-                                  reinterpret_cast<const float*>(plds + OFF_BIAS + ((ntiles - 1) % 3) * 1024), gi);
+      for (int gi = 0; gi < X::GROUPS; ++gi)
+        p_store_group<EPI, NWV, PM>(g, pend, Tp, wm, wn, r, h,
+                                    reinterpret_cast<const float*>(plds + OFF_BIAS + ((ntiles - 1) % 3) * 1024), gi);
+    }
 #else
     if (pend[0][0][0] == 1234.5f) g.C[tid] = pend[WI - 1][1][3] + pend[0][1][2] + pend[WI - 1][0][1];
 #endif
@@ -626,16 +713,18 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 
 typedef void (*x3p_fn)(PArgs);
 
-// [epilogue (PLAIN, BIAS_ELU, DELU_COLSUM)][KBT index: 0 (runtime K), 4, 8, 16]
+// [epilogue (PLAIN, BIAS_ELU, DELU_COLSUM, DELU)][KBT index: 0 (runtime K), 4, 8, 16]
 template <int NWV, int PM>
 struct X3PTable {
-  static constexpr x3p_fn k[3][4] = {
+  static constexpr x3p_fn k[4][4] = {
       {&gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 4, NWV, PM>,
        &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_PLAIN, 16, NWV, PM>},
       {&gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 4, NWV, PM>,
        &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_BIAS_ELU, 16, NWV, PM>},
       {&gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 4, NWV, PM>,
-       &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 16, NWV, PM>}};
+       &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU_COLSUM, 16, NWV, PM>},
+      {&gemm_nt_x3p_kernel<LGX_GEMM_DELU, 0, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU, 4, NWV, PM>,
+       &gemm_nt_x3p_kernel<LGX_GEMM_DELU, 8, NWV, PM>, &gemm_nt_x3p_kernel<LGX_GEMM_DELU, 16, NWV, PM>}};
 };
 
 template <int NWV, int PM>

@@ -432,13 +432,6 @@ class FusedPPOUpdate:
         self.gemm_fwd = fwd
         # algorithmic K of each launch (layer 1: the unpadded input width) for the bench's roofline
         self.k_alg = {id(g): k for g, k in zip(fwd[0], [self.num_obs, self.num_cobs])}
-        bwd = {}
-        for k in range(L - 1, 0, -1):   # dZ_{k-1} = (dZ_k W_k) * elu'(Y_{k-1}); dZ_{L-1} lives in Y[L-1]
-            dz = self.Y[L - 1] if k == L - 1 else self.D[k]
-            bwd[k] = gemm(dz.data_ptr(), h[k], M * h[k], None if self.split else self.WT[k].data_ptr(), h[k],
-                          h[k - 1] * h[k], self.D[k - 1], h[k - 1], h[k], 2, abi.GEMM_DELU_COLSUM, Y=self.Y[k - 1],
-                          parts=self.col_parts[k - 1], Bs=nlt[k])
-        self.gemm_bwd = bwd
         # weight gradients (lgx_gemm_tn): dW_k = dZ_k^T Y_{k-1} over Sk row slices into P[k]
         self.gemm_dw = {}
         if self.tn:
@@ -469,6 +462,29 @@ class FusedPPOUpdate:
                 else:                                # one input for both networks: batch stride 0
                     self.gemm_dw[0] = [tn(d0.data_ptr(), h[0], M * h[0], 0, self.Kp, 0, self.P[0].data_ptr(), h[0],
                                           self.num_obs, self.Sk[0], 2)]
+        # bias gradients db_k of the hidden layers below the last: the column sums of dZ_k, taken by
+        # dW_k's lgx_gemm_tn from the rows it stages anyway (per-slice partials, reduced with the
+        # weight gradients); the dA GEMM producing dZ_k then runs the plain ELU' epilogue
+        # (LGX_GEMM_DELU: transposed accumulators, output deferred into the next tile's slots).
+        # Layers whose dW is not on lgx_gemm_tn keep the ELU' + column-sum epilogue.
+        self.colsum = {}
+        if self.split and os.environ.get("LGX_PPO_TN_COLSUM", "1") != "0":
+            for k in range(L - 1):
+                if k not in self.gemm_dw:
+                    continue
+                cs = torch.empty(2, self.Sk[k], h[k], device=dev)
+                self.colsum[k] = cs
+                for z, t in enumerate(self.gemm_dw[k]):   # (batch 2, or one launch per network)
+                    t.colsum = cs.data_ptr() + 4 * z * self.Sk[k] * h[k]
+        bwd = {}
+        for k in range(L - 1, 0, -1):   # dZ_{k-1} = (dZ_k W_k) * elu'(Y_{k-1}); dZ_{L-1} lives in Y[L-1]
+            dz = self.Y[L - 1] if k == L - 1 else self.D[k]
+            plain = (k - 1) in self.colsum
+            bwd[k] = gemm(dz.data_ptr(), h[k], M * h[k], None if self.split else self.WT[k].data_ptr(), h[k],
+                          h[k - 1] * h[k], self.D[k - 1], h[k - 1], h[k], 2,
+                          abi.GEMM_DELU if plain else abi.GEMM_DELU_COLSUM, Y=self.Y[k - 1],
+                          parts=None if plain else self.col_parts[k - 1], Bs=nlt[k])
+        self.gemm_bwd = bwd
 
     def _separate_critic_obs(self):
         st = self.ppo.storage
@@ -494,6 +510,9 @@ class FusedPPOUpdate:
             job(self.P[0][1], self.Wg[0] + n1, n1c, 1, 0, Sk[0], n1c, 0)
         else:
             job(self.P[0], self.Wg[0], n1, 2, Sk[0] * n1, Sk[0], n1, n1)            # dW1 (actor, critic)
+        colsum = getattr(self, "colsum", {})
+        if 0 in colsum:   # db_1 from dW1's column sums: complete with dW1
+            job(colsum[0], self.bo[0], h[0], 2, Sk[0] * h[0], Sk[0], h[0], h[0])
         n_dw1 = len(jobs)   # (the layer-1 jobs come first: the rest can be reduced before dW1 is done)
         for k in range(1, self.L):
             nk = h[k] * h[k - 1]
@@ -504,6 +523,10 @@ class FusedPPOUpdate:
         hp_b = self.head_parts[(A + 1) * h[-1]:]
         job(hp_b, self.bo[self.L - 1], 2 * h[-1], 1, 0, hchunks, nh, 0)              # db of the last hidden layer
         for k in range(self.L - 1):
+            if k in colsum:
+                if k > 0:                                                            # db_k from dW_k's column sums
+                    job(colsum[k], self.bo[k], h[k], 2, Sk[k] * h[k], Sk[k], h[k], h[k])
+                continue
             cchunks = self.col_parts[k].numel() // (2 * h[k])
             job(self.col_parts[k], self.bo[k], 2 * h[k], 1, 0, cchunks, 2 * h[k], 0)  # db_k
         if len(jobs) > abi.MAX_REDUCE_JOBS:

@@ -141,7 +141,7 @@ class LgxGemmArgs(C.Structure):
 class LgxGemmTnArgs(C.Structure):
     _fields_ = [("M", i64), ("R", i32), ("Cc", i32), ("slices", i32), ("batch", i32),
                 ("A", C.c_void_p), ("lda", i64), ("sa", i64), ("B", C.c_void_p), ("ldb", i64), ("sb", i64),
-                ("C", C.c_void_p), ("ldc", i64)]
+                ("C", C.c_void_p), ("ldc", i64), ("colsum", C.c_void_p)]
 
 
 class LgxCopy2dJob(C.Structure):
@@ -151,7 +151,7 @@ class LgxCopy2dJob(C.Structure):
 
 PPO_MAX_ACTIONS = 16
 MAX_REDUCE_JOBS = 16
-GEMM_PLAIN, GEMM_BIAS_ELU, GEMM_DELU_COLSUM = 0, 1, 2
+GEMM_PLAIN, GEMM_BIAS_ELU, GEMM_DELU_COLSUM, GEMM_DELU = 0, 1, 2, 3
 GEMM_ALGO_DEFAULT, GEMM_ALGO_F32, GEMM_ALGO_SPLIT_BF16 = 0, 1, 2
 GEMM_TILE_M, GEMM_TILE_N, GEMM_K_STEP = 128, 128, 32   # K step: layer-1 rows padded to 1024 B (aligned 128-B lines)
 

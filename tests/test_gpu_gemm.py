@@ -95,7 +95,7 @@ def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0, algo=abi.GEMM_A
     acc = torch.bmm(A64, B.double().transpose(1, 2))
     if epi == abi.GEMM_BIAS_ELU:
         ref = torch.nn.functional.elu(acc + bias.double()[:, None, :])
-    elif epi == abi.GEMM_DELU_COLSUM:
+    elif epi in (abi.GEMM_DELU_COLSUM, abi.GEMM_DELU):
         y = Y.double()
         ref = acc * torch.where(y > 0, torch.ones_like(y), y + 1)
     else:
@@ -157,6 +157,26 @@ def test_gemm_presplit_delu_pipelined(gpu, monkeypatch, pm, M, N, K):
     monkeypatch.setenv("LGX_GEMM_X3P_DELU", "1")
     monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
     _run(M, N, K, 2, abi.GEMM_DELU_COLSUM, seed=M + K + pm + 1, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+
+
+@pytest.mark.parametrize("pm", [128, 256])
+@pytest.mark.parametrize("M,N,K", [(24576, 256, 128), (24576, 512, 256), (4096, 512, 512), (300, 128, 256),
+                                   (513, 256, 128), (1000, 128, 96), (1, 128, 32), (257, 384, 64)])
+def test_gemm_presplit_delu_deferred(gpu, monkeypatch, pm, M, N, K):
+    """LGX_GEMM_DELU (ELU' without column sums, the backward dA of the fused update): transposed
+    accumulators, the output deferred into the next tile's slots with the Y runs of every slot
+    loaded one slot ahead (K 128 / 256 / 512 unrolled), at the tile's end for runtime K (96, 64, 32);
+    both tile heights, ragged M, one row, several tiles per workgroup (24,576 rows)."""
+    monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
+    _run(M, N, K, 2, abi.GEMM_DELU, seed=M + K + pm + 3, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+
+
+def test_gemm_delu_needs_presplit(gpu):
+    """LGX_GEMM_DELU exists on the pipelined split-bf16 kernel only: other paths refuse it."""
+    with pytest.raises(lgxlib.LgxError):
+        _run(256, 128, 64, 1, abi.GEMM_DELU, algo=abi.GEMM_ALGO_F32)
+    with pytest.raises(lgxlib.LgxError):
+        _run(256, 128, 64, 1, abi.GEMM_DELU, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=False)
 
 
 @pytest.mark.parametrize("transpose", [False, True])
@@ -248,8 +268,9 @@ def test_split_bf16_is_f32_accurate(gpu, spread):
     assert bool((esp <= K * 2.0 ** -24 * scale).all())
 
 
-def _run_tn(M, S, R, Cc, batch, ldb=None, seed=0):
-    """lgx_gemm_tn against float64: C[z][s] = A[z, slice s]^T B[z, slice s, :Cc]."""
+def _run_tn(M, S, R, Cc, batch, ldb=None, seed=0, colsum=False):
+    """lgx_gemm_tn against float64: C[z][s] = A[z, slice s]^T B[z, slice s, :Cc] (and with colsum
+    the per-slice column sums of A)."""
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(seed)
     ldb = ldb or Cc
@@ -261,6 +282,9 @@ def _run_tn(M, S, R, Cc, batch, ldb=None, seed=0):
     a.A, a.lda, a.sa = A.data_ptr(), R, M * R
     a.B, a.ldb, a.sb = B.data_ptr(), ldb, M * ldb
     a.C, a.ldc = Cout.data_ptr(), Cc
+    cs = torch.full((batch, S, R), float("nan"), device=dev)
+    if colsum:
+        a.colsum = cs.data_ptr()
     lgxlib.check(_lib().lgx_gemm_tn(C.byref(a), _stream()), "lgx_gemm_tn")
     torch.cuda.synchronize()
     Ms = M // S
@@ -268,6 +292,10 @@ def _run_tn(M, S, R, Cc, batch, ldb=None, seed=0):
     tol = 2e-5 * Ms ** 0.5 * ref.abs().max().item() + 1e-6
     err = (Cout.double() - ref).abs().max().item()
     assert err <= tol, f"M={M} S={S} R={R} Cc={Cc}: max err {err:.3e} > {tol:.3e}"
+    if colsum:   # f32 sums of f32 rows (4 per thread, then 8 row groups in a fixed order)
+        rcs = A.double().view(batch, S, Ms, R).sum(2)
+        cerr = (cs.double() - rcs).abs().max().item()
+        assert cerr <= 1e-6 * Ms * A.abs().max().item(), f"colsum max err {cerr:.3e}"
 
 
 @pytest.mark.parametrize("M,S,R,Cc,ldb", [(1024, 2, 128, 128, None), (2048, 4, 256, 235, 256), (96, 3, 128, 384, None),
@@ -281,12 +309,13 @@ def test_gemm_tn_weight_gradients(gpu, M, S, R, Cc, ldb):
 
 
 @pytest.mark.parametrize("M,S,R,Cc,ldb", [(1024, 2, 128, 128, None), (2048, 4, 256, 235, 256), (96, 3, 128, 384, None),
-                                          (24576, 8, 512, 235, 256)])
-def test_gemm_tn_exact_f32_variant(gpu, monkeypatch, M, S, R, Cc, ldb):
-    """The exact-f32 MFMA dW kernel (LGX_GEMM_TN_F32=1, the A/B alternative to the split-bf16
-    products) under the same float64 bound."""
-    monkeypatch.setenv("LGX_GEMM_TN_F32", "1")
-    _run_tn(M, S, R, Cc, 2, ldb=ldb, seed=M + S + 1)
+                                          (24576, 16, 256, 512, None), (24576, 16, 512, 235, 256),
+                                          (24576, 32, 128, 256, None)])
+def test_gemm_tn_column_sums(gpu, M, S, R, Cc, ldb):
+    """lgx_gemm_tn's colsum (the bias gradient db = column sums of dZ, per row slice, taken from
+    the staged f32 rows by the first column tile of each output row tile): one stage per slice,
+    ragged output columns, several row and column tiles, both tile heights."""
+    _run_tn(M, S, R, Cc, 2, ldb=ldb, seed=M + S + 7, colsum=True)
 
 
 def test_gemm_tn_rejects_bad_shapes(gpu):

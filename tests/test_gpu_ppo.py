@@ -120,10 +120,11 @@ def test_fused_update_single_stream(gpu, monkeypatch):
     assert getattr(fus._fused, "_side", None) is None
 
 
-@pytest.mark.parametrize("var,val", [("LGX_GEMM_TN_F32", "1"), ("LGX_PPO_DEV_EVENTS", "0")])
+@pytest.mark.parametrize("var,val", [("LGX_PPO_TN_COLSUM", "0"), ("LGX_PPO_DEV_EVENTS", "0")])
 def test_fused_update_ab_variants(gpu, monkeypatch, var, val):
-    """The update's A/B variants against autograd: the exact-f32 MFMA weight-gradient kernel
-    (LGX_GEMM_TN_F32=1) and torch events for the cross-stream joins (LGX_PPO_DEV_EVENTS=0)."""
+    """The update's variants against autograd: the hidden-layer bias gradients from the dA GEMMs'
+    ELU' + column-sum epilogue instead of lgx_gemm_tn's column sums (LGX_PPO_TN_COLSUM=0), and torch
+    events for the cross-stream joins (LGX_PPO_DEV_EVENTS=0)."""
     monkeypatch.setenv(var, val)
     ref, fus = make_pair()
     torch.manual_seed(11)
