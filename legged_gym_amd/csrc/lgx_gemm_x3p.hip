@@ -46,6 +46,7 @@ typedef float fx2 __attribute__((ext_vector_type(2)));
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
 constexpr int PN = 128, PK = 32;
+constexpr int LGX_X3P_MAX_LDS = 160 * 1024;   // LDS per CU (one workgroup per CU)
 constexpr int B_ST = 3 * PN * PK * 2;        // 24 KB: limb B stage ([limb][128 n][64 B])
 constexpr int NSA = 3, NSB = 2;              // ring depths
 constexpr int B_BLK = 3 * 128 * 32;             // bf16 per pre-split (128 n x 32 k) block
@@ -64,6 +65,9 @@ struct XC {
   static constexpr int OFF_B = NSA * A_ST;
   static constexpr int OFF_BIAS = OFF_B + NSB * B_ST;    // 3 x 1 KB: bias of the pending / current / next tile
   static constexpr int P_LDS = OFF_BIAS + 4 * 1024;      // 151,552 | 102,400 B (DELU: 4 KB column-sum scratch)
+  // LGX_GEMM_DELU with the deferred epilogue: in place of the bias / scratch area, one 16-byte Y run
+  // per lane and per deferred store run of a slot (gps), wave-private (wave w's runs at w * gps KB)
+  static constexpr int y_lds(int gps) { return OFF_BIAS + NWV * gps * 1024; }
   static constexpr int WGN = NWV == 8 && (PM == 128 || X3P_WGN == 2) ? 2 : 1;   // waves along N
   static constexpr int WGM = NWV / WGN;                  // waves along M (4 | 8)
   static constexpr int WI = PM / WGM / 32;               // 32-row accumulator tiles per wave (2 | 1)
@@ -348,16 +352,7 @@ __device__ __forceinline__ float4 delu_load(const PArgs& g, const PTile& T, int 
   return *reinterpret_cast<const float4*>(delu_addr<NWV, PM>(g, T, wm, wn, r, h, gi));
 }
 
-// The deferred epilogue's Y runs are loaded one slot ahead by an inline-asm load: the compiler's
-// own wait for a visible load would be counted without the (inline-asm) LDS-DMA loads issued
-// after it and drain them; the slot-top vmcnt wait covers these loads (issued before the slot's
-// B stage), and y_pin() after it orders every use behind that wait (the registers are named).
-__device__ __forceinline__ float4 y_load_asm(const float* p) {
-  float4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ void y_pin(float4& v) { asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w)); }
+
 
 template <int NWV, int PM>
 __device__ __forceinline__ void delu_apply(int gi, const float4& y, f32x16v (&pend)[XC<NWV, PM>::WI][XC<NWV, PM>::WJ]) {
@@ -482,9 +477,11 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   // tile's slots; the Y runs of a slot's stores are loaded one slot ahead (before that slot's
   // B stage, so the pipeline's vmcnt counts are unchanged) and multiplied in after its barrier
   constexpr bool DELU_T = EPI == LGX_GEMM_DELU;
-  constexpr bool DEFER = KBT > 0 && !DELU;             // (ELU' + column sums: at the tile's end)
   // deferred store runs per slot (slots k with k * GPS < GROUPS store GPS runs each)
-  constexpr int GPS = DEFER ? (X::GROUPS >= KBT ? X::GROUPS / KBT : 1) : 0;
+  constexpr int GPS0 = KBT > 0 ? (X::GROUPS >= KBT ? X::GROUPS / KBT : 1) : 0;
+  // (DELU: deferred only where the Y runs of a slot fit the LDS beside the rings)
+  constexpr bool DEFER = KBT > 0 && !DELU && !(DELU_T && X::y_lds(GPS0) > LGX_X3P_MAX_LDS);
+  constexpr int GPS = DEFER ? GPS0 : 0;
   static_assert(!DEFER || X::GROUPS % GPS == 0, "every storing slot issues exactly GPS runs (vmcnt counts)");
   constexpr int UNR = KBT > 0 ? KBT : 1;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -542,7 +539,6 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = pend[i][j][e] = 0.f;
   PTile Tp{0, 0, 0};           // tile whose output is pending (DEFER)
-  float4 ynext[DELU_T && DEFER ? GPS : 1];   // (DELU) the Y runs of the next slot's stores
   bool pending = false, pend_full = false;
   int32_t q = 0;
   bool waited = false;         // (!DEFER) the epilogue already waited for the next slot's stages
@@ -598,23 +594,33 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       X3P_STAMP(3);
       const bool st_now = DEFER && pending && k * GPS < X::GROUPS;
       if constexpr (DELU_T && DEFER) {
-        if (st_now) {   // this slot's runs of the pending tile: Y loaded in the previous slot
+        // this slot's runs of the pending tile: Y staged by the previous slot's LDS-DMA into this
+        // wave's private runs (the slot-top vmcnt wait covers it: issued before that slot's B stage)
+        const char* ylds = plds + X::OFF_BIAS + wave * (GPS * 1024) + lane * 16;
+        if (st_now) {
 #pragma unroll
           for (int u = 0; u < GPS; ++u)
-            if (k * GPS + u < X::GROUPS) {
-              y_pin(ynext[u]);
-              delu_apply<NWV, PM>(k * GPS + u, ynext[u], pend);
-            }
+            if (k * GPS + u < X::GROUPS)
+              delu_apply<NWV, PM>(k * GPS + u, *reinterpret_cast<const float4*>(ylds + u * 1024), pend);
         }
-        // the next slot's runs: of the pending tile within this tile, of this tile (pending from the
-        // next tile on) in its last slot
+        // the next slot's runs (of the pending tile within this tile; of this tile, pending from the
+        // next tile on, in its last slot) into the same runs once this slot's reads have completed
         const bool last = k + 1 == KBT;
         const bool ld = last ? tj + 1 < ntiles : (pending && (k + 1) * GPS < X::GROUPS);
         if (ld) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          const PTile& Ty = last ? T : Tp;
+          const char* yb = uniform_ptr(g.Y + Ty.z * g.sc + ((int64_t)Ty.mt * PM) * g.ldc + Ty.nt * PN);
+          const uint32_t ydst = (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + X::OFF_BIAS + wave * (GPS * 1024));
 #pragma unroll
           for (int u = 0; u < GPS; ++u) {
             const int gi = (last ? 0 : (k + 1) * GPS) + u;
-            if (gi < X::GROUPS) ynext[u] = y_load_asm(delu_addr<NWV, PM>(g, last ? T : Tp, wm, wn, r, h, gi));
+            if (gi < X::GROUPS) {
+              const int q4i = gi & 3, jj = (gi >> 2) % WJ, ii = (gi >> 2) / WJ;
+              const int64_t rt = min((int64_t)wm * 32 * WI + 32 * ii + r, g.M - 1 - (int64_t)Ty.mt * PM);
+              const int cn = wn * 32 * WJ + 32 * jj + 8 * q4i + 4 * h;
+              glds16(yb, (uint32_t)((rt * g.ldc + cn) * 4), ydst + u * 1024);
+            }
           }
         }
       }
@@ -734,8 +740,20 @@ bool x3p_attrs() {
     for (x3p_fn f : row)
       if (f)
         ok &= hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  XC<NWV, PM>::P_LDS) == hipSuccess;
+                                  LGX_X3P_MAX_LDS) == hipSuccess;
   return ok;
+}
+
+// Dynamic LDS of an instantiation: the rings + bias / scratch area, or for the deferred
+// LGX_GEMM_DELU (where its Y runs fit; the kernel decides alike) the rings + the Y runs
+template <int NWV, int PM>
+int x3p_lds(int epi, int kbt) {
+  using X = XC<NWV, PM>;
+  if (epi == LGX_GEMM_DELU && kbt > 0) {
+    const int yl = X::y_lds(X::GROUPS >= kbt ? X::GROUPS / kbt : 1);
+    if (yl <= LGX_X3P_MAX_LDS) return std::max(X::P_LDS, yl);
+  }
+  return X::P_LDS;
 }
 
 // Tile height: 256 rows, or 128 (8 waves) when that fills the CUs' rounds better: cost = rounds of
@@ -798,7 +816,8 @@ int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
   const int ki = kbt == 0 ? 0 : kbt == 4 ? 1 : kbt == 8 ? 2 : 3;
   const x3p_fn f = nwv == 4 ? X3PTable<4, 256>::k[a.epi][ki]
                  : pm == 128 ? X3PTable<8, 128>::k[a.epi][ki] : X3PTable<8, 256>::k[a.epi][ki];
-  const int lds = nwv == 8 && pm == 128 ? XC<8, 128>::P_LDS : XC<8, 256>::P_LDS;
+  const int lds = nwv == 4 ? x3p_lds<4, 256>(a.epi, kbt) : pm == 128 ? x3p_lds<8, 128>(a.epi, kbt)
+                                                                  : x3p_lds<8, 256>(a.epi, kbt);
   // persistent: one workgroup per CU, a multiple of 8 (XCD tile ranges)
   const int64_t per_xcd = (g.tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));

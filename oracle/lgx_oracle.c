@@ -70,6 +70,7 @@ typedef struct {
   const lgx_buffers* b;
   const float* draws; /* injected [N, stride] or NULL */
   int32_t stride;
+  int32_t substep;    /* physics: substep index within the call (branch records) */
 } ctx_t;
 
 static float draw(const ctx_t* cx, int env, int slot, int64_t step, uint32_t tag) {
@@ -424,6 +425,7 @@ typedef struct {
   real mu;
   int status; /* 1 stick, 2 slide, 0 dropped */
   real fslide[3];
+  int point;  /* candidate primitive (branch records) */
 } contact_t;
 
 static void add_weighted_jtj(real* A, const real* J, const real* n, real wn, real wt) {
@@ -439,6 +441,60 @@ static void add_weighted_jtj(real* A, const real* J, const real* n, real wn, rea
 }
 
 #define MAXC LGX_MAX_POINTS
+
+/* ---- branch records / forced branches of the physics (test infrastructure: the derived physics
+ * tolerances of tests/test_gpu_parity.py).  The lgx contact model is discontinuous: every decision
+ * below is identified by (env, substep of the lgxo_simulate call, kind, index) and recorded with
+ * its decision and a relative margin to its threshold (|margin| small = within rounding of a
+ * flip); a forced list makes the physics take the given decision instead of the computed one, so a
+ * float64 run can follow the branch a float32 run took.
+ *   kind 1  drive of joint `index`: 1 implicit PD drive (|te| <= effort), 0 saturated;
+ *           margin (|te| - effort) / effort
+ *   kind 2  limit of joint `index`: -1 below the lower limit, 0 inside, 1 above;
+ *           margin = distance to the nearer limit (rad), negative outside
+ *   kind 3  candidate primitive `index` in contact: 1 if depth > 0; margin depth / max(radius, 1 cm)
+ *   kind 4  status of the contact of primitive `index` after pass 0: 0 separate (fn <= 0),
+ *           1 stick, 2 slide (ct |vt| > mu fn); margin = the nearer of fn / (kn depth) and
+ *           (ct |vt| - mu fn) / (mu fn) */
+typedef struct {
+  int32_t env, substep, kind, index, decision;
+  float margin;
+} lgxo_branch;
+static lgxo_branch* g_rec;
+static int64_t g_rec_cap, g_rec_n;
+static const lgxo_branch* g_force;
+static int64_t g_force_n;
+
+void lgxo_branch_trace(lgxo_branch* buf, int64_t cap) {
+  g_rec = buf;
+  g_rec_cap = buf ? cap : 0;
+  g_rec_n = 0;
+}
+int64_t lgxo_branch_count(void) { return g_rec_n; }
+void lgxo_branch_force(const lgxo_branch* list, int64_t n) {
+  g_force = list;
+  g_force_n = list ? n : 0;
+}
+
+static int branch(const ctx_t* cx, int e, int kind, int index, int decision, real margin) {
+  for (int64_t i = 0; i < g_force_n; ++i) {
+    const lgxo_branch* f = &g_force[i];
+    if (f->env == e && f->substep == cx->substep && f->kind == kind && f->index == index) {
+      decision = f->decision;
+      break;
+    }
+  }
+  if (g_rec) {
+    int64_t slot;
+#pragma omp atomic capture
+    slot = g_rec_n++;
+    if (slot < g_rec_cap) {
+      lgxo_branch r = {e, cx->substep, kind, index, decision, (float)margin};
+      g_rec[slot] = r;
+    }
+  }
+  return decision;
+}
 
 static void physics_env(const ctx_t* cx, int e) {
   const lgx_model* m = cx->m;
@@ -543,7 +599,7 @@ static void physics_env(const ctx_t* cx, int e) {
     real eff = m->dof_effort[j];
     if (p->control_type == LGX_CTRL_POS_DRIVE) {
       real te = m->kp[j] * (tgt[j] - th[j]) - m->kd[j] * thd[j];
-      if (FABS_R(te) <= eff) {
+      if (branch(cx, e, 1, j, FABS_R(te) <= eff, (FABS_R(te) - eff) / eff)) {
         implicit_drive[j] = 1;
         Dimp[j] += dt * (m->kd[j] + dt * m->kp[j]);
         g[6 + j] += m->kp[j] * (tgt[j] - th[j]);
@@ -554,10 +610,12 @@ static void physics_env(const ctx_t* cx, int e) {
       g[6 + j] += bf->torques[(int64_t)e * 12 + j]; /* explicit torques precomputed by caller */
     }
     if (m->dof_lower[j] < m->dof_upper[j]) {
-      if (th[j] < m->dof_lower[j]) {
+      const int lim = branch(cx, e, 2, j, th[j] < m->dof_lower[j] ? -1 : (th[j] > m->dof_upper[j] ? 1 : 0),
+                             FMIN_R(th[j] - m->dof_lower[j], m->dof_upper[j] - th[j]));
+      if (lim < 0) {
         Dimp[j] += dt * (m->limit_c + dt * m->limit_k);
         g[6 + j] += m->limit_k * (m->dof_lower[j] - th[j]);
-      } else if (th[j] > m->dof_upper[j]) {
+      } else if (lim > 0) {
         Dimp[j] += dt * (m->limit_c + dt * m->limit_k);
         g[6 + j] -= m->limit_k * (th[j] - m->dof_upper[j]);
       }
@@ -576,8 +634,9 @@ static void physics_env(const ctx_t* cx, int e) {
     real n[3];
     const real Pw[3] = {P[0] + rs[0], P[1] + rs[1], P[2] + rs[2]};
     real depth = ground_contact(cx, Pw, m->point_radius[i], n);
-    if (depth <= 0.0f) continue;
+    if (!branch(cx, e, 3, i, depth > 0.0f, depth / FMAX_R((real)m->point_radius[i], (real)0.01f))) continue;
     contact_t* c = &C[nc++];
+    c->point = i;
     c->body = b; c->report = m->point_report[i];
     real Pc[3] = {P[0] - n[0] * m->point_radius[i], P[1] - n[1] * m->point_radius[i], P[2] - n[2] * m->point_radius[i]};
     point_jac(&K, b, Pc, c->J);
@@ -627,12 +686,14 @@ static void physics_env(const ctx_t* cx, int e) {
         real fn = kn * c->depth - (cn + dt * kn) * vn;
         real vt[3] = {vp[0] - vn * c->n[0], vp[1] - vn * c->n[1], vp[2] - vn * c->n[2]};
         real vtn = SQRT_R(dot3(vt, vt));
-        if (fn <= 0.0f) c->status = 0;
-        else if (ct * vtn > c->mu * fn) {
-          c->status = 2;
-          real s = -c->mu * fn / vtn;
+        const int st = fn <= 0.0f ? 0 : (ct * vtn > c->mu * fn ? 2 : 1);
+        const real m_sep = fn / FMAX_R(kn * FABS_R(c->depth), (real)1e-6f);
+        const real m_slide = (ct * vtn - c->mu * fn) / FMAX_R(c->mu * FABS_R(fn), (real)1e-6f);
+        c->status = branch(cx, e, 4, c->point, st, FABS_R(m_sep) < FABS_R(m_slide) ? m_sep : m_slide);
+        if (c->status == 2) {
+          real s = -c->mu * fn / FMAX_R(vtn, (real)1e-12f);
           c->fslide[0] = s * vt[0]; c->fslide[1] = s * vt[1]; c->fslide[2] = s * vt[2];
-        } else c->status = 1;
+        }
       }
     }
   }
@@ -746,9 +807,11 @@ void lgxo_explicit_torques(const lgx_env_params* p, const lgx_buffers* b) {
 #endif /* LGXO_PHYSICS_ONLY */
 
 void lgxo_simulate(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b, int n) {
-  ctx_t cx = {m, p, b, NULL, 0};
-  for (int s = 0; s < n; ++s)
+  ctx_t cx = {m, p, b, NULL, 0, 0};
+  for (int s = 0; s < n; ++s) {
+    cx.substep = s;
     for (int e = 0; e < p->num_envs; ++e) physics_env(&cx, e);
+  }
 }
 
 #ifndef LGXO_PHYSICS_ONLY
@@ -1108,6 +1171,7 @@ void lgxo_drive_inputs(const lgx_model* m, const lgx_env_params* p, const lgx_bu
   ctx_t cx = {m, p, b, NULL, 0};
   for (int i = 0; i < p->num_envs * 12; ++i) b->actions[i] = clampf(b->actions[i], -p->clip_actions, p->clip_actions);
   for (int s = 0; s < p->decimation; ++s) {
+    cx.substep = s;
     if (p->use_actuator_history)
       for (int e = 0; e < p->num_envs; ++e) actuator_history(&cx, e, s);
     if (p->control_type == LGX_CTRL_POS_DRIVE) lgxo_compute_targets(m, p, b);
@@ -1121,6 +1185,7 @@ int lgxo_step(const lgx_model* m, const lgx_env_params* p, const lgx_buffers* b,
   ctx_t cx = {m, p, b, draws, LGX_DRAW_NOISE + p->num_obs};
   for (int i = 0; i < p->num_envs * 12; ++i) b->actions[i] = clampf(b->actions[i], -p->clip_actions, p->clip_actions);
   for (int s = 0; s < p->decimation; ++s) {
+    cx.substep = s;
     if (p->use_actuator_history)
       for (int e = 0; e < p->num_envs; ++e) actuator_history(&cx, e, s);
     if (p->control_type == LGX_CTRL_POS_DRIVE) lgxo_compute_targets(m, p, b);

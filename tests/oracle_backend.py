@@ -64,14 +64,46 @@ def load_oracle64():
         M, P, B = C.POINTER(abi.LgxModel), C.POINTER(abi.LgxEnvParams), C.POINTER(abi.LgxBuffers)
         lib.lgxo_simulate.argtypes, lib.lgxo_simulate.restype = [M, P, B, C.c_int32], None
         lib.lgxo_struct_sizes.argtypes, lib.lgxo_struct_sizes.restype = [C.POINTER(C.c_int64)], None
+        lib.lgxo_branch_trace.argtypes, lib.lgxo_branch_trace.restype = [C.c_void_p, C.c_int64], None
+        lib.lgxo_branch_count.argtypes, lib.lgxo_branch_count.restype = [], C.c_int64
+        lib.lgxo_branch_force.argtypes, lib.lgxo_branch_force.restype = [C.c_void_p, C.c_int64], None
         abi.check_layout(lib.lgxo_struct_sizes, n=3)
         _LIB64 = lib
     return _LIB64
 
 
-def simulate64(env, n):
-    """`n` physics substeps of an oracle-backed env in float64 arithmetic (state in its buffers)."""
-    load_oracle64().lgxo_simulate(*env._backend._args(), n)
+class LgxoBranch(C.Structure):
+    """One discontinuous decision of the oracle physics (lgx_oracle.c, lgxo_branch): kind 1 drive
+    (1 implicit / 0 saturated), 2 joint limit (-1 / 0 / 1), 3 candidate in contact (1 / 0), 4 contact
+    status after pass 0 (0 separate / 1 stick / 2 slide); margin = relative distance to the flip."""
+    _fields_ = [("env", C.c_int32), ("substep", C.c_int32), ("kind", C.c_int32), ("index", C.c_int32),
+                ("decision", C.c_int32), ("margin", C.c_float)]
+
+
+BRANCH_KINDS = {1: "drive", 2: "limit", 3: "contact", 4: "status"}
+BRANCH_ALTERNATIVES = {1: (0, 1), 2: (-1, 0, 1), 3: (0, 1), 4: (0, 1, 2)}
+
+
+def simulate64(env, n, force=(), record=False):
+    """`n` physics substeps of an oracle-backed env in float64 arithmetic (state in its buffers).
+    force: (env, substep, kind, index, decision) tuples the physics must take; record=True returns
+    every decision as a list of (env, substep, kind, index, decision, margin)."""
+    lib = load_oracle64()
+    fl = (LgxoBranch * max(1, len(force)))(*[LgxoBranch(*f, 0.0) for f in force])
+    lib.lgxo_branch_force(C.cast(fl, C.c_void_p) if force else None, len(force))
+    cap = env.num_envs * n * 512 if record else 0
+    buf = (LgxoBranch * max(1, cap))()
+    lib.lgxo_branch_trace(C.cast(buf, C.c_void_p) if record else None, cap)
+    try:
+        lib.lgxo_simulate(*env._backend._args(), n)
+    finally:
+        count = lib.lgxo_branch_count()
+        lib.lgxo_branch_trace(None, 0)
+        lib.lgxo_branch_force(None, 0)
+    if record:
+        assert count <= cap, "branch record buffer too small"
+        return [(b.env, b.substep, b.kind, b.index, b.decision, b.margin) for b in buf[:count]]
+    return None
 
 
 def vp(t):

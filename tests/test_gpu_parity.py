@@ -82,37 +82,108 @@ def test_library_loaded_is_in_tree(gpu, envs_flat):
 #   * the worst env of the HIP kernel within PHYS_C_MAX x the float32 oracle's worst env, and its
 #     90th-percentile env within PHYS_C_Q90 x the oracle's, each plus a floor of PHYS_ULPS float32
 #     ulps of the quantity's scale (where the float32 oracle happens to be exact);
-#   * at most one env in 64 above the worst-env bound: the contact model is discontinuous (stick /
-#     slide / separate, drive saturation), and a state within rounding of a threshold can take
-#     either branch in float32 (measured: 1 env of 192 at a 700x ratio, tools/physics_err_probe.py).
+#   * an env above the worst-env bound must be EXPLAINED by a branch flip: the contact model is
+#     discontinuous (drive saturation, joint limits, a candidate touching or not, stick / slide /
+#     separate), and a state within rounding of such a threshold can take either branch in float32.
+#     The float64 run records every decision with its relative distance to the threshold; the
+#     outlier env's nearest decisions (|margin| <= BRANCH_MARGIN_MAX) are flipped one at a time, and
+#     two at a time, in forced float64 runs, and the env must come within the bound of one of those
+#     branch truths in EVERY quantity (explain_outliers; the flip and its margin are recorded in
+#     BRANCH_FLIPS).  An outlier that no near-threshold flip explains fails the test.
 # The two float32 paths use different algorithms (dense 18x18 Cholesky vs per-leg Schur complement
 # with fma contraction), so their rounding differs: measured worst-env ratios 0.4-9x over 24
 # randomised 64-env states (standing and falling), 90th-percentile ratios <= 3x.
 PHYS_C_MAX = 16.0
 PHYS_C_Q90 = 4.0
 PHYS_ULPS = 64
+BRANCH_MARGIN_MAX = 1e-3      # relative distance to a decision's threshold that float32 rounding can cross
+BRANCH_CANDIDATES = 12        # nearest decisions tried per outlier env (single flips; pairs among the first 6)
+BRANCH_FLIPS = []             # (quantity set, env, flips, margins, HIP error before / after) of explained outliers
 PHYS_QTY = {"root_pose": lambda e: e.root_states[:, :7], "root_vel": lambda e: e.root_states[:, 7:],
             "dof_pos": lambda e: e.dof_pos, "dof_vel": lambda e: e.dof_vel, "torques": lambda e: e.torques,
             "contact_forces": lambda e: e.contact_forces}
+PHYS_STATE = ("root_states", "dof_state", "torques", "_contact_forces_full")
 
 
-def float64_truth(ora, n, state=("root_states", "dof_state", "torques", "_contact_forces_full")):
-    """{quantity: float64 tensor} after `n` substeps of the float64 physics from the oracle env's
-    current state; the oracle env's state is restored afterwards."""
+class Float64Truth(dict):
+    """{quantity: float64 tensor} after `n` float64 substeps from an oracle env's state, with what
+    a forced re-run needs: the start state and the recorded decisions."""
+
+    def forced(self, flips):
+        """The float64 quantities of a run from the same start state with `flips` (env, substep,
+        kind, index, decision) taken; the oracle env's current state is restored afterwards."""
+        from oracle_backend import simulate64
+        ora = self.ora
+        cur = {k: getattr(ora, k).clone() for k in PHYS_STATE}
+        for k, v in self.s0.items():
+            getattr(ora, k).copy_(v)
+        simulate64(ora, self.n, force=flips)
+        out = {k: f(ora).detach().double().clone() for k, f in PHYS_QTY.items()}
+        for k, v in cur.items():
+            getattr(ora, k).copy_(v)
+        return out
+
+
+def float64_truth(ora, n, state=PHYS_STATE):
+    """Float64Truth after `n` substeps of the float64 physics from the oracle env's current state
+    (decisions recorded); the oracle env's state is restored afterwards."""
     from oracle_backend import simulate64
     s0 = {k: getattr(ora, k).clone() for k in state}
-    simulate64(ora, n)
-    out = {k: f(ora).detach().double().clone() for k, f in PHYS_QTY.items()}
+    rec = simulate64(ora, n, record=True)
+    out = Float64Truth({k: f(ora).detach().double().clone() for k, f in PHYS_QTY.items()})
     for k, v in s0.items():
         getattr(ora, k).copy_(v)
+    out.ora, out.n, out.s0, out.records = ora, n, s0, rec
+    return out
+
+
+def _env_errors(truth, hip_vals, e, qty):
+    return {k: (hip_vals[k][e].detach().cpu().double() - truth[k][e]).abs().max().item() for k in qty}
+
+
+def explain_outliers(t64, hip_vals, envs, bounds, qty):
+    """Every env in `envs` (original indices) above its worst-env bound in some quantity must come
+    within `bounds` in every quantity of `qty` against the float64 truth of a near-threshold branch
+    flip (one, or two among the nearest); returns [(env, flips, margins)], appends to BRANCH_FLIPS."""
+    from oracle_backend import BRANCH_ALTERNATIVES, BRANCH_KINDS
+    import itertools
+    out = []
+    for e in envs:
+        before = _env_errors(t64, hip_vals, e, qty)
+        near = sorted((r for r in t64.records if r[0] == e and abs(r[5]) <= BRANCH_MARGIN_MAX), key=lambda r: abs(r[5]))
+        near = near[:BRANCH_CANDIDATES]
+        singles = [[(r, alt)] for r in near for alt in BRANCH_ALTERNATIVES[r[2]] if alt != r[4]]
+        pairs = [a + b for a, b in itertools.combinations(
+            [[(r, alt)] for r in near[:6] for alt in BRANCH_ALTERNATIVES[r[2]] if alt != r[4]], 2)
+            if a[0][0] is not b[0][0]]
+        found = None
+        for cand in singles + pairs:
+            flips = [(r[0], r[1], r[2], r[3], alt) for r, alt in cand]
+            errs = _env_errors(t64.forced(flips), hip_vals, e, qty)
+            if all(errs[k] <= bounds[k] for k in qty):
+                found = (flips, [r[5] for r, _ in cand], errs)
+                break
+        assert found is not None, (
+            f"env {e}: HIP error vs float64 above the worst-env bound ({before}, bounds {bounds}) and no flip of its "
+            f"{len(near)} decisions within {BRANCH_MARGIN_MAX} of a threshold explains it; nearest decisions: "
+            f"{[(BRANCH_KINDS[r[2]], r[1], r[3], r[4], r[5]) for r in sorted((r for r in t64.records if r[0] == e), key=lambda r: abs(r[5]))[:5]]}")
+        flips, margins, errs = found
+        desc = [(BRANCH_KINDS[f[2]], f"substep {f[1]}", f"index {f[3]}", f"-> {f[4]}") for f in flips]
+        BRANCH_FLIPS.append({"env": e, "flips": desc, "margins": margins, "hip_err_before": before,
+                             "hip_err_on_flipped_branch": errs})
+        out.append((e, flips, margins))
     return out
 
 
 def check_derived(t64, ora_vals, hip_vals, keep=None, qty=None):
-    """The derived physics tolerance above for every quantity (rows `keep` only when given).
+    """The derived physics tolerance above for every quantity (rows `keep` only when given), with
+    every env above the worst-env bound explained by a branch flip (explain_outliers).
     Returns {quantity: (HIP worst-env error, oracle worst-env error)}."""
-    out = {}
-    for k in qty or PHYS_QTY:
+    out, bounds, outliers = {}, {}, set()
+    qty = list(qty or PHYS_QTY)
+    n_all = t64[qty[0]].shape[0]
+    idx = torch.arange(n_all) if keep is None else torch.arange(n_all)[keep]
+    for k in qty:
         t, o, h = t64[k], ora_vals[k].detach().cpu().double(), hip_vals[k].detach().cpu().double()
         if keep is not None:
             t, o, h = t[keep], o[keep], h[keep]
@@ -120,13 +191,13 @@ def check_derived(t64, ora_vals, hip_vals, keep=None, qty=None):
         eh = (h - t).abs().reshape(n, -1).max(1).values
         eo = (o - t).abs().reshape(n, -1).max(1).values
         floor = PHYS_ULPS * 2.0 ** -23 * t.abs().max().item()
-        bound = PHYS_C_MAX * eo.max().item() + floor
-        over = int((eh > bound).sum())
-        assert over <= max(1, n // 64), (f"{k}: {over} envs with HIP error vs float64 above {PHYS_C_MAX} x the float32 "
-                                          f"oracle's worst env + floor = {bound:.3g} (HIP worst {eh.max().item():.3g})")
+        bounds[k] = PHYS_C_MAX * eo.max().item() + floor
+        outliers |= set(idx[eh > bounds[k]].tolist())
         qh, qo = torch.quantile(eh, 0.9).item(), torch.quantile(eo, 0.9).item()
         assert qh <= PHYS_C_Q90 * qo + floor, f"{k}: 90th-percentile env error {qh:.3g} > {PHYS_C_Q90} x {qo:.3g} + {floor:.3g}"
         out[k] = (eh.max().item(), eo.max().item())
+    if outliers:   # (hip_vals rows are numbered like the truth's envs; keep only selects among them)
+        explain_outliers(t64, hip_vals, sorted(outliers), bounds, qty)
     return out
 
 
