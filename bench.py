@@ -72,10 +72,8 @@ def gemm_kernel_info(key, split):
     pipe = "bf16 MFMA (v_mfma_f32_32x32x16_bf16), split-bf16: 6 limb products per f32 product"
     if key == "tn":
         return "gemm_tn_x3_kernel<*>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
-    if split:   # the pipelined kernel (ELU' + column sums on the register-staged one with LGX_GEMM_X3P_DELU=0)
-        staged = key == 2 and os.environ.get("LGX_GEMM_X3P_DELU", "1") == "0"
-        name = "gemm_nt_x3_kernel<2, true>" if staged else f"gemm_nt_x3p_kernel<{key}, *>"
-        return name, pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+    if split:   # the pipelined kernel (lgx_gemm_x3p.hip)
+        return f"gemm_nt_x3p_kernel<{key}, *>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     return f"gemm_nt_kernel<8, {key}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
 GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "
                  "to 256, 512->256, 256->128)",
@@ -513,16 +511,7 @@ def main():
     if fused_act:
         # the actuator net shares the post-physics launch in the rollout; its own roofline is
         # measured on the same rows with the standalone launch (after the timed region)
-        # (the f32 body is the one the fused launch runs: LGX_ACT_X3=0 selects its standalone kernel)
-        prev = os.environ.get("LGX_ACT_X3")
-        os.environ["LGX_ACT_X3"] = "0"
         avg[1], launches = standalone_actuator_ms(lib, env, torch)
-        os.environ["LGX_ACT_X3"] = "1"
-        act_x3_ms, _ = standalone_actuator_ms(lib, env, torch)
-        if prev is None:
-            os.environ.pop("LGX_ACT_X3")
-        else:
-            os.environ["LGX_ACT_X3"] = prev
         act_note = (f"standalone lgx_actuator_ws_kernel on this step's model_ins rows, {launches} launches after the "
                     "timed region (in the rollout it runs on workgroups of lgx_post_physics_act_kernel)")
     decim = env.cfg.control.decimation
@@ -544,11 +533,6 @@ def main():
              "algorithmic_per_launch": act_flop}
     if act_note:
         roof2["note"] = act_note
-        # the split-bf16 actuator kernel of the serial / aux-stream modes, same rows
-        roof2["split_bf16_kernel"] = {
-            "kernel": "lgx_actuator_x3_kernel", "avg_ms": act_x3_ms, "peak": MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS,
-            "achieved": act_flop / (act_x3_ms * 1e-3) / 1e12 if act_x3_ms else None,
-            "frac": (act_flop / (act_x3_ms * 1e-3) / 1e12 / (MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS)) if act_x3_ms else None}
     for r in (roof, roof2):
         if r["achieved"] is not None:
             r["frac"] = r["achieved"] / r["peak"]

@@ -315,8 +315,8 @@ int lgx_reset_idx(lgx_sim* sim, const int32_t* env_ids, int32_t n, int64_t commo
 int lgx_set_draws(lgx_sim* sim, const float* draws);
 
 /* Go1 actuator MLP (UniNet, go1.py:22-35,100-105): rows of 30 inputs -> 3 outputs,
- * 30-128-128-128-3 tanh MLP, f32-accurate: split-bf16 MFMA (three bf16 limbs per operand, six
- * limb products; LGX_ACT_X3=0 selects the f32-MFMA kernel).  w: packed [W0t b0 W1t b1 W2t b2
+ * 30-128-128-128-3 tanh MLP on the f32 MFMA (the weight-stationary body the step's post-physics
+ * launch runs).  w: packed [W0t b0 W1t b1 W2t b2
  * W3t b3] with W_lt = transposed torch Linear weight ([in x out]).  out = net(in) *
  * out_scale[col] (dVel *= vel_std). */
 int lgx_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
@@ -608,7 +608,8 @@ typedef struct lgx_gemm_args {
   const float* Y;               /* like C (DELU_COLSUM) */
   float* partials;              /* [lgx_gemm_partials_floats(M, N, batch)] (DELU_COLSUM) */
   int32_t algo;                 /* LGX_GEMM_ALGO_*: how the f32 products are evaluated */
-  int32_t reserved;
+  int32_t tile_rows;            /* pipelined split-bf16 kernel: 0 = automatic, 128 / 256 forces the
+                                   output tile height */
   const uint16_t* Bs;           /* split-bf16 only, optional: B pre-split by lgx_split_bf16 into
                                    [batch][N][ceil(K/32)][3 limbs][32] bf16 (then B is not read) */
 } lgx_gemm_args;

@@ -140,195 +140,3 @@ LGX_DEV void actuator_ws_body(const WsArgs& a, int wg, int nwg) {
     }
   }
 }
-
-// ---------------------------------------------------------------- split-bf16 weight-stationary variant
-// The same network on v_mfma_f32_32x32x16_bf16 with three RNE bf16 limbs per f32 operand and the
-// six limb products of order <= 2 (f32-accurate, lgx_gemm_split.hip), 2.67x fewer MFMA cycles
-// than the f32 MFMA.  A wave's 32-column slice of layers 0-2 lives in VGPRs as bf16 limb B
-// fragments (24 + 96 + 96 registers: one wave per SIMD, so this body runs in a launch of its own,
-// lgx_actuator_x3_kernel, not inside the post-physics launch's 256-register budget).  Weights are
-// the MFMA's first operand: each lane ends with one row and 4 runs of 4 consecutive columns, so
-// the tanh outputs are split once and stored as 8-byte limb runs of the next layer's LDS image
-// [limb][32 rows][K] (no per-fragment split); layer 2 writes f32 rows for the VALU 128 -> 3 layer.
-typedef __bf16 ax_bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 ax_bf16x2 __attribute__((ext_vector_type(2)));
-typedef float ax_fx2 __attribute__((ext_vector_type(2)));
-#define AX_RS0 (32 * 2 + 16)     // layer-0 input image row stride (bytes): K = 32 + pad
-#define AX_RS1 (128 * 2 + 16)    // hidden image row stride
-
-LGX_DEV void ax_split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
-  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((ax_fx2){x0, x1}, ax_bf16x2));
-  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
-  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((ax_fx2){r0, r1}, ax_bf16x2));
-  r0 -= __uint_as_float(l1 << 16);
-  r1 -= __uint_as_float(l1 & 0xffff0000u);
-  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((ax_fx2){r0, r1}, ax_bf16x2));
-}
-
-// B fragment limbs of W^t [K][128] (row k, column n): lane (r, h) holds column n0 + r, k = 16 kb + 8 h ..
-template <int KB>
-LGX_DEV void ax_load_w(const float* __restrict__ Wt, int K, int n, int h, ax_bf16x8 (&w)[KB][3]) {
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    float v[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int k = 16 * kb + 8 * h + i;
-      v[i] = k < K ? Wt[k * WS_H + n] : 0.f;
-    }
-    uint4 u0, u1, u2;
-    ax_split2(v[0], v[1], u0.x, u1.x, u2.x);
-    ax_split2(v[2], v[3], u0.y, u1.y, u2.y);
-    ax_split2(v[4], v[5], u0.z, u1.z, u2.z);
-    ax_split2(v[6], v[7], u0.w, u1.w, u2.w);
-    w[kb][0] = __builtin_bit_cast(ax_bf16x8, u0);
-    w[kb][1] = __builtin_bit_cast(ax_bf16x8, u1);
-    w[kb][2] = __builtin_bit_cast(ax_bf16x8, u2);
-  }
-}
-
-// acc (transposed: lane row r, columns 8 q + 4 h + i of the wave's 32) += W . X over KB k blocks
-template <int KB>
-LGX_DEV void ax_layer(const char* __restrict__ img, int rs, const ax_bf16x8 (&w)[KB][3], int r, int h,
-                      lgx_f32x16& acc) {
-  const int limb = WS_BM * rs;
-#pragma unroll
-  for (int kb = 0; kb < KB; ++kb) {
-    const char* p = img + r * rs + (16 * kb + 8 * h) * 2;
-    const ax_bf16x8 a0 = *reinterpret_cast<const ax_bf16x8*>(p);
-    const ax_bf16x8 a1 = *reinterpret_cast<const ax_bf16x8*>(p + limb);
-    const ax_bf16x8 a2 = *reinterpret_cast<const ax_bf16x8*>(p + 2 * limb);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[kb][2], a0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[kb][1], a1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[kb][0], a2, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[kb][1], a0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[kb][0], a1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[kb][0], a0, acc, 0, 0, 0);
-  }
-}
-
-// tanh(acc + b) of the lane's row into the next layer's limb image (8-byte runs of 4 columns)
-LGX_DEV void ax_epilogue_limbs(const lgx_f32x16& acc, const float (&bb)[16], char* __restrict__ img, int wave, int r,
-                               int h) {
-  const int limb = WS_BM * AX_RS1;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = fast_tanh(acc[4 * q + i] + bb[4 * q + i]);
-    uint32_t a0, a1, a2, b0, b1, b2;
-    ax_split2(v[0], v[1], a0, a1, a2);
-    ax_split2(v[2], v[3], b0, b1, b2);
-    char* p = img + r * AX_RS1 + (wave * 32 + 8 * q + 4 * h) * 2;
-    *reinterpret_cast<uint2*>(p) = make_uint2(a0, b0);
-    *reinterpret_cast<uint2*>(p + limb) = make_uint2(a1, b1);
-    *reinterpret_cast<uint2*>(p + 2 * limb) = make_uint2(a2, b2);
-  }
-}
-
-LGX_DEV void actuator_x3_body(const WsArgs& a, int wg, int nwg) {
-  __shared__ __attribute__((aligned(16))) char img0[3 * WS_BM * AX_RS0];   // layer-0 input (K 32)
-  __shared__ __attribute__((aligned(16))) char img1[3 * WS_BM * AX_RS1];   // layer-0 output
-  __shared__ __attribute__((aligned(16))) char img2[3 * WS_BM * AX_RS1];   // layer-1 output
-  __shared__ float act2[WS_BM * WS_S1];                                     // layer-2 output (f32)
-  __shared__ float w3[WS_H * 3 + 3];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const float* W0 = a.w;
-  const float* b0 = W0 + WS_IN * WS_H;
-  const float* W1 = b0 + WS_H;
-  const float* b1 = W1 + WS_H * WS_H;
-  const float* W2 = b1 + WS_H;
-  const float* b2 = W2 + WS_H * WS_H;
-  const float* W3 = b2 + WS_H;        // [128][3]
-  const float* b3 = W3 + WS_H * 3;
-  const int n = wave * 32 + r;        // this lane's weight column
-  ax_bf16x8 wl0[2][3], wl1[8][3], wl2[8][3];
-  ax_load_w<2>(W0, WS_IN, n, h, wl0);
-  ax_load_w<8>(W1, WS_H, n, h, wl1);
-  ax_load_w<8>(W2, WS_H, n, h, wl2);
-  for (int i = tid; i < WS_H * 3 + 3; i += 256) w3[i] = i < WS_H * 3 ? W3[i] : b3[i - WS_H * 3];
-  // the lane's bias values: columns wave * 32 + 8 q + 4 h + i (transposed accumulator layout)
-  float bb0[16], bb1[16], bb2[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = wave * 32 + 8 * q + 4 * h + i;
-      bb0[4 * q + i] = b0[c];
-      bb1[4 * q + i] = b1[c];
-      bb2[4 * q + i] = b2[c];
-    }
-  const float osc = a.out_scale ? a.out_scale[min(tid & 7, 2)] : 1.f;
-  const int64_t ntiles = (a.rows + WS_BM - 1) / WS_BM;
-  // the next tile's input rows (32 x 32, zero past column 30) are prefetched during this tile:
-  // thread t holds row t >> 3, columns 4 (t & 7) .. + 3
-  float pre[4];
-  auto fetch = [&](int64_t tile) {
-    const int row = tid >> 3, c0 = 4 * (tid & 7);
-    const int64_t gr = min(tile * WS_BM + row, a.rows - 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pre[i] = a.x[gr * WS_IN + min(c0 + i, WS_IN - 1)];
-  };
-  fetch(wg);
-  for (int64_t tile = wg; tile < ntiles; tile += nwg) {
-    const int64_t r0 = tile * WS_BM;
-    __syncthreads();   // the previous tile's readers of the images are done
-    {
-      const int row = tid >> 3, c0 = 4 * (tid & 7);
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = (c0 + i < WS_IN && r0 + row < a.rows) ? pre[i] : 0.f;
-      uint32_t a0, a1, a2, b0_, b1_, b2_;
-      ax_split2(v[0], v[1], a0, a1, a2);
-      ax_split2(v[2], v[3], b0_, b1_, b2_);
-      char* p = img0 + row * AX_RS0 + c0 * 2;
-      *reinterpret_cast<uint2*>(p) = make_uint2(a0, b0_);
-      *reinterpret_cast<uint2*>(p + WS_BM * AX_RS0) = make_uint2(a1, b1_);
-      *reinterpret_cast<uint2*>(p + 2 * WS_BM * AX_RS0) = make_uint2(a2, b2_);
-    }
-    fetch(tile + nwg < ntiles ? tile + nwg : tile);
-    __syncthreads();
-    lgx_f32x16 acc;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    ax_layer<2>(img0, AX_RS0, wl0, r, h, acc);           // layer 0: 30 (padded 32) -> 128
-    ax_epilogue_limbs(acc, bb0, img1, wave, r, h);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    ax_layer<8>(img1, AX_RS1, wl1, r, h, acc);           // layer 1: 128 -> 128
-    ax_epilogue_limbs(acc, bb1, img2, wave, r, h);
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-    ax_layer<8>(img2, AX_RS1, wl2, r, h, acc);           // layer 2: 128 -> 128, f32 rows for layer 3
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        act2[r * WS_S1 + wave * 32 + 8 * q + 4 * h + i] = fast_tanh(acc[4 * q + i] + bb2[4 * q + i]);
-    __syncthreads();
-    // layer 3: 128 -> 3 on the VALU; thread = (row, 16-wide k slice), 8-lane shuffle reduction
-    {
-      const int rr = tid >> 3, part = tid & 7;
-      const float* hrow = act2 + rr * WS_S1 + 16 * part;
-      const float* wk = w3 + 16 * part * 3;
-      float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const float v = hrow[k];
-        s0 += v * wk[3 * k]; s1 += v * wk[3 * k + 1]; s2 += v * wk[3 * k + 2];
-      }
-#pragma unroll
-      for (int m = 1; m < 8; m <<= 1) {
-        s0 += __shfl_xor(s0, m); s1 += __shfl_xor(s1, m); s2 += __shfl_xor(s2, m);
-      }
-      const int64_t gr = r0 + rr;
-      if (part < 3 && gr < a.rows) {
-        const float sv = part == 0 ? s0 : (part == 1 ? s1 : s2);
-        a.y[gr * 3 + part] = (sv + w3[WS_H * 3 + part]) * osc;
-      }
-    }
-  }
-}

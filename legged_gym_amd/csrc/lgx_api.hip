@@ -34,6 +34,8 @@ static int launch_check(int rc, const char* what) {
 struct lgx_sim {
   int device;
   bool dense;             // physics on lgx_physics_dense_kernel (leg_dof 6 / LGX_PHYS_DENSE=1)
+  int pp;                 // lanes per leg of the arrowhead physics kernel (lgx_physics_pp at create)
+  int act_mode;           // where the Go1 actuator net runs (LGX_ACT_OVERLAP at create)
   int32_t num_points;     // contact candidates of the model (the dense kernel's LDS sizing)
   lgx_env_params params;  // host copy
   lgx_buffers bufs;
@@ -185,6 +187,12 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   if (!s) return fail(LGX_ENOMEM, "lgx_sim_create: out of host memory");
   s->device = device;
   s->dense = dense;
+  s->pp = lgx_physics_pp(params->num_envs);
+  // where the Go1 actuator net runs (LGX_ACT_OVERLAP, read here once): 2 (default) = on workgroups
+  // of its own inside the post-physics launch, 1 = its own launch on an auxiliary stream, 0 = its
+  // own launch on the caller's stream (the PMC passes that measure it alone)
+  const char* am = getenv("LGX_ACT_OVERLAP");
+  s->act_mode = am ? atoi(am) : 2;
   s->num_points = model->num_points;
   s->params = *params;
   s->bufs = *bufs;
@@ -252,14 +260,6 @@ static int join_aux(lgx_sim* s, hipStream_t st) {
   return hip_check(hipStreamWaitEvent(st, s->aux_done, 0), "hipStreamWaitEvent(aux)");
 }
 
-// Where the Go1 actuator net runs (A/B switch LGX_ACT_OVERLAP): 2 (default) = on workgroups of
-// its own inside the post-physics launch (f32 MFMA body), 3 = the same with the split-bf16 body,
-// 1 = its own launch on an auxiliary stream, 0 = its own launch on the caller's stream (own
-// launches: the split-bf16 kernel unless LGX_ACT_X3=0).
-static int act_mode() {
-  const char* e = getenv("LGX_ACT_OVERLAP");
-  return e ? atoi(e) : 2;
-}
 
 int lgx_sync_aux(lgx_sim* s, void* stream) {
   if (!s) return fail(LGX_EINVAL, "lgx_sync_aux: null sim");
@@ -271,7 +271,7 @@ static int physics(lgx_sim* s, int32_t nsub, int32_t from_actions, const float* 
   return s->dense ? lgx_launch_physics_dense(s->d_model, s->d_params, s->bufs, s->params.num_envs, nsub, from_actions,
                                              actions, st, frozen, s->num_points)
                   : lgx_launch_physics(s->d_model, s->d_params, s->bufs, s->params.num_envs, nsub, from_actions, actions,
-                                       st, frozen);
+                                       st, frozen, s->pp);
 }
 
 int lgx_simulate(lgx_sim* s, int32_t n, void* stream) {
@@ -316,15 +316,15 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
   rc = launch_check(physics(s, p.decimation, 1, actions, st, 0), "lgx_step: physics launch");
   if (rc) return rc;
   const bool act_net = p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel;
-  const int mode = act_mode();
-  if (act_net && (mode == 2 || mode == 3)) {
+  const int mode = s->act_mode;
+  if (act_net && mode == 2) {
     // UniNet on every (substep, env, leg) row of this step's model_ins, inside the post-physics
     // launch (the next physics launch, stream-ordered after it, rewrites model_ins)
     arm(s, 2, sample);
     rc = launch_check(lgx_launch_post_physics_act(s->d_params, s->bufs, p.num_envs, step, s->draws, s->extras_snapshot,
                                                   s->bufs.model_ins, s->bufs.act_dvel,
                                                   (int64_t)p.decimation * p.num_envs * 4, s->bufs.act_net_w,
-                                                  s->bufs.act_net_scale, st, mode == 3),
+                                                  s->bufs.act_net_scale, st),
                       "lgx_step: post-physics + actuator launch");
     lgx_timing = lgx_timing_slot{};
     return rc;

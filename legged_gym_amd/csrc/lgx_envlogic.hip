@@ -630,15 +630,6 @@ lgx_post_physics_act_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B,
   else actuator_ws_body(wa, blockIdx.x - nblocks, gridDim.x - nblocks);
 }
 
-// the same launch with the split-bf16 actuator body (329 registers: one wave per SIMD, so the
-// post-physics and actuator workgroups take turns on a CU instead of sharing it)
-__global__ void __launch_bounds__(ENV_THREADS, 1)
-lgx_post_physics_act_x3_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, int64_t step, const float* draws,
-                               float* snapshot, WsArgs wa, int32_t nblocks) {
-  if ((int)blockIdx.x < nblocks) post_physics_body(P, B, step, draws, blockIdx.x, nblocks, snapshot);
-  else actuator_x3_body(wa, blockIdx.x - nblocks, gridDim.x - nblocks);
-}
-
 // reset_idx on an explicit env list (BaseTask.reset, base_task.py:111-115)
 __global__ void __launch_bounds__(LGX_ENV_BLOCK)
 lgx_reset_idx_kernel(const lgx_env_params* __restrict__ P, lgx_buffers B, const int32_t* ids, int32_t n, int64_t step,
@@ -683,8 +674,7 @@ int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int3
 
 int lgx_launch_post_physics_act(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int64_t step,
                                 const float* draws, float* extras_snapshot, const float* act_in, float* act_out,
-                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream,
-                                int x3) {
+                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream) {
   static_assert(ENV_THREADS == 256, "the actuator-net workgroups are 256 threads");
   const int blocks = (n_envs + LGX_ENV_BLOCK - 1) / LGX_ENV_BLOCK;
   const int64_t tiles = (act_rows + WS_BM - 1) / WS_BM;
@@ -693,12 +683,8 @@ int lgx_launch_post_physics_act(const lgx_env_params* dp, const lgx_buffers& b, 
   // one persistent actuator workgroup per CU next to the post-physics workgroups
   const int act_wgs = (int)std::max<int64_t>(1, std::min<int64_t>(tiles, cus));
   WsArgs wa{act_in, act_out, act_rows, act_w, act_scale};
-  if (x3)
-    LGX_LAUNCH(lgx_post_physics_act_x3_kernel, dim3(blocks + act_wgs), dim3(ENV_THREADS), 0, stream, dp, b, step,
-               draws, extras_snapshot, wa, blocks);
-  else
-    LGX_LAUNCH(lgx_post_physics_act_kernel, dim3(blocks + act_wgs), dim3(ENV_THREADS), 0, stream, dp, b, step, draws,
-               extras_snapshot, wa, blocks);
+  LGX_LAUNCH(lgx_post_physics_act_kernel, dim3(blocks + act_wgs), dim3(ENV_THREADS), 0, stream, dp, b, step, draws,
+             extras_snapshot, wa, blocks);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -299,10 +299,7 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
     return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: split-bf16 path needs 16-byte aligned C / Y / bias rows");
   const int64_t tiles = ((a.M + BM - 1) / BM) * (a.N / BN) * a.batch;
   if (tiles > (1ll << 31) - 1) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too large");
-  static const int prio = [] {  // A/B switch LGX_GEMM_PRIO=0/1 (s_setprio around the MFMA stages)
-    const char* e = getenv("LGX_GEMM_PRIO");
-    return e ? atoi(e) : 1;
-  }();
+  constexpr int prio = 1;   // s_setprio around the MFMA stages
   GemmArgs g{a.M, a.N, a.K, a.batch, a.epi, a.A, a.lda, a.sa, a.B, a.ldb, a.sb, a.C, a.ldc, a.sc, a.bias, a.Y,
              a.partials, prio, nullptr};
   int dev = 0, cus = 256;
@@ -313,21 +310,11 @@ extern "C" int lgx_gemm_nt(const lgx_gemm_args* args, void* stream) {
   // persistent: 2 workgroups per CU (LDS-bound), a multiple of 8 (XCD tile ranges)
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, 2 * cus / 8));
   const dim3 grid((unsigned)wgs);
-  const char* ew = getenv("LGX_GEMM_WAVES");  // A/B switch: 4 or 8 waves per 128 x 128 tile
-  const int nw = ew && atoi(ew) == 4 ? 4 : 8;
-  if (nw == 8) {
-    const dim3 block(512);
-    if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_BIAS_ELU>), grid, block, 0, LGX_STREAM(stream), g);
-    else if (a.epi == LGX_GEMM_DELU_COLSUM)
-      LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_DELU_COLSUM>), grid, block, 0, LGX_STREAM(stream), g);
-    else LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_PLAIN>), grid, block, 0, LGX_STREAM(stream), g);
-  } else {
-    const dim3 block(256);
-    if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH((gemm_nt_kernel<4, LGX_GEMM_BIAS_ELU>), grid, block, 0, LGX_STREAM(stream), g);
-    else if (a.epi == LGX_GEMM_DELU_COLSUM)
-      LGX_LAUNCH((gemm_nt_kernel<4, LGX_GEMM_DELU_COLSUM>), grid, block, 0, LGX_STREAM(stream), g);
-    else LGX_LAUNCH((gemm_nt_kernel<4, LGX_GEMM_PLAIN>), grid, block, 0, LGX_STREAM(stream), g);
-  }
+  const dim3 block(512);   // 8 waves per 128 x 128 tile
+  if (a.epi == LGX_GEMM_BIAS_ELU) LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_BIAS_ELU>), grid, block, 0, LGX_STREAM(stream), g);
+  else if (a.epi == LGX_GEMM_DELU_COLSUM)
+    LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_DELU_COLSUM>), grid, block, 0, LGX_STREAM(stream), g);
+  else LGX_LAUNCH((gemm_nt_kernel<8, LGX_GEMM_PLAIN>), grid, block, 0, LGX_STREAM(stream), g);
   return lgx_hip_status("lgx_gemm_nt");
 }
 

@@ -405,22 +405,10 @@ __global__ void __launch_bounds__(256) split_rows_kernel(SplitJobs J) {
 
 }  // namespace
 
-#ifndef X3P_DELU_DEFAULT
-#define X3P_DELU_DEFAULT 1
-#endif
-// lgx_gemm_nt's split-bf16 path (lgx_gemm.hip checks the common arguments first)
+// lgx_gemm_nt's split-bf16 path (lgx_gemm.hip checks the common arguments first): the pipelined
+// kernel (lgx_gemm_x3p.hip) whenever B is pre-split and K % 32 == 0, else the register-staged one
 int lgx_gemm_nt_split(const lgx_gemm_args& a, int cus, void* stream_) {
-  static const bool pipelined = [] {   // A/B switch: LGX_GEMM_X3P=0 keeps the register-staged kernel
-    const char* e = getenv("LGX_GEMM_X3P");
-    return !(e && e[0] == '0');
-  }();
-
-  // the pipelined kernel for the bias + ELU / plain epilogues and (LGX_GEMM_X3P_DELU, read per
-  // call) the ELU' + column-sum epilogue at its tiles' ends
-  const char* ed = getenv("LGX_GEMM_X3P_DELU");
-  const bool x3p_delu = ed ? ed[0] != '0' : X3P_DELU_DEFAULT;
-  if (a.Bs && a.K % BK == 0 && pipelined && (a.epi != LGX_GEMM_DELU_COLSUM || x3p_delu))
-    return lgx_gemm_nt_x3p(a, cus, stream_);
+  if (a.Bs && a.K % BK == 0) return lgx_gemm_nt_x3p(a, cus, stream_);
   if (a.epi == LGX_GEMM_DELU)
     return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: LGX_GEMM_DELU needs a pre-split B (Bs) and K % 32 == 0");
   const hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);

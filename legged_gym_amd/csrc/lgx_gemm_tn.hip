@@ -324,12 +324,8 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   g.ldc = a.ldc;
   g.colsum = a.colsum;
   if (a.colsum && ((uintptr_t)a.colsum & 15)) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: colsum must be 16-byte aligned");
-  // 256-row tiles (8 waves) when R allows; LGX_GEMM_TN_WAVES=4 forces the 128-row tiles
-  static const int force4 = [] {
-    const char* e = getenv("LGX_GEMM_TN_WAVES");
-    return e && atoi(e) == 4;
-  }();
-  const int nwv = (a.R % 256 == 0 && !force4) ? 8 : 4;
+  // 256-row tiles (8 waves) when R allows, else 128-row tiles (4 waves)
+  const int nwv = a.R % 256 == 0 ? 8 : 4;
   const int RA = nwv == 8 ? 256 : 128;
   g.rt = a.R / RA;
   g.ct = (a.Cc + TT - 1) / TT;

@@ -756,14 +756,11 @@ int x3p_lds(int epi, int kbt) {
   return X::P_LDS;
 }
 
-// Tile height: 256 rows, or 128 (8 waves) when that fills the CUs' rounds better: cost = rounds of
-// persistent tiles x tile time, a half tile measured 0.55-0.62 of a full one (e.g. the 512 -> 256 layer
-// at M = 24576: 384 full tiles = 2 rounds on 256 CUs, 768 half tiles = 3 rounds of 0.6: 100 -> 93 us).
-// LGX_GEMM_X3P_PM=128 / 256 forces one (A/B switch).
-int pick_pm(int64_t M, int ntn, int batch, int cus, int nwv) {
-  const char* e = getenv("LGX_GEMM_X3P_PM");   // (read per call: tests switch it)
-  const int forced = e ? atoi(e) : 0;
-  if (nwv != 8) return 256;
+// Tile height: 256 rows, or 128 when that fills the CUs' rounds better: cost = rounds of persistent
+// tiles x tile time, a half tile measured 0.55-0.62 of a full one (e.g. the 512 -> 256 layer at
+// M = 24576: 384 full tiles = 2 rounds on 256 CUs, 768 half tiles = 3 rounds of 0.6: 100 -> 93 us).
+// lgx_gemm_args.tile_rows = 128 / 256 forces one (tests of both heights).
+int pick_pm(int64_t M, int ntn, int batch, int cus, int forced) {
   if (forced == 128 || forced == 256) return forced;
   const int64_t t256 = (M + 255) / 256 * ntn * batch, t128 = (M + 127) / 128 * ntn * batch;
   const double c256 = (double)((t256 + cus - 1) / cus), c128 = 0.6 * (double)((t128 + cus - 1) / cus);
@@ -795,29 +792,22 @@ int lgx_gemm_nt_x3p(const lgx_gemm_args& a, int cus, void* stream_) {
   g.ntn = a.N / PN;
   if (((uintptr_t)a.Bs & 15) || a.M * a.lda * 4 >= (1ll << 32))
     return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: pre-split B must be 16-byte aligned; A < 4 GB per batch entry");
-  // K = 128 / 256 / 512 (the PPO-update layers): the k loop unrolled, BIAS_ELU / PLAIN epilogue
-  // deferred into the next tile; other K: the runtime loop with the epilogue at the tile's end.
-  // A/B switches: LGX_GEMM_DEFER=0, LGX_GEMM_X3P_WAVES=4 (8 measured 2-8 % faster on the update shapes)
-  static const bool defer = [] {
-    const char* e = getenv("LGX_GEMM_DEFER");
-    return !(e && e[0] == '0');
-  }();
-  static const int nwv = [] {
-    const char* e = getenv("LGX_GEMM_X3P_WAVES");
-    return e && atoi(e) == 4 ? 4 : 8;
-  }();
-  static const bool attrs = x3p_attrs<4, 256>() && x3p_attrs<8, 256>() && x3p_attrs<8, 128>();
+  // K = 128 / 256 / 512 (the PPO-update layers): the k loop unrolled, the epilogue deferred into
+  // the next tile; other K: the runtime loop with the epilogue at the tile's end.  Eight waves (two
+  // per SIMD; four measured 2-8 % slower on the update shapes).
+  constexpr int nwv = 8;
+  static const bool attrs = x3p_attrs<8, 256>() && x3p_attrs<8, 128>();
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_nt: hipFuncSetAttribute (dynamic LDS) failed");
-  const int pm = pick_pm(a.M, g.ntn, a.batch, cus, nwv);
+  if (a.tile_rows != 0 && a.tile_rows != 128 && a.tile_rows != 256)
+    return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: tile_rows must be 0 (automatic), 128 or 256");
+  const int pm = pick_pm(a.M, g.ntn, a.batch, cus, a.tile_rows);
   const int64_t tiles = ((a.M + pm - 1) / pm) * g.ntn * a.batch;
   if (tiles >= (1ll << 31) / 8) return lgx_fail(LGX_EINVAL, "lgx_gemm_nt: too many tiles");
   g.tiles = (int32_t)tiles;
-  const int kbt = (defer && (g.kb == 4 || g.kb == 8 || g.kb == 16)) ? g.kb : 0;
+  const int kbt = (g.kb == 4 || g.kb == 8 || g.kb == 16) ? g.kb : 0;
   const int ki = kbt == 0 ? 0 : kbt == 4 ? 1 : kbt == 8 ? 2 : 3;
-  const x3p_fn f = nwv == 4 ? X3PTable<4, 256>::k[a.epi][ki]
-                 : pm == 128 ? X3PTable<8, 128>::k[a.epi][ki] : X3PTable<8, 256>::k[a.epi][ki];
-  const int lds = nwv == 4 ? x3p_lds<4, 256>(a.epi, kbt) : pm == 128 ? x3p_lds<8, 128>(a.epi, kbt)
-                                                                  : x3p_lds<8, 256>(a.epi, kbt);
+  const x3p_fn f = pm == 128 ? X3PTable<8, 128>::k[a.epi][ki] : X3PTable<8, 256>::k[a.epi][ki];
+  const int lds = pm == 128 ? x3p_lds<8, 128>(a.epi, kbt) : x3p_lds<8, 256>(a.epi, kbt);
   // persistent: one workgroup per CU, a multiple of 8 (XCD tile ranges)
   const int64_t per_xcd = (g.tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));

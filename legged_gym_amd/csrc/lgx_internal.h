@@ -19,12 +19,13 @@ struct lgx_dev_model {
 
 int lgx_launch_ground_contact(const lgx_env_params* dp, const lgx_buffers& b, const float* q, int32_t n, float* o,
                               hipStream_t stream);
-int lgx_physics_pp(int32_t n_envs);   // lanes per leg of the physics launch at n_envs
+int lgx_physics_pp(int32_t n_envs);   // lanes per leg of the physics launch at n_envs (LGX_PHYS_PP overrides)
 // frozen != 0: only the drive inputs of `nsub` substeps (clip, targets, actuator-net history and
 // model_ins rows) with the state held fixed (lgx_drive_inputs)
+// pp: lanes per leg (lgx_physics_pp at lgx_sim_create)
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
-                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
-                       int32_t frozen = 0);
+                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream, int32_t frozen,
+                       int pp);
 // the dense joint-space kernel (lgx_physics.hip): leg_dof == 6 robots, or any with LGX_PHYS_DENSE=1
 int lgx_launch_physics_dense(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
                              int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream,
@@ -35,7 +36,7 @@ int lgx_launch_post_physics(const lgx_env_params* dp, const lgx_buffers& b, int3
 // post-physics + the Go1 actuator net (act_rows rows of act_in -> act_out) in one launch
 int lgx_launch_post_physics_act(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int64_t step,
                                 const float* draws, float* extras_snapshot, const float* act_in, float* act_out,
-                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream, int x3 = 0);
+                                int64_t act_rows, const float* act_w, const float* act_scale, hipStream_t stream);
 int lgx_launch_reset_idx(const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs, int32_t n_term_rows,
                          const int32_t* ids, int32_t n, int64_t step, int32_t init_done, const float* draws,
                          float* extras_snapshot, hipStream_t stream);

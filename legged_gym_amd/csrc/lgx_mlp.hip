@@ -222,10 +222,6 @@ static int needed_actw(const MlpArgs& a) {
   return w;
 }
 
-static int wide_waves() {
-  const char* e = getenv("LGX_MLP_WAVES");  // A/B switch: waves per workgroup of the wide kernel
-  return e ? atoi(e) : 8;
-}
 
 static int launch_batch(const MlpBatch& b, int count, hipStream_t stream) {
   int64_t rows = 0;
@@ -246,19 +242,14 @@ static int launch_batch(const MlpBatch& b, int count, hipStream_t stream) {
   const bool narrow = actw <= 264 && maxw <= 128;
   if (!narrow && actw > 1032) return -1;
   // narrow nets (actuator MLP, <= 128 wide): 32-row tiles, 33 KB LDS; wide (policy): 16-row tiles
-  const int ww = wide_waves();  // 4: 16-row tiles x 4 waves; 8: 16 x 8; 16: 32-row tiles x 8 waves
-  const int bm = (narrow || (ww == 16 && actw <= 776)) ? 32 : 16;
+  const int bm = narrow ? 32 : 16;
   int64_t tiles = (rows + bm - 1) / bm;
   int64_t grid = tiles < 2048 ? tiles : 2048;
   dim3 g((unsigned)grid, (unsigned)count);
   if (narrow)
     LGX_LAUNCH((lgx_mlp_forward_kernel<2, 264, 2, 4>), g, dim3(256), 0, stream, b);
-  else if (actw <= 776 && ww == 16)
-    LGX_LAUNCH((lgx_mlp_forward_kernel<2, 776, 8, 8>), g, dim3(512), 0, stream, b);
-  else if (actw <= 776 && ww == 8)
+  else if (actw <= 776)   // 16-row tiles x 8 waves
     LGX_LAUNCH((lgx_mlp_forward_kernel<1, 776, 8, 8>), g, dim3(512), 0, stream, b);
-  else if (actw <= 776)
-    LGX_LAUNCH((lgx_mlp_forward_kernel<1, 776, 8, 4>), g, dim3(256), 0, stream, b);
   else
     LGX_LAUNCH((lgx_mlp_forward_kernel<1, 1032, 8, 4>), g, dim3(256), 0, stream, b);
   return hipGetLastError() == hipSuccess ? 0 : -2;
@@ -292,53 +283,17 @@ int lgx_launch_mlp_forward2(const lgx_mlp_desc* d, int32_t count, hipStream_t st
 #include "lgx_actuator_ws.h"
 
 __global__ void __launch_bounds__(256, 2) lgx_actuator_ws_kernel(WsArgs a) { actuator_ws_body(a, blockIdx.x, gridDim.x); }
-// split-bf16 body: one workgroup (one wave per SIMD) per CU, 216 weight registers per lane
-__global__ void __launch_bounds__(256, 1) lgx_actuator_x3_kernel(WsArgs a) { actuator_x3_body(a, blockIdx.x, gridDim.x); }
 
-static int actuator_ws_enabled() {
-  const char* e = getenv("LGX_ACT_WS");  // A/B switch: 0 = generic fused MLP kernel
-  return e ? atoi(e) : 1;
-}
-
-int lgx_actuator_x3_enabled() {   // A/B switch: LGX_ACT_X3=0 keeps the f32 MFMA kernel for own launches
-  const char* e = getenv("LGX_ACT_X3");
-  return e ? atoi(e) : 1;
-}
-
-// packed actuator weights: W0t[30x128] b0 W1t[128x128] b1 W2t[128x128] b2 W3t[128x3] b3 (see lgx.h)
+// packed actuator weights: W0t[30x128] b0 W1t[128x128] b1 W2t[128x128] b2 W3t[128x3] b3 (see lgx.h):
+// the weight-stationary f32-MFMA body (lgx_actuator_ws.h), the one the post-physics launch runs
 int lgx_launch_actuator_mlp(const float* in, float* out, int64_t rows, const float* w, const float* out_scale,
                             hipStream_t stream, int wg_per_cu) {
   if (rows <= 0) return 0;
-  if (actuator_ws_enabled() && lgx_actuator_x3_enabled()) {
-    WsArgs wa{in, out, rows, w, out_scale};
-    const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int grid = (int)std::min<int64_t>(tiles, cus);
-    LGX_LAUNCH(lgx_actuator_x3_kernel, dim3(grid), dim3(256), 0, stream, wa);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-  }
-  if (actuator_ws_enabled()) {
-    WsArgs wa{in, out, rows, w, out_scale};
-    const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
-    const char* e = getenv("LGX_ACT_WS_PER_CU");  // persistent workgroups per CU (A/B switch)
-    const int per_cu = e ? std::max(1, atoi(e)) : std::max(1, wg_per_cu);
-    const int grid = (int)std::min<int64_t>(tiles, 256 * per_cu);
-    LGX_LAUNCH(lgx_actuator_ws_kernel, dim3(grid), dim3(256), 0, stream, wa);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-  }
-  MlpBatch b{};
-  MlpArgs& a = b.m[0];
-  a.x = in; a.y = out; a.rows = rows; a.nl = 4; a.act = 2; a.out_scale = out_scale;
-  const int d[5] = {30, 128, 128, 128, 3};
-  const float* p = w;
-  for (int l = 0; l < 4; ++l) {
-    a.dims[l] = d[l];
-    a.wt[l] = p; p += d[l] * d[l + 1];
-    a.b[l] = p; p += d[l + 1];
-  }
-  a.dims[4] = 3;
-  return launch_batch(b, 1, stream);
+  WsArgs wa{in, out, rows, w, out_scale};
+  const int64_t tiles = (rows + WS_BM - 1) / WS_BM;
+  const int grid = (int)std::min<int64_t>(tiles, 256 * std::max(1, wg_per_cu));
+  LGX_LAUNCH(lgx_actuator_ws_kernel, dim3(grid), dim3(256), 0, stream, wa);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // ---------------------------------------------------------------- ANYmal SEA LSTM

@@ -1407,9 +1407,9 @@ int lgx_physics_pp(int32_t n_envs) {
 }
 
 int lgx_launch_physics(const lgx_dev_model* dm, const lgx_env_params* dp, const lgx_buffers& b, int32_t n_envs,
-                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream, int32_t frozen) {
+                       int32_t nsub, int32_t from_actions, const float* act_src, hipStream_t stream, int32_t frozen,
+                       int ppx) {
   if (!act_src) act_src = b.actions;
-  const int ppx = lgx_physics_pp(n_envs);
   const int blocks = (n_envs + 15) / 16;       // 16 envs per workgroup of 64*PP lanes
   if (ppx == 8)
     LGX_LAUNCH(lgx_physics_kernel<8>, dim3(blocks), dim3(512), 0, stream, dm, dp, b, nsub, from_actions, act_src, frozen);

@@ -1125,9 +1125,7 @@ extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int6
                      ((1ULL << 40) + rc - 1) / rc, ((1ULL << 40) + (uint64_t)j.cols - 1) / (uint64_t)j.cols};
   }
   hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
-  const char* eb = getenv("LGX_ADAM_BLOCKS");   // A/B (read per call)
-  const int cap = eb && atoi(eb) > 0 ? atoi(eb) : 1024;
-  int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, cap);
+  int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
   hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
                      grad_scale, max_norm, lr, step, beta1, beta2, eps, M);
   return lgx_hip_status("lgx_adam_clip_mirror");

@@ -135,7 +135,7 @@ class LgxGemmArgs(C.Structure):
     _fields_ = [("M", i64), ("N", i32), ("K", i32), ("batch", i32), ("epi", i32),
                 ("A", C.c_void_p), ("lda", i64), ("sa", i64), ("B", C.c_void_p), ("ldb", i64), ("sb", i64),
                 ("C", C.c_void_p), ("ldc", i64), ("sc", i64), ("bias", C.c_void_p), ("Y", C.c_void_p),
-                ("partials", C.c_void_p), ("algo", i32), ("reserved", i32), ("Bs", C.c_void_p)]
+                ("partials", C.c_void_p), ("algo", i32), ("tile_rows", i32), ("Bs", C.c_void_p)]
 
 
 class LgxGemmTnArgs(C.Structure):

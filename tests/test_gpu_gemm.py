@@ -66,7 +66,8 @@ def _limbs_to_f32(Bs, batch, nout, kout):
     return _limbs(Bs, batch, nout, kout).sum(1)
 
 
-def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0, algo=abi.GEMM_ALGO_DEFAULT, presplit=False):
+def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0, algo=abi.GEMM_ALGO_DEFAULT, presplit=False,
+         tile_rows=0):
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(seed)
     lda = K + lda_pad
@@ -83,7 +84,7 @@ def _run(M, N, K, batch, epi, shared_a=False, lda_pad=0, seed=0, algo=abi.GEMM_A
     a.B, a.ldb, a.sb = B.data_ptr(), K, N * K
     a.C, a.ldc, a.sc = Cout.data_ptr(), N, M * N
     a.bias, a.Y, a.partials = bias.data_ptr(), Y.data_ptr(), parts.data_ptr()
-    a.algo = algo
+    a.algo, a.tile_rows = algo, tile_rows
     if presplit:
         Bs = _presplit(B)
         a.Bs = Bs.data_ptr()
@@ -138,37 +139,34 @@ def test_gemm_presplit_update_shape(gpu, epi):
 @pytest.mark.parametrize("pm", [128, 256])
 @pytest.mark.parametrize("M,N,K", [(24576, 256, 512), (4096, 512, 256), (300, 128, 256), (513, 256, 128),
                                    (1000, 128, 96), (1, 128, 32)])
-def test_gemm_presplit_tile_heights(gpu, monkeypatch, pm, M, N, K):
+def test_gemm_presplit_tile_heights(gpu, pm, M, N, K):
     """The pipelined kernel with 256-row tiles and with 128-row half tiles (chosen when they fill the
-    CUs' rounds better, forced here with LGX_GEMM_X3P_PM): unrolled K 512 / 256 / 128 with the
+    CUs' rounds better, forced here with lgx_gemm_args.tile_rows): unrolled K 512 / 256 / 128 with the
     deferred epilogue, runtime K 96, ragged M, one row."""
-    monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
     for epi in (abi.GEMM_PLAIN, abi.GEMM_BIAS_ELU):
-        _run(M, N, K, 2, epi, seed=M + K + pm, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+        _run(M, N, K, 2, epi, seed=M + K + pm, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True, tile_rows=pm)
 
 
 @pytest.mark.parametrize("pm", [128, 256])
 @pytest.mark.parametrize("M,N,K", [(24576, 256, 128), (24576, 512, 256), (300, 128, 256), (513, 256, 128),
                                    (1000, 128, 96), (1, 128, 32)])
-def test_gemm_presplit_delu_pipelined(gpu, monkeypatch, pm, M, N, K):
-    """ELU' + bias-gradient column sums on the pipelined kernel (LGX_GEMM_X3P_DELU=1): the epilogue
-    at each tile's end with non-transposed accumulators, partial rows per 128 output rows from
-    the waves of both tile heights; ragged M, one row, runtime K."""
-    monkeypatch.setenv("LGX_GEMM_X3P_DELU", "1")
-    monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
-    _run(M, N, K, 2, abi.GEMM_DELU_COLSUM, seed=M + K + pm + 1, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+def test_gemm_presplit_delu_pipelined(gpu, pm, M, N, K):
+    """ELU' + bias-gradient column sums on the pipelined kernel: the epilogue at each tile's end
+    with non-transposed accumulators, partial rows per 128 output rows from the waves of both tile
+    heights; ragged M, one row, runtime K."""
+    _run(M, N, K, 2, abi.GEMM_DELU_COLSUM, seed=M + K + pm + 1, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True,
+         tile_rows=pm)
 
 
 @pytest.mark.parametrize("pm", [128, 256])
 @pytest.mark.parametrize("M,N,K", [(24576, 256, 128), (24576, 512, 256), (4096, 512, 512), (300, 128, 256),
                                    (513, 256, 128), (1000, 128, 96), (1, 128, 32), (257, 384, 64)])
-def test_gemm_presplit_delu_deferred(gpu, monkeypatch, pm, M, N, K):
+def test_gemm_presplit_delu_deferred(gpu, pm, M, N, K):
     """LGX_GEMM_DELU (ELU' without column sums, the backward dA of the fused update): transposed
     accumulators, the output deferred into the next tile's slots with the Y runs of every slot
     loaded one slot ahead (K 128 / 256 / 512 unrolled), at the tile's end for runtime K (96, 64, 32);
     both tile heights, ragged M, one row, several tiles per workgroup (24,576 rows)."""
-    monkeypatch.setenv("LGX_GEMM_X3P_PM", str(pm))
-    _run(M, N, K, 2, abi.GEMM_DELU, seed=M + K + pm + 3, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True)
+    _run(M, N, K, 2, abi.GEMM_DELU, seed=M + K + pm + 3, algo=abi.GEMM_ALGO_SPLIT_BF16, presplit=True, tile_rows=pm)
 
 
 def test_gemm_delu_needs_presplit(gpu):

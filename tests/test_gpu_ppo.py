@@ -410,7 +410,7 @@ def test_fused_update_bench_shape_every_step_is_exact(gpu, n_envs):
     minibatches, every coordinate of every step checked as in test_fused_update_every_step_is_exact
     (gradient vs autograd at the recorded parameters and rows, the step vs float64 clip + Adam)."""
     from ppo_trace import StepTrace, adam64, flat_view
-    for var in ("LGX_GEMM_ALGO", "LGX_PPO_DW_SIDE", "LGX_PPO_EARLY_REDUCE", "LGX_PPO_SPLITS", "LGX_GEMM_X3P_PM"):
+    for var in ("LGX_GEMM_ALGO", "LGX_PPO_DW_SIDE", "LGX_PPO_EARLY_REDUCE", "LGX_PPO_SPLITS"):
         assert var not in os.environ, var     # the bench's default schedule
     Tb = 24
     ref, fus = make_pair("adaptive", None, T=Tb, N=n_envs, epochs=1)

@@ -37,8 +37,8 @@ for step in $STEPS; do
     run $O stall phys SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT && \
     run $O inst phys SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 && \
     run $O fetch phys FETCH_SIZE && run $O write phys WRITE_SIZE && \
-    LGX_ACT_OVERLAP=0 LGX_ACT_X3=0 run $O fetch_sep phys FETCH_SIZE && \
-    LGX_ACT_OVERLAP=0 LGX_ACT_X3=0 run $O write_sep phys WRITE_SIZE || exit 1
+    LGX_ACT_OVERLAP=0 run $O fetch_sep phys FETCH_SIZE && \
+    LGX_ACT_OVERLAP=0 run $O write_sep phys WRITE_SIZE || exit 1
     python tools/pmc_summary.py $O gpurun_out/${TAG}_pmc_env_kernels.json "rocprofv3 --kernel-trace --pmc, per-dispatch means over tools/kbench.py physrun (go1_rough, 4096 envs, 10 env steps); FETCH_SIZE/WRITE_SIZE in KB (gfx950: FETCH_SIZE reads half of wide coalesced bytes); SQ_* cycle counters per dispatch summed over SEs (DESIGN 4.1); passes *_sep ran with LGX_ACT_OVERLAP=0 (actuator net as its own launch), instruction counters = wave-instructions per dispatch" > /dev/null || exit 1 ;;
   ppopmc)
     O=gpurun_out/${TAG}_pmc_ppo; rm -rf $O; mkdir -p $O

@@ -114,34 +114,18 @@ def env_env_ab(task=os.environ.get("KB_TASK", "go1_rough"), n=int(os.environ.get
 
 
 def phys_ab():
-    """A/B the physics kernel lanes-per-leg variants in one process."""
-    import ctypes as C
+    """A/B the physics kernel lanes-per-leg variants (LGX_PHYS_PP, read when a sim is created)."""
     from oracle_backend import make_env
     for task in ("go1_flat_bench", "go1_rough"):
-        env = make_env(task, num_envs=4096, device="cuda:0", backend="lgx")
-        env.reset()
-        for pp in ("2", "4", "8", "4", "8"):
+        envs = {}
+        for pp in ("2", "4", "8"):
             os.environ["LGX_PHYS_PP"] = pp
-            ms = timeit(lambda: env.simulate(4), iters=20)
-            print(f"{task} physics 4 substeps N=4096 PP={pp}: {ms*1e3:.1f} us")
+            envs[pp] = make_env(task, num_envs=4096, device="cuda:0", backend="lgx")
+            envs[pp].reset()
         os.environ.pop("LGX_PHYS_PP")
-
-
-def mlp_ab():
-    """A/B the wide (policy) MLP tile height: rollout actor+critic on 4096 rows."""
-    from legged_gym_amd.rl.actor_critic import ActorCritic
-    ac = ActorCritic(235, 235, 12, [512, 256, 128], [512, 256, 128]).cuda()
-    x = torch.randn(4096, 235, device="cuda:0")
-    f = 2 * 4096 * 2 * (235 * 512 + 512 * 256 + 256 * 128 + 128 * 6.5)
-    with torch.inference_mode():
-        ref = (ac.actor(x), ac.critic(x))
-        for rs in ("1", "1"):
-            os.environ["LGX_MLP_WIDE_RS"] = rs
-            m, v = ac.rollout_forward(x, x)
-            err = max((m - ref[0]).abs().max().item(), (v - ref[1]).abs().max().item())
-            ms = timeit(lambda: ac.rollout_forward(x, x), iters=50)
-            print(f"rollout MLP RS={rs}: {ms*1e3:.1f} us {f/ms/1e9:.1f} TFLOP/s  max|err| {err:.2e}")
-    os.environ.pop("LGX_MLP_WIDE_RS")
+        for pp in ("2", "4", "8", "4", "8"):
+            ms = timeit(lambda: envs[pp].simulate(4), iters=20)
+            print(f"{task} physics 4 substeps N=4096 PP={pp}: {ms*1e3:.1f} us")
 
 
 def ppo_ab(T=24, N=4096, OBS=235, ACT=12, modes=("lib", "auto", "lgx", "lib", "auto", "lgx"), gemms=True):
@@ -257,8 +241,7 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
         j.src, j.dst, j.src_ld, j.src_bs, j.dst_ld, j.dst_bs = B.data_ptr(), Bs.data_ptr(), k_, n_ * k_, ld, n_ * ld
         j.rows, j.cols, j.batch, j.transpose = n_, k_, 2, 0
         lgxlib.check(lib.lgx_split_bf16((abi.LgxCopy2dJob * 1)(j), 1, stream), "split")
-        for algo, waves in [(al, "8") for al in algos]:   # 3 = split-bf16 with pre-split B
-            os.environ["LGX_GEMM_WAVES"] = waves
+        for algo in algos:   # 3 = split-bf16 with pre-split B
             a.algo = min(algo, 2)
             a.Bs = Bs.data_ptr() if algo == 3 else None
             t1 = timeit(lambda: lib.lgx_gemm_nt(C.byref(a), stream), iters=iters)
@@ -275,9 +258,8 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
                     tot = (d[1:, 0] - d[:-1, 0]).mean().item() if v.sum() > 1 else 0
                     print(f"  wave {w}: slots {int(v.sum())} per-slot cycles {tot:.0f}: wait {seg[0]:.0f} "
                           f"barrier {seg[1]:.0f} issue {seg[2]:.0f} stores {seg[3]:.0f} compute {seg[4]:.0f}", flush=True)
-            print(f"gemm M={M} N={n_} K={k_} epi={epi} algo={algo} waves={waves}: lgx {t1*1e3:.1f} us "
+            print(f"gemm M={M} N={n_} K={k_} epi={epi} algo={algo}: lgx {t1*1e3:.1f} us "
                   f"{f/t1/1e9:.1f} TF/s", flush=True)
-        os.environ.pop("LGX_GEMM_WAVES")
         if torch_too:
             t2 = timeit(lambda: torch.bmm(A, B.transpose(1, 2), out=Cc), iters=iters)
             print(f"  torch bmm (no epilogue) {t2*1e3:.1f} us {f/t2/1e9:.1f} TF/s", flush=True)
@@ -352,8 +334,6 @@ if __name__ == "__main__":
         env_bench()
     if "phys" in what:
         phys_ab()
-    if "mlpab" in what:
-        mlp_ab()
     if "physrun" in what:
         phys_run()
     if "ppo" in what:
