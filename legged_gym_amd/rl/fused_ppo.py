@@ -195,11 +195,14 @@ class FusedPPOUpdate:
         self.num_obs = la[0].in_features
         self.num_cobs = lc[0].in_features
         self.A = la[-1].out_features
-        # flat layout: layer-major so that {actor, critic} blocks of a layer are adjacent
-        order = []
-        for k in range(self.L + 1):
+        # flat layout: layer-major so that {actor, critic} blocks of a layer are adjacent; the layer-1
+        # biases right after the layer-1 weights: both come from dW1's lgx_gemm_tn (weights, and the
+        # bias gradient from its column sums), so the second data-parallel gradient bucket - what
+        # is complete only once dW1 is - is the contiguous prefix [0, nW1)
+        order = [la[0].weight, lc[0].weight, la[0].bias, lc[0].bias]
+        for k in range(1, self.L + 1):
             order += [la[k].weight, lc[k].weight]
-        for k in range(self.L + 1):
+        for k in range(1, self.L + 1):
             order += [la[k].bias, lc[k].bias]
         order.append(ac.std)
         n = sum(p.numel() for p in order)
@@ -219,7 +222,7 @@ class FusedPPOUpdate:
                 p.grad = self.flat_g[off:off + k].view_as(p)
                 off += k
         self.n = n
-        self.nW1 = self.off[id(la[1].weight)]   # end of the {actor, critic} layer-1 weight blocks
+        self.nW1 = self.off[id(la[1].weight)]   # end of the {actor, critic} layer-1 weight + bias blocks
         self.bucketed = False                     # (last minibatch: two all-reduce buckets)
         self.la, self.lc = la, lc
         self.W = []    # per layer k < L: stacked [2, out, in] weight view (k >= 1) or per-net views (k == 0)
