@@ -214,6 +214,63 @@ def update_env_ab(var=os.environ.get("KB_VAR", "LGX_PPO_EARLY_REDUCE"), rounds=i
         print(f"{var}={m}: median {v[len(v) // 2]:.3f} ms, min {v[0]:.3f} ms over {len(v)} updates", flush=True)
 
 
+def update_plan_ab(var=os.environ.get("KB_VAR", "LGX_PPO_TN_COLSUM"), rounds=int(os.environ.get("KB_ROUNDS", "12")),
+                   T=24, N=4096, OBS=235, ACT=12, modes=tuple(os.environ.get("KB_VALUES", "1,0").split(","))):
+    """A/B of an update switch read when the update's launch plan is built (FusedPPOUpdate._alloc):
+    one PPO object per value (built with `var` set, same seed and data), updates interleaved in ONE
+    process (HIP events around each full update); prints median / min per value and the kernel
+    time of one minibatch's backward is left to the rocprof trace."""
+    from legged_gym_amd.rl.actor_critic import ActorCritic
+    from legged_gym_amd.rl.ppo import PPO
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(3)
+    data = dict(observations=torch.randn(T, N, OBS, device=dev, generator=g),
+                actions=torch.randn(T, N, ACT, device=dev, generator=g),
+                rewards=torch.randn(T, N, 1, device=dev, generator=g),
+                values=torch.randn(T, N, 1, device=dev, generator=g),
+                actions_log_prob=torch.randn(T, N, 1, device=dev, generator=g) * 0.3 - 17,
+                mu=torch.randn(T, N, ACT, device=dev, generator=g) * 0.1,
+                sigma=torch.rand(T, N, ACT, device=dev, generator=g) * 0.5 + 0.75)
+    last = torch.randn(N, 1, device=dev, generator=g)
+    ppos = {}
+
+    def one(ppo):
+        st = ppo.storage
+        for k, v in data.items():
+            getattr(st, k).copy_(v)
+        st.step = T
+        st.compute_returns(last, 0.99, 0.95)
+        ppo.update()
+    prev = os.environ.get(var)
+    for m in modes:
+        os.environ[var] = m
+        torch.manual_seed(0)
+        ac = ActorCritic(OBS, OBS, ACT, [512, 256, 128], [512, 256, 128]).to(dev)
+        ppo = PPO(ac, num_learning_epochs=5, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95,
+                  value_loss_coef=1.0, entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0,
+                  schedule="adaptive", desired_kl=0.01, device=dev, use_fused_update=True)
+        ppo.init_storage(N, T, [OBS], [None], [ACT])
+        one(ppo)   # (builds the plan with `var` set)
+        ppos[m] = ppo
+    if prev is None:
+        os.environ.pop(var)
+    else:
+        os.environ[var] = prev
+    res = {m: [] for m in modes}
+    for r in range(rounds):
+        for m in modes:
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            one(ppos[m])
+            e1.record()
+            e1.synchronize()
+            res[m].append(e0.elapsed_time(e1))
+    for m in modes:
+        v = sorted(res[m])
+        print(f"{var}={m}: median {v[len(v) // 2]:.3f} ms, min {v[0]:.3f} ms over {len(v)} updates", flush=True)
+
+
 def gemm_bench(M=24576, torch_too=False, iters=20):
     """lgx_gemm_nt at the PPO-update shapes (and torch bmm without epilogue for reference)."""
     import ctypes as C
@@ -347,6 +404,8 @@ if __name__ == "__main__":
         tn_bench()
     if "update_env" in what:
         update_env_ab()
+    if "update_plan" in what:
+        update_plan_ab()
     if "env_env" in what:
         env_env_ab()
 
