@@ -84,6 +84,11 @@ __device__ __forceinline__ void xm_load(bf16x8 (&b)[XM_PF], const char* __restri
                                         int lane) {
   constexpr int G = 4 / TPW;
   const int lo = (lane & 31) * 32 + (lane >> 5) * 16;     // B fragment lane offset in a 1 KB limb block
+#ifdef XM_NO_WLOAD   // A/B: no weight stream (wrong results; measures the MFMA + LDS side alone)
+#pragma unroll
+  for (int i = 0; i < XM_PF; ++i) b[i] = __builtin_bit_cast(bf16x8, make_uint4(lo + kb0, i, wave, KB));
+  return;
+#endif
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -131,6 +136,11 @@ __device__ __forceinline__ void xm_layer(const char* __restrict__ img, int rs, c
       for (int t = 0; t < TPW; ++t) {
         const bf16x8* w = b + (g * TPW + t) * 3;
         f32x16 c = acc[t];   // small limb products first
+#ifdef XM_NO_MFMA   // A/B: weight stream + A reads only (wrong results)
+        c[0] += (float)w[2][0] + (float)w[1][1] + (float)w[0][2] + (float)a0[0] + (float)a1[1] + (float)a2[2];
+        acc[t] = c;
+        continue;
+#endif
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[2], a0, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[1], a1, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w[0], a2, c, 0, 0, 0);
@@ -219,9 +229,8 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
       off += xm_bp(a.dims[l + 1]);
     }
   }
-  LGX_CLK(0);
   __syncthreads();
-  LGX_CLK(1);
+  LGX_CLK(0);
   int boff = 0;   // layer l's bias offset in bias_lds
   const int row = lane & 31, h = lane >> 5;
   for (int l = 0; l < a.nl; ++l) {
@@ -240,7 +249,7 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
     if (tpw == 2) xm_layer<2>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc, pre);
     else if (tpw == 1) xm_layer<1>(in, xm_rs(K), W, xm_kp(K) / 16, wave, lane, acc, pre);
     if (!last) xm_prefetch(pre, a, l + 1, wave, lane);
-    LGX_CLK(2 + (l < 3 ? l : 2));
+    LGX_CLK(1 + (l < 4 ? l : 3));
     // epilogue: lane holds row `row`, columns cb*32 + 8q + 4h + (0..3) in acc[t][4q .. 4q+3]
     const int rs_out = xm_rs(N);
 #pragma unroll

@@ -215,7 +215,9 @@ def update_env_ab(var=os.environ.get("KB_VAR", "LGX_PPO_EARLY_REDUCE"), rounds=i
 
 
 def update_plan_ab(var=os.environ.get("KB_VAR", "LGX_PPO_TN_COLSUM"), rounds=int(os.environ.get("KB_ROUNDS", "12")),
-                   T=24, N=4096, OBS=235, ACT=12, modes=tuple(os.environ.get("KB_VALUES", "1,0").split(","))):
+                   T=24, N=4096, OBS=235, ACT=12,
+                   modes=tuple(os.environ.get("KB_VALUES", "1,0").split(";" if ";" in os.environ.get("KB_VALUES", "")
+                                                                          else ","))):
     """A/B of an update switch read when the update's launch plan is built (FusedPPOUpdate._alloc):
     one PPO object per value (built with `var` set, same seed and data), updates interleaved in ONE
     process (HIP events around each full update); prints median / min per value and the kernel
