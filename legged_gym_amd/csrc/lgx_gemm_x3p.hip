@@ -547,22 +547,42 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   // KBT of this tile or the next), so the next tile's coordinates and A row offsets are computed
   // once per tile instead of the iterators' per-slot wrap tests (measured: ~230 scalar / VALU
   // instructions between the barrier and the first MFMA of every slot)
-  static_assert(KBT == 0 || KBT >= 2, "A runs two slots ahead: at most one tile boundary");
+  static_assert(KBT == 0 || (KBT >= 2 && KBT % 2 == 0), "A runs two slots ahead: at most one tile boundary; "
+                "an even K step count keeps the B ring index compile-time");
   AOffs<NWV, PM> aon = ao;
   PTile T = ptile(g, t0);
+  // (KBT > 0) the DMA plans of a slot from per-tile uniform bases and running ring offsets: the
+  // per-slot plan arithmetic (64-bit address products, ring indices modulo 3, readfirstlanes) took
+  // 300-500 cycles between the barrier and the first MFMA of every slot (X3P_CLOCK)
+  constexpr int BG0 = X::B_GL;
+  const uint32_t lds_aw = (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + (tid >> 6) * (AG * 1024));
+  const uint32_t lds_bw = (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + OFF_B + (tid >> 6) * (BG0 * 1024));
+  uint32_t off_ac = 0, off_ai = 2 * A_ST;   // A ring byte offsets of slot q (compute) and q + 2 (issue)
+  const char* a_nxt = uniform_ptr(reinterpret_cast<const char*>(g.A + T.z * g.sa));
+  const char* b_nxt = uniform_ptr(reinterpret_cast<const char*>(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb) * B_BLK) +
+                                  (tid >> 6) * (BG0 * 1024));
   for (int32_t tj = 0; tj < ntiles; ++tj) {
     if (KBT == 0) T = ptile(g, t0 + tj * stride);
     PTile Tn = T;
+    const char* a_cur = a_nxt;
+    const char* b_cur = b_nxt;
+    const bool last_tile = tj + 1 == ntiles;
     if constexpr (KBT > 0) {
-      Tn = ptile(g, t0 + (tj + 1) * stride);
-      if (tj + 1 < ntiles) a_offs<NWV, PM>(aon, g, Tn.mt, tid);
+      Tn = ptile(g, t0 + (tj + 1) * stride);   // (past the last tile: bases computed, never loaded)
+      if (!last_tile) a_offs<NWV, PM>(aon, g, Tn.mt, tid);
+      a_nxt = uniform_ptr(reinterpret_cast<const char*>(g.A + Tn.z * g.sa));
+      b_nxt = uniform_ptr(reinterpret_cast<const char*>(g.Bs + Tn.z * g.sbs + (int64_t)(Tn.nt * g.kb) * B_BLK) +
+                          (tid >> 6) * (BG0 * 1024));
     }
 #pragma unroll UNR
     for (int k = 0; k < kb; ++k, ++q) {
       X3P_STAMP(0);
+      // slots q + 1 / q + 2 exist (KBT > 0: compile-time except in the last tile's last slots)
+      const bool more1 = KBT > 0 ? !(last_tile && k + 1 >= KBT) : q + 1 < nslots;
+      const bool more2 = KBT > 0 ? !(last_tile && k + 2 >= KBT) : q + 2 < nslots;
       if (!waited) {
         // slot q's stages; A(q+1) (AG loads) and last iteration's stores may stay in flight
-        if (q + 1 < nslots) {
+        if (more1) {
           if (DEFER && stores) wait_vm<AG + GPS>();
           else wait_vm<AG>();
         } else {
@@ -577,15 +597,18 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       // slot q+1's B stage and slot q+2's A stage (same order as always: B, bias, A), and this
       // slot's share of the pending output, spread over the MFMA blocks of compute(q)
       const bool a_next = KBT > 0 && k + 2 >= KBT, b_next = KBT > 0 && k + 1 >= KBT;
-      const bool do_b = q + 1 < nslots, do_a = q + 2 < nslots;
+      const bool do_b = more1, do_a = more2;
       const bool do_bias = BIAS && w0 && (KBT > 0 ? b_next : kbb == 0) && do_b;
       const int bbuf = KBT > 0 ? (tj + (b_next ? 1 : 0)) % 3 : jb % 3;
       DmaPlan pb{nullptr, 0}, pa{nullptr, 0};
       const PTile Tbias = KBT > 0 ? (b_next ? Tn : T) : Tb;
-      if (do_b) pb = plan_b<NWV, PM>(lds0, (q + 1) % NSB, g, Tbias, KBT > 0 ? (k + 1) % KBT : kbb, tid);
-      if (do_a)
-        pa = plan_a<NWV, PM>(lds0, (q + 2) % NSA, g, KBT > 0 ? (a_next ? Tn.z : T.z) : Ta.z,
-                             KBT > 0 ? (k + 2) % KBT : ka, tid);
+      if constexpr (KBT > 0) {   // (KBT even: the B ring index (q + 1) % 2 is (k + 1) % 2)
+        pb = DmaPlan{(b_next ? b_nxt : b_cur) + ((k + 1) % KBT) * (B_BLK * 2), lds_bw + ((k + 1) % NSB) * B_ST};
+        pa = DmaPlan{(a_next ? a_nxt : a_cur) + ((k + 2) % KBT) * (PK * 4), lds_aw + off_ai};
+      } else {
+        if (do_b) pb = plan_b<NWV, PM>(lds0, (q + 1) % NSB, g, Tbias, kbb, tid);
+        if (do_a) pa = plan_a<NWV, PM>(lds0, (q + 2) % NSA, g, Ta.z, ka, tid);
+      }
       const AOffs<NWV, PM> aoq = KBT > 0 && a_next ? aon : ao;
       if (KBT == 0) {
         if (do_b) next_b();
@@ -656,11 +679,14 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       };
       X3P_STAMP(4);
 #ifndef X3P_NO_COMPUTE
-      compute_slot<NWV, PM, !DELU>(plds + (q % NSA) * A_ST, plds + OFF_B + (q % NSB) * B_ST, wm, wn, r, h, acc, side);
+      compute_slot<NWV, PM, !DELU>(plds + (KBT > 0 ? off_ac : (q % NSA) * A_ST),
+                                   plds + OFF_B + (KBT > 0 ? k % NSB : q % NSB) * B_ST, wm, wn, r, h, acc, side);
 #else
       for (int blk = 0; blk < X::NB; ++blk) side(blk);
 #endif
       X3P_STAMP(5);
+      off_ac = off_ac == (NSA - 1) * A_ST ? 0u : off_ac + A_ST;
+      off_ai = off_ai == (NSA - 1) * A_ST ? 0u : off_ai + A_ST;
     }
     // ---- tile end
     if constexpr (DEFER) {

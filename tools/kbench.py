@@ -281,7 +281,10 @@ def gemm_bench(M=24576, torch_too=False, iters=20):
     dev = "cuda:0"
     lib = lgxlib.load()
     stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
-    for (n_, k_, epi) in ((512, 240, 1), (512, 256, 1), (256, 512, 1), (128, 256, 1), (256, 128, 2), (512, 256, 2)):
+    shapes = ((512, 256, 1), (256, 512, 1), (128, 256, 1), (256, 128, 3), (512, 256, 3))   # forwards, dA3, dA2
+    if os.environ.get("KB_SHAPES"):   # "n,k,epi;n,k,epi..."
+        shapes = [tuple(int(v) for v in s.split(",")) for s in os.environ["KB_SHAPES"].split(";")]
+    for (n_, k_, epi) in shapes:
         A = torch.randn(2, M, k_, device=dev)
         B = torch.randn(2, n_, k_, device=dev)
         Cc = torch.empty(2, M, n_, device=dev)
