@@ -57,6 +57,9 @@ constexpr int B_BLK = 3 * 128 * 32;             // bf16 per pre-split (128 n x 3
 #ifndef X3P_WGN
 #define X3P_WGN 1
 #endif
+#ifndef X3P_BOLD
+#define X3P_BOLD 1
+#endif
 // Tile of PM = 256 rows (the default) or 128 rows (half tiles: the layer whose 256-row tile count
 // leaves a fractional last round on the CUs, e.g. 384 tiles on 256 CUs -> 768 half tiles = 3 rounds)
 template <int NWV, int PM>
@@ -79,6 +82,17 @@ struct XC {
   static constexpr int NB = 2 * WI * WJ;                 // MFMA blocks per slot (two 16-k halves)
   static constexpr int ITEMS = B_GL + 1 + A_GL;          // side items per slot: B loads, bias, A loads
   static constexpr int IPB = (ITEMS + NB - 1) / NB;      // side items per MFMA block
+  // BOLD: the older half of the waves (0 .. NWV/2-1, which win issue arbitration and then idle at
+  // the slot barrier) issues the whole B stage, 2 B_GL loads each; the younger half only its A rows.
+  // Half tiles only (isolated, 3 alternated runs: 512 -> 256 forward 90.1 -> 87.2 us; the 256-row
+  // tiles' K = 256 forwards 71.8 -> 72.8 and 32.4 -> 34.3 us: a longer pipeline prologue per tile)
+  static constexpr bool BOLD = X3P_BOLD && PM == 128;
+  static constexpr int ITEMS_O = 2 * B_GL + 1 + A_GL, IPB_O = (ITEMS_O + NB - 1) / NB;
+  static constexpr int IPB_Y = (A_GL + NB - 1) / NB;
+  // B-stage byte offset of wave w's loads
+  static __device__ __forceinline__ int bw_off(int w) {
+    return BOLD ? (w < NWV / 2 ? w * (2 * B_GL * 1024) : 0) : w * (B_GL * 1024);
+  }
   static_assert((WGM == 4 || WGM == 8) && (WI == 1 || WI == 2), "wave rows of 32 WI rows");
 };
 
@@ -204,9 +218,10 @@ template <int NWV, int PM>
 __device__ __forceinline__ DmaPlan plan_b(uint32_t lds0, int buf, const PArgs& g, const PTile& T, int ks, int tid) {
   using X = XC<NWV, PM>;
   constexpr int BG = X::B_GL;
+  (void)BG;
   return DmaPlan{uniform_ptr(reinterpret_cast<const char*>(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb + ks) * B_BLK) +
-                             (tid >> 6) * (BG * 1024)),
-                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + X::OFF_B + buf * B_ST + (tid >> 6) * (BG * 1024))};
+                             X::bw_off(tid >> 6)),
+                 (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + X::OFF_B + buf * B_ST + X::bw_off(tid >> 6))};
 }
 
 template <int NWV, int PM>
@@ -230,9 +245,12 @@ __device__ __forceinline__ void issue_b(uint32_t lds0, int buf, const PArgs& g, 
   constexpr int BG = X::B_GL;
   const int w = tid >> 6, lane = tid & 63;
   const char* src = uniform_ptr(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb + ks) * B_BLK);
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + X::OFF_B + buf * B_ST + w * (BG * 1024));
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(lds0 + X::OFF_B + buf * B_ST + X::bw_off(w));
+  if (!X::BOLD || __builtin_amdgcn_readfirstlane(w) < NWV / 2) {
 #pragma unroll
-  for (int i = 0; i < BG; ++i) glds16(src, (uint32_t)(w * (BG * 1024) + i * 1024 + lane * 16), dst + i * 1024);
+    for (int i = 0; i < (X::BOLD ? 2 * BG : BG); ++i)
+      glds16(src, (uint32_t)(X::bw_off(w) + i * 1024 + lane * 16), dst + i * 1024);
+  }
   if (bias)
     glds16(uniform_ptr(g.bias + (int64_t)T.z * g.N + T.nt * PN), (uint32_t)((lane & 31) * 16),
            __builtin_amdgcn_readfirstlane(lds0 + X::OFF_BIAS + bbuf * 1024));
@@ -556,11 +574,13 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
   // 300-500 cycles between the barrier and the first MFMA of every slot (X3P_CLOCK)
   constexpr int BG0 = X::B_GL;
   const uint32_t lds_aw = (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + (tid >> 6) * (AG * 1024));
-  const uint32_t lds_bw = (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + OFF_B + (tid >> 6) * (BG0 * 1024));
+  const uint32_t lds_bw = (uint32_t)__builtin_amdgcn_readfirstlane(lds0 + OFF_B + X::bw_off(tid >> 6));
+  const bool older = __builtin_amdgcn_readfirstlane(tid >> 6) < NWV / 2;
+  (void)BG0;
   uint32_t off_ac = 0, off_ai = 2 * A_ST;   // A ring byte offsets of slot q (compute) and q + 2 (issue)
   const char* a_nxt = uniform_ptr(reinterpret_cast<const char*>(g.A + T.z * g.sa));
   const char* b_nxt = uniform_ptr(reinterpret_cast<const char*>(g.Bs + T.z * g.sbs + (int64_t)(T.nt * g.kb) * B_BLK) +
-                                  (tid >> 6) * (BG0 * 1024));
+                                  X::bw_off(tid >> 6));
   for (int32_t tj = 0; tj < ntiles; ++tj) {
     if (KBT == 0) T = ptile(g, t0 + tj * stride);
     PTile Tn = T;
@@ -572,7 +592,7 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       if (!last_tile) a_offs<NWV, PM>(aon, g, Tn.mt, tid);
       a_nxt = uniform_ptr(reinterpret_cast<const char*>(g.A + Tn.z * g.sa));
       b_nxt = uniform_ptr(reinterpret_cast<const char*>(g.Bs + Tn.z * g.sbs + (int64_t)(Tn.nt * g.kb) * B_BLK) +
-                          (tid >> 6) * (BG0 * 1024));
+                          X::bw_off(tid >> 6));
     }
 #pragma unroll UNR
     for (int k = 0; k < kb; ++k, ++q) {
@@ -653,17 +673,26 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_nt_x3p_kernel(PArgs g) {
       auto side = [&](int blk) {
         // side items (IPB per MFMA block, in this order): BG B loads, the bias, AG A loads; then
         // the stores
+        if (!X::BOLD || older) {
+          constexpr int NBW = X::BOLD ? 2 * BG : BG, IPBW = X::BOLD ? X::IPB_O : X::IPB;
 #pragma unroll
-        for (int e = 0; e < X::IPB; ++e) {
-          const int it = blk * X::IPB + e;
-          if (it < BG) {
-            if (do_b) glds16(pb.src, (uint32_t)(lane * 16 + it * 1024), pb.dst + it * 1024);
-          } else if (it == BG) {
-            if (do_bias)
-              glds16(uniform_ptr(g.bias + (int64_t)Tbias.z * g.N + Tbias.nt * PN), (uint32_t)((lane & 31) * 16),
-                     __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
-          } else if (it <= BG + AG) {
-            if (do_a) glds16(pa.src, aoq.o[it - BG - 1], pa.dst + (it - BG - 1) * 1024);
+          for (int e = 0; e < IPBW; ++e) {
+            const int it = blk * IPBW + e;
+            if (it < NBW) {
+              if (do_b) glds16(pb.src, (uint32_t)(lane * 16 + it * 1024), pb.dst + it * 1024);
+            } else if (it == NBW) {
+              if (do_bias)
+                glds16(uniform_ptr(g.bias + (int64_t)Tbias.z * g.N + Tbias.nt * PN), (uint32_t)((lane & 31) * 16),
+                       __builtin_amdgcn_readfirstlane(lds0 + OFF_BIAS + bbuf * 1024));
+            } else if (it <= NBW + AG) {
+              if (do_a) glds16(pa.src, aoq.o[it - NBW - 1], pa.dst + (it - NBW - 1) * 1024);
+            }
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < X::IPB_Y; ++e) {
+            const int it = blk * X::IPB_Y + e;
+            if (it < AG && do_a) glds16(pa.src, aoq.o[it], pa.dst + it * 1024);
           }
         }
         if constexpr (DEFER) {
