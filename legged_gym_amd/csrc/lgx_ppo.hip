@@ -285,18 +285,7 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
 // one workgroup: reduce the loss partials, write d std / d b4a / d b4c into the flat gradient,
 // the KL mean and the running loss sums.  Thread (g, k): value k over partial blocks g, g+8, ...
 // then a fixed-order combine of the 8 groups.
-// 64-lane sum in a fixed butterfly order (every lane of the wave gets it)
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
-  return v;
-}
-
-// sq (optional): the sum of squares of the gradient entries written here (d std, d b4a, d b4c) ->
-// *sq, and the optimizer step counter advanced (the clip norm's partial for
-// lgx_adam_clip_mirror_sq; lgx_reduce_slices_sq)
-__device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks, float* sq = nullptr,
-                              int64_t* step = nullptr) {   // TPB threads
+__device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks) {   // TPB threads
   const int A = a.num_actions;
   const int NP = 2 * A + 4;               // <= 36
   __shared__ float red[8][2 * LGX_PPO_MAX_ACTIONS + 4];
@@ -317,20 +306,6 @@ __device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks, float
   }
   __syncthreads();
   const int t = threadIdx.x;
-  if (sq && t < 64) {   // wave 0 (NP <= 36 lanes hold values): squares of the written entries
-    float v = 0.f;
-    if (t < NP) {
-      float s2 = 0.f;
-#pragma unroll
-      for (int g = 0; g < 8; ++g) s2 += red[g][t];
-      v = t < A ? s2 - a.entropy_coef / a.std[t] : t <= 2 * A ? s2 : 0.f;
-    }
-    v = wave_sum(v * v);
-    if (t == 0) {
-      *sq = v;
-      if (step) step[0] += 1;
-    }
-  }
   if (t >= NP) return;
   float s = 0.f;
 #pragma unroll
@@ -695,15 +670,12 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
 // Jobs whose offsets, strides and n are multiples of 4 floats (16-byte aligned: the split-K weight
 // partials) run on float4 lanes (tile_outputs < 0: -4 x 64 outputs per workgroup, 64 lanes x 4
 // slice groups), the rest on scalar lanes.
-// sq (optional): sq[workgroup] = the sum of squares of the outputs it writes (fixed order: wave 0's
-// lanes, butterfly), so the clip norm needs no pass of its own over the gradient
 __global__ void __launch_bounds__(TPB)
-reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin, int32_t fin_blocks, float* sq,
-                     int64_t* step) {
+reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin, int32_t fin_blocks) {
   // workgroup 0: the deferred loss finalize of lgx_ppo_loss_bwd (first, so its serial partial
   // sums overlap the reduction tiles instead of trailing them)
   if (fin_blocks > 0 && blockIdx.x == 0) {
-    loss_finalize(fin, fin_blocks, sq, step);
+    loss_finalize(fin, fin_blocks);
     return;
   }
   __shared__ float red[TPB];
@@ -731,7 +703,6 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin,
     }
     red4[t] = acc;
     __syncthreads();
-    float q2 = 0.f;
     if (g == 0 && o4 < total4) {
       float4 sum = red4[oi];
       for (int q = 1; q < groups; ++q) {
@@ -739,11 +710,6 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin,
         sum.x += u.x; sum.y += u.y; sum.z += u.z; sum.w += u.w;
       }
       *reinterpret_cast<float4*>(jb.dst + j * jb.dst_stride + i) = sum;
-      q2 = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
-    }
-    if (sq && g == 0) {   // (g == 0: wave 0)
-      q2 = wave_sum(q2);
-      if (t == 0) sq[blockIdx.x] = q2;
     }
     return;
   }
@@ -762,16 +728,10 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin,
   }
   red[t] = acc;
   __syncthreads();
-  float q2 = 0.f;
   if (g == 0 && o < total) {
     float sum = red[oi];
     for (int q = 1; q < groups; ++q) sum += red[q * ot + oi];
     jb.dst[j * jb.dst_stride + i] = sum;
-    q2 = sum * sum;
-  }
-  if (sq && t < 64) {   // (the g == 0 lanes t < ot <= 64 are in wave 0)
-    q2 = wave_sum(q2);
-    if (t == 0) sq[blockIdx.x] = q2;
   }
 }
 
@@ -1087,8 +1047,7 @@ extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32
 }
 
 static int reduce_slices_launch(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* fin,
-                                void* stream, float* sq = nullptr, int64_t* step = nullptr,
-                                int64_t* blocks_out = nullptr) {
+                                void* stream) {
   if (!jobs || njobs <= 0 || njobs > LGX_MAX_REDUCE_JOBS) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job count");
   lgx_reduce_jobs J;
   int64_t tiles = 0;
@@ -1112,31 +1071,9 @@ static int reduce_slices_launch(const lgx_reduce_job* jobs, int32_t njobs, const
     fin_blocks = (int32_t)((f.rows + LB_ROWS - 1) / LB_ROWS);
     tiles += 1;
   }
-  if (blocks_out) {   // (query only)
-    *blocks_out = tiles;
-    return LGX_OK;
-  }
   hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs, f,
-                     fin_blocks, sq, step);
+                     fin_blocks);
   return lgx_hip_status("lgx_reduce_slices");
-}
-
-extern "C" int64_t lgx_reduce_slices_blocks(const lgx_reduce_job* jobs, int32_t njobs, int32_t with_finalize) {
-  lgx_ppo_loss_args f{};
-  f.rows = 1;
-  int64_t n = -1;
-  if (reduce_slices_launch(jobs, njobs, with_finalize ? &f : nullptr, nullptr, nullptr, nullptr, &n) != LGX_OK)
-    return -1;
-  return n;
-}
-
-extern "C" int lgx_reduce_slices_sq(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* loss,
-                                    float* sq, int64_t* step, void* stream) {
-  if (!sq) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_sq: null sum-of-squares output");
-  if (loss && (!loss->defer_finalize || loss->rows <= 0))
-    return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_sq: loss args must be a deferred-finalize lgx_ppo_loss_bwd call's");
-  if (step && !loss) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_sq: the step advances on the finalize workgroup");
-  return reduce_slices_launch(jobs, njobs, loss, stream, sq, step);
 }
 
 extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream) {
@@ -1163,15 +1100,13 @@ extern "C" int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, 
   return lgx_hip_status("lgx_adam_clip");
 }
 
-static int adam_clip_mirror_launch(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
-                                   float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
-                                   float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
-                                   void* stream, bool presummed) {
-  if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 ||
-      nparts > (presummed ? (1 << 20) : 1024) || nmirrors < 0 || nmirrors > MAX_MIRRORS || (nmirrors && !mirrors))
+extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
+                                    float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
+                                    float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
+                                    void* stream) {
+  if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 || nparts > 1024 || nmirrors < 0 ||
+      nmirrors > MAX_MIRRORS || (nmirrors && !mirrors))
     return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: bad args");
-  if (presummed && grad_scale != 1.0f)
-    return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror_sq: the presummed squares are of the unscaled gradient");
   Mirrors M{};
   M.n = nmirrors;
   for (int q = 0; q < nmirrors; ++q) {
@@ -1189,26 +1124,9 @@ static int adam_clip_mirror_launch(float* p, float* g, float* m, float* v, int64
     M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose,
                      ((1ULL << 40) + rc - 1) / rc, ((1ULL << 40) + (uint64_t)j.cols - 1) / (uint64_t)j.cols};
   }
-  if (!presummed)
-    hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
   int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
   hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
                      grad_scale, max_norm, lr, step, beta1, beta2, eps, M);
   return lgx_hip_status("lgx_adam_clip_mirror");
-}
-
-extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
-                                    float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
-                                    float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
-                                    void* stream) {
-  return adam_clip_mirror_launch(p, g, m, v, n, partials, nparts, grad_scale, max_norm, lr, step, beta1, beta2, eps,
-                                 mirrors, nmirrors, stream, false);
-}
-
-extern "C" int lgx_adam_clip_mirror_sq(float* p, float* g, float* m, float* v, int64_t n, const float* sq,
-                                       int32_t nsq, float max_norm, const double* lr, int64_t* step, float beta1,
-                                       float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
-                                       void* stream) {
-  return adam_clip_mirror_launch(p, g, m, v, n, const_cast<float*>(sq), nsq, 1.0f, max_norm, lr, step, beta1, beta2,
-                                 eps, mirrors, nmirrors, stream, true);
 }
