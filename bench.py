@@ -78,12 +78,14 @@ def gemm_kernel_info(key, split):
 GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor and critic (235->512 with K padded "
                  "to 256, 512->256, 256->128)",
               2: "lgx_gemm_nt LGX_GEMM_DELU_COLSUM: backward dA of the hidden layers (512x256 and 256x128 weights)",
+              3: "lgx_gemm_nt LGX_GEMM_DELU: backward dA of the hidden layers (512x256 and 256x128 weights; the "
+                 "bias gradients come from lgx_gemm_tn's column sums)",
               "tn": "lgx_gemm_tn: weight gradients dW_k = dZ_k^T Y_{k-1} of the hidden layers over row slices "
                     "(512x235, 256x512, 128x256 per network)"}
 
 
 # the MFMA kernels of one iteration whose utilisation the bench line reports (PMC pass "mfma")
-MFMA_KERNELS = ["gemm_tn_x3_kernel<*>", "gemm_nt_x3p_kernel<1, *>", "gemm_nt_x3p_kernel<2, *>", "lgx_mlp_x3_kernel*",
+MFMA_KERNELS = ["gemm_tn_x3_kernel<*>", "gemm_nt_x3p_kernel<1, *>", "gemm_nt_x3p_kernel<3, *>", "lgx_mlp_x3_kernel*",
                 "lgx_post_physics_act_kernel*"]
 
 
