@@ -1,5 +1,5 @@
 """Rollout policy forward on lgx_mlp_x3_kernel (actor + critic 235->512->256->128->{12,1}, one
-launch): time per launch at 4096 / 8192 rows.  With LGX_LIB_PATH=build/clock/liblgx.so
+launch): time per launch at 4096 / 8192 rows.  With LGX_LIB_PATH=tools/_tmp/clock/liblgx.so
 (tools/phase_clock.sh) the kernel also prints wave 0's phase cycles of workgroup 0 per launch."""
 import os
 import sys
