@@ -564,6 +564,16 @@ int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream);
  * workgroup; loss->defer_finalize != 0): d std, head-bias gradients, KL, stats, adaptive LR */
 int lgx_reduce_slices_finalize(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* loss,
                                void* stream);
+/* lgx_reduce_slices (loss == NULL) / lgx_reduce_slices_finalize (loss != NULL) that also writes
+ * sq[w] = the sum of squares of the gradient values workgroup w writes (the finalize workgroup:
+ * d std and the head-bias gradients; fixed summation order), w < lgx_reduce_slices_blocks(jobs,
+ * njobs, loss != NULL); with step != NULL (needs loss) the finalize workgroup also advances the
+ * optimizer step.  The clip norm of torch's clip_grad_norm_ then needs no pass of its own over the
+ * gradient (lgx_adam_clip_mirror_sq); single-process updates (a data-parallel gradient is
+ * all-reduced after its reduction) */
+int64_t lgx_reduce_slices_blocks(const lgx_reduce_job* jobs, int32_t njobs, int32_t with_finalize);
+int lgx_reduce_slices_sq(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* loss, float* sq,
+                         int64_t* step, void* stream);
 
 /* clip_grad_norm_(max_norm) of (grad_scale * g) fused into torch-Adam (no weight decay) over
  * one flat parameter buffer; *step is advanced on the device; lr is a device double */
@@ -665,6 +675,11 @@ int lgx_split_bf16(const lgx_copy2d_job* jobs, int32_t njobs, void* stream);
 int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
                          float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1, float beta2,
                          float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors, void* stream);
+/* lgx_adam_clip_mirror on the nsq sums of squares written by lgx_reduce_slices_sq calls (the step
+ * advanced there too): no sum-of-squares launch; grad_scale 1 */
+int lgx_adam_clip_mirror_sq(float* p, float* g, float* m, float* v, int64_t n, const float* sq, int32_t nsq,
+                            float max_norm, const double* lr, int64_t* step, float beta1, float beta2, float eps,
+                            const lgx_copy2d_job* mirrors, int32_t nmirrors, void* stream);
 
 /* lgx_ppo_gather_rows into rows of dst_ld floats, columns width .. dst_ld-1 zero-filled */
 int lgx_ppo_gather_rows_padded(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width,

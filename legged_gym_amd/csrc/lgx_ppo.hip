@@ -285,7 +285,18 @@ ppo_loss_kernel(lgx_ppo_loss_args a) {
 // one workgroup: reduce the loss partials, write d std / d b4a / d b4c into the flat gradient,
 // the KL mean and the running loss sums.  Thread (g, k): value k over partial blocks g, g+8, ...
 // then a fixed-order combine of the 8 groups.
-__device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks) {   // TPB threads
+// 64-lane sum in a fixed butterfly order (every lane of the wave gets it)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+// sq (optional): the sum of squares of the gradient entries written here (d std, d b4a, d b4c) ->
+// *sq, and the optimizer step counter advanced (the clip norm's partial for
+// lgx_adam_clip_mirror_sq; lgx_reduce_slices_sq)
+__device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks, float* sq = nullptr,
+                              int64_t* step = nullptr) {   // TPB threads
   const int A = a.num_actions;
   const int NP = 2 * A + 4;               // <= 36
   __shared__ float red[8][2 * LGX_PPO_MAX_ACTIONS + 4];
@@ -306,6 +317,20 @@ __device__ void loss_finalize(const lgx_ppo_loss_args& a, int32_t nblocks) {   /
   }
   __syncthreads();
   const int t = threadIdx.x;
+  if (sq && t < 64) {   // wave 0 (NP <= 36 lanes hold values): squares of the written entries
+    float v = 0.f;
+    if (t < NP) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) s2 += red[g][t];
+      v = t < A ? s2 - a.entropy_coef / a.std[t] : t <= 2 * A ? s2 : 0.f;
+    }
+    v = wave_sum(v * v);
+    if (t == 0) {
+      *sq = v;
+      if (step) step[0] += 1;
+    }
+  }
   if (t >= NP) return;
   float s = 0.f;
 #pragma unroll
@@ -670,20 +695,15 @@ elu_bwd_colsum_kernel(float* __restrict__ dA, const float* __restrict__ Y, int64
 // Jobs whose offsets, strides and n are multiples of 4 floats (16-byte aligned: the split-K weight
 // partials) run on float4 lanes (tile_outputs < 0: -4 x 64 outputs per workgroup, 64 lanes x 4
 // slice groups), the rest on scalar lanes.
-__global__ void __launch_bounds__(TPB)
-reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin, int32_t fin_blocks) {
-  // workgroup 0: the deferred loss finalize of lgx_ppo_loss_bwd (first, so its serial partial
-  // sums overlap the reduction tiles instead of trailing them)
-  if (fin_blocks > 0 && blockIdx.x == 0) {
-    loss_finalize(fin, fin_blocks);
-    return;
-  }
-  __shared__ float red[TPB];
-  __shared__ float4 red4[TPB];
-  int b = blockIdx.x - (fin_blocks > 0 ? 1 : 0), ji = 0;
+// One reduction tile b; returns this lane's sum of squares of the outputs it wrote (wave 0's lanes
+// write).  Ends with a barrier (the LDS scratch is reused by the workgroup's next tile).
+__device__ __forceinline__ float reduce_tile(const lgx_reduce_jobs& jobs, int32_t njobs, int b, float* red,
+                                             float4* red4) {
+  int ji = 0;
   while (ji + 1 < njobs && b >= jobs.tile_start[ji + 1]) ++ji;
   const lgx_reduce_job& jb = jobs.job[ji];
   const int ot = jobs.tile_outputs[ji];
+  float q2 = 0.f;
   if (ot < 0) {   // float4 path: 64 lanes x 4 outputs per group, TPB / 64 groups over the slices
     const int groups = TPB / 64;
     const int t = threadIdx.x, oi = t % 64, g = t / 64;
@@ -710,28 +730,56 @@ reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, lgx_ppo_loss_args fin,
         sum.x += u.x; sum.y += u.y; sum.z += u.z; sum.w += u.w;
       }
       *reinterpret_cast<float4*>(jb.dst + j * jb.dst_stride + i) = sum;
+      q2 = sum.x * sum.x + sum.y * sum.y + sum.z * sum.z + sum.w * sum.w;
     }
+  } else {
+    const int groups = TPB / ot;
+    const int t = threadIdx.x, oi = t % ot, g = t / ot;
+    const int64_t o = (int64_t)(b - jobs.tile_start[ji]) * ot + oi;
+    const int64_t total = (int64_t)jb.count * jb.n;
+    float acc = 0.f;
+    int64_t j = 0, i = 0;
+    if (o < total) {
+      j = o / jb.n;
+      i = o % jb.n;
+      const float* s = jb.src + j * jb.job_stride + i;
+#pragma unroll 8
+      for (int k = g; k < jb.slices; k += groups) acc += s[(int64_t)k * jb.slice_stride];
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (g == 0 && o < total) {   // (the g == 0 lanes t < ot <= 64 are in wave 0)
+      float sum = red[oi];
+      for (int q = 1; q < groups; ++q) sum += red[q * ot + oi];
+      jb.dst[j * jb.dst_stride + i] = sum;
+      q2 = sum * sum;
+    }
+  }
+  __syncthreads();
+  return q2;
+}
+
+// Persistent over the tiles (workgroup w: tiles w, w + nwg, ...).  sq (optional): sq[workgroup] =
+// the sum of squares of every output it wrote (fixed order: tiles in order per lane, then wave 0's
+// lanes by butterfly), so the clip norm needs no pass of its own over the gradient
+__global__ void __launch_bounds__(TPB)
+reduce_slices_kernel(lgx_reduce_jobs jobs, int32_t njobs, int32_t ntiles, lgx_ppo_loss_args fin, int32_t fin_blocks,
+                     float* sq, int64_t* step) {
+  // workgroup 0: the deferred loss finalize of lgx_ppo_loss_bwd (first, so its serial partial
+  // sums overlap the reduction tiles instead of trailing them)
+  if (fin_blocks > 0 && blockIdx.x == 0) {
+    loss_finalize(fin, fin_blocks, sq, step);
     return;
   }
-  const int groups = TPB / ot;
-  const int t = threadIdx.x, oi = t % ot, g = t / ot;
-  const int64_t o = (int64_t)(b - jobs.tile_start[ji]) * ot + oi;
-  const int64_t total = (int64_t)jb.count * jb.n;
-  float acc = 0.f;
-  int64_t j = 0, i = 0;
-  if (o < total) {
-    j = o / jb.n;
-    i = o % jb.n;
-    const float* s = jb.src + j * jb.job_stride + i;
-#pragma unroll 8
-    for (int k = g; k < jb.slices; k += groups) acc += s[(int64_t)k * jb.slice_stride];
-  }
-  red[t] = acc;
-  __syncthreads();
-  if (g == 0 && o < total) {
-    float sum = red[oi];
-    for (int q = 1; q < groups; ++q) sum += red[q * ot + oi];
-    jb.dst[j * jb.dst_stride + i] = sum;
+  __shared__ float red[TPB];
+  __shared__ float4 red4[TPB];
+  const int f = fin_blocks > 0 ? 1 : 0;
+  const int nwg = (int)gridDim.x - f;
+  float q2 = 0.f;
+  for (int b = (int)blockIdx.x - f; b < ntiles; b += nwg) q2 += reduce_tile(jobs, njobs, b, red, red4);
+  if (sq && threadIdx.x < 64) {
+    q2 = wave_sum(q2);
+    if (threadIdx.x == 0) sq[blockIdx.x] = q2;
   }
 }
 
@@ -815,7 +863,14 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
   __shared__ float red[TPB];
   __shared__ float coef_s, step_size_s, bc2_sqrt_s;
   float s = 0.f;
-  for (int i = threadIdx.x; i < nparts; i += TPB) s += partials[i];
+  {   // (lgx_adam_clip_mirror_sq reads up to ~1k partials: 16-byte loads)
+    const int n4 = ((uintptr_t)partials & 15) == 0 ? nparts / 4 : 0;
+    for (int i = threadIdx.x; i < n4; i += TPB) {
+      const float4 v = reinterpret_cast<const float4*>(partials)[i];
+      s += (v.x + v.y) + (v.z + v.w);
+    }
+    for (int i = 4 * n4 + threadIdx.x; i < nparts; i += TPB) s += partials[i];
+  }
   red[threadIdx.x] = s;
   __syncthreads();
   for (int w = TPB / 2; w > 0; w >>= 1) {
@@ -1046,8 +1101,11 @@ extern "C" int lgx_elu_bwd_colsum(float* dA, const float* Y, int64_t rows, int32
   return lgx_hip_status("lgx_elu_bwd_colsum");
 }
 
+constexpr int64_t LGX_REDUCE_SQ_WGS = 512;
+
 static int reduce_slices_launch(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* fin,
-                                void* stream) {
+                                void* stream, float* sq = nullptr, int64_t* step = nullptr,
+                                int64_t* blocks_out = nullptr) {
   if (!jobs || njobs <= 0 || njobs > LGX_MAX_REDUCE_JOBS) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices: bad job count");
   lgx_reduce_jobs J;
   int64_t tiles = 0;
@@ -1071,9 +1129,35 @@ static int reduce_slices_launch(const lgx_reduce_job* jobs, int32_t njobs, const
     fin_blocks = (int32_t)((f.rows + LB_ROWS - 1) / LB_ROWS);
     tiles += 1;
   }
-  hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)tiles), dim3(TPB), 0, LGX_STREAM(stream), J, njobs, f,
-                     fin_blocks);
+  // one tile per workgroup; with sums of squares at most LGX_REDUCE_SQ_WGS persistent workgroups (the
+  // partials Adam's every workgroup re-reads stay few)
+  const int64_t ntiles = tiles - (fin ? 1 : 0);
+  const int64_t grid = (sq || blocks_out ? std::min<int64_t>(ntiles, LGX_REDUCE_SQ_WGS) : ntiles) + (fin ? 1 : 0);
+  if (blocks_out) {   // (query only: the lgx_reduce_slices_sq grid)
+    *blocks_out = grid;
+    return LGX_OK;
+  }
+  hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)grid), dim3(TPB), 0, LGX_STREAM(stream), J, njobs,
+                     (int32_t)ntiles, f, fin_blocks, sq, step);
   return lgx_hip_status("lgx_reduce_slices");
+}
+
+extern "C" int64_t lgx_reduce_slices_blocks(const lgx_reduce_job* jobs, int32_t njobs, int32_t with_finalize) {
+  lgx_ppo_loss_args f{};
+  f.rows = 1;
+  int64_t n = -1;
+  if (reduce_slices_launch(jobs, njobs, with_finalize ? &f : nullptr, nullptr, nullptr, nullptr, &n) != LGX_OK)
+    return -1;
+  return n;
+}
+
+extern "C" int lgx_reduce_slices_sq(const lgx_reduce_job* jobs, int32_t njobs, const lgx_ppo_loss_args* loss,
+                                    float* sq, int64_t* step, void* stream) {
+  if (!sq) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_sq: null sum-of-squares output");
+  if (loss && (!loss->defer_finalize || loss->rows <= 0))
+    return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_sq: loss args must be a deferred-finalize lgx_ppo_loss_bwd call's");
+  if (step && !loss) return lgx_fail(LGX_EINVAL, "lgx_reduce_slices_sq: the step advances on the finalize workgroup");
+  return reduce_slices_launch(jobs, njobs, loss, stream, sq, step);
 }
 
 extern "C" int lgx_reduce_slices(const lgx_reduce_job* jobs, int32_t njobs, void* stream) {
@@ -1100,13 +1184,15 @@ extern "C" int lgx_adam_clip(float* p, float* g, float* m, float* v, int64_t n, 
   return lgx_hip_status("lgx_adam_clip");
 }
 
-extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
-                                    float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
-                                    float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
-                                    void* stream) {
-  if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 || nparts > 1024 || nmirrors < 0 ||
-      nmirrors > MAX_MIRRORS || (nmirrors && !mirrors))
+static int adam_clip_mirror_launch(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
+                                   float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
+                                   float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
+                                   void* stream, bool presummed) {
+  if (!p || !g || !m || !v || !partials || !lr || !step || n <= 0 || nparts <= 0 ||
+      nparts > (presummed ? (1 << 20) : 1024) || nmirrors < 0 || nmirrors > MAX_MIRRORS || (nmirrors && !mirrors))
     return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror: bad args");
+  if (presummed && grad_scale != 1.0f)
+    return lgx_fail(LGX_EINVAL, "lgx_adam_clip_mirror_sq: the presummed squares are of the unscaled gradient");
   Mirrors M{};
   M.n = nmirrors;
   for (int q = 0; q < nmirrors; ++q) {
@@ -1124,9 +1210,26 @@ extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int6
     M.mj[q] = Mirror{off, j.dst_ld, j.dst_bs, j.dst, (int32_t)count, j.rows, j.cols, j.transpose,
                      ((1ULL << 40) + rc - 1) / rc, ((1ULL << 40) + (uint64_t)j.cols - 1) / (uint64_t)j.cols};
   }
-  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
+  if (!presummed)
+    hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(TPB), 0, LGX_STREAM(stream), g, n, grad_scale, partials, step);
   int blocks = (int)std::min<int64_t>((n + TPB - 1) / TPB, 1024);
   hipLaunchKernelGGL(adam_clip_kernel, dim3(blocks), dim3(TPB), 0, LGX_STREAM(stream), p, g, m, v, n, partials, nparts,
                      grad_scale, max_norm, lr, step, beta1, beta2, eps, M);
   return lgx_hip_status("lgx_adam_clip_mirror");
+}
+
+extern "C" int lgx_adam_clip_mirror(float* p, float* g, float* m, float* v, int64_t n, float* partials, int32_t nparts,
+                                    float grad_scale, float max_norm, const double* lr, int64_t* step, float beta1,
+                                    float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
+                                    void* stream) {
+  return adam_clip_mirror_launch(p, g, m, v, n, partials, nparts, grad_scale, max_norm, lr, step, beta1, beta2, eps,
+                                 mirrors, nmirrors, stream, false);
+}
+
+extern "C" int lgx_adam_clip_mirror_sq(float* p, float* g, float* m, float* v, int64_t n, const float* sq,
+                                       int32_t nsq, float max_norm, const double* lr, int64_t* step, float beta1,
+                                       float beta2, float eps, const lgx_copy2d_job* mirrors, int32_t nmirrors,
+                                       void* stream) {
+  return adam_clip_mirror_launch(p, g, m, v, n, const_cast<float*>(sq), nsq, 1.0f, max_norm, lr, step, beta1, beta2,
+                                 eps, mirrors, nmirrors, stream, true);
 }

@@ -542,6 +542,17 @@ class FusedPPOUpdate:
         # or from launches on the main stream before the side stream's first join (loss): the
         # early reduction then needs no join after the dA GEMMs
         self.rest_on_side = all(k in colsum for k in range(1, self.L - 1))
+        # the clip norm's sums of squares written by the reduction launches themselves
+        # (lgx_reduce_slices_sq; single-process updates with the fused loss): one launch less per minibatch
+        self.fused_sq = self.lgx_gemm and self.loss_bwd and os.environ.get("LGX_PPO_FUSED_SQ", "1") != "0"
+        if self.fused_sq:
+            blocks = self.lib.lgx_reduce_slices_blocks
+            self.nsq_rest = int(blocks(self.jobs_rest, len(self.jobs_rest), 1)) if len(self.jobs_rest) else 0
+            self.nsq_dw1 = int(blocks(self.jobs_dw1, len(self.jobs_dw1), 0))
+            self.nsq_all = int(blocks(self.jobs, self.njobs, 1))
+            if min(self.nsq_rest, self.nsq_dw1, self.nsq_all) < 0:
+                raise RuntimeError("lgx_reduce_slices_blocks failed")
+            self.sq_parts = torch.zeros(max(self.nsq_rest + self.nsq_dw1, self.nsq_all, 1), device=self.dev)
 
     # ------------------------------------------------------------------ update
     @torch.no_grad()
@@ -918,14 +929,22 @@ class FusedPPOUpdate:
             dZ = self.D[k - 1]
         early = (side_used and self.loss_bwd and len(self.jobs_rest) > 0
                  and os.environ.get("LGX_PPO_EARLY_REDUCE", "1") != "0")
+        use_sq = self.fused_sq and apply and ppo.dist is None
+        step_p = _vp(self.optimizer.step_dev) if use_sq else None
+        sq = self.sq_parts.data_ptr() if use_sq else 0
+        nsq = 0
         if early:
             # every gradient block but dW1's is complete once dA_1 (this stream) and the side
             # stream's dW GEMMs are: reduce them (+ the loss finalize) on the side stream while dW1
             # runs here - the memory-bound reduction next to the MFMA-bound GEMM
             if not self.rest_on_side:   # (skipping the join when possible: 10.478 -> 10.468 ms per update)
                 self._join(torch.cuda.current_stream(self.dev), self._side, 0)
-            chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
-                                               C.c_void_p(self._side.cuda_stream)), "reduce")
+            if use_sq:
+                chk(lib.lgx_reduce_slices_sq(self.jobs_rest, len(self.jobs_rest), C.byref(args), C.c_void_p(sq), step_p,
+                                             C.c_void_p(self._side.cuda_stream)), "reduce")
+            else:
+                chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
+                                                   C.c_void_p(self._side.cuda_stream)), "reduce")
         bucketed = early and apply and ppo.dist is not None
         self.bucketed = bucketed
         if bucketed:
@@ -952,10 +971,18 @@ class FusedPPOUpdate:
         if side_used and not early:   # the weight gradients are complete before the reduction reads them
             self._join(self._side, torch.cuda.current_stream(self.dev), L)
         if early:   # (dW1's partials come from this stream; the side stream's blocks are joined below)
-            chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
+            if use_sq:
+                chk(lib.lgx_reduce_slices_sq(self.jobs_dw1, len(self.jobs_dw1), None, C.c_void_p(sq + 4 * self.nsq_rest),
+                                             None, stream), "reduce")
+                nsq = self.nsq_rest + self.nsq_dw1
+            else:
+                chk(lib.lgx_reduce_slices(self.jobs_dw1, len(self.jobs_dw1), stream), "reduce")
             if bucketed:
                 self._all_reduce(self.g_comm[:self.nW1], torch.cuda.current_stream(self.dev))
             self._join(self._side, torch.cuda.current_stream(self.dev), L)
+        elif self.loss_bwd and use_sq:
+            chk(lib.lgx_reduce_slices_sq(self.jobs, self.njobs, C.byref(args), C.c_void_p(sq), step_p, stream), "reduce")
+            nsq = self.nsq_all
         elif self.loss_bwd:
             chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
         else:
@@ -975,7 +1002,11 @@ class FusedPPOUpdate:
                 chk(lib.lgx_ppo_adapt_lr(C.c_void_p(self.g_comm.data_ptr() + 4 * self.n), grad_scale,
                                          _vp(self.optimizer.lr_dev), ppo.desired_kl, stream), "adapt_lr")
         o = self.optimizer
-        if fused:   # the step also refreshes the GEMM weight copies (padded W1, transposed W2..)
+        if fused and nsq:   # (norm from the reductions' sums of squares; step advanced there)
+            chk(lib.lgx_adam_clip_mirror_sq(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n, C.c_void_p(sq),
+                                            nsq, ppo.max_grad_norm, _vp(o.lr_dev), _vp(o.step_dev), o.betas[0],
+                                            o.betas[1], o.eps, self.copy_jobs, len(self.copy_jobs), stream), "adam")
+        elif fused:   # the step also refreshes the GEMM weight copies (padded W1, transposed W2..)
             chk(lib.lgx_adam_clip_mirror(_vp(self.flat_p), _vp(self.flat_g), _vp(o.m), _vp(o.v), self.n,
                                          _vp(self.norm_parts), self.norm_parts.numel(), grad_scale, ppo.max_grad_norm,
                                          _vp(o.lr_dev), _vp(o.step_dev), o.betas[0], o.betas[1], o.eps, self.copy_jobs,

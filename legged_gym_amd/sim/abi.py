@@ -209,6 +209,8 @@ def declare(lib, prefix="lgx"):
             "elu_bwd_colsum": (C.c_int, [vp, vp, i64, i32, i32, vp, vp]),
             "reduce_slices": (C.c_int, [C.POINTER(LgxReduceJob), i32, vp]),
             "reduce_slices_finalize": (C.c_int, [C.POINTER(LgxReduceJob), i32, C.POINTER(LgxPpoLossArgs), vp]),
+            "reduce_slices_blocks": (i64, [C.POINTER(LgxReduceJob), i32, i32]),
+            "reduce_slices_sq": (C.c_int, [C.POINTER(LgxReduceJob), i32, C.POINTER(LgxPpoLossArgs), vp, vp, vp]),
             "ppo_loss_bwd_layout": (C.c_int, [i64, i32, i32, C.POINTER(i64)]),
             "ppo_loss_bwd": (C.c_int, [C.POINTER(LgxPpoLossArgs), vp, vp]),
             "mlp_x3_weight_elems": (i64, [i32, i32]),
@@ -228,6 +230,8 @@ def declare(lib, prefix="lgx"):
                                     C.c_float, C.c_float, vp]),
             "adam_clip_mirror": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, C.c_float, vp, vp, C.c_float,
                                            C.c_float, C.c_float, C.POINTER(LgxCopy2dJob), i32, vp]),
+            "adam_clip_mirror_sq": (C.c_int, [vp, vp, vp, vp, i64, vp, i32, C.c_float, vp, vp, C.c_float,
+                                              C.c_float, C.c_float, C.POINTER(LgxCopy2dJob), i32, vp]),
             "event_create": (C.c_int, [C.POINTER(vp)]),
             "event_destroy": (C.c_int, [vp]),
             "event_record": (C.c_int, [vp, vp]),
@@ -246,7 +250,7 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trim
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",
             "lgx_head_bwd_partials_floats", "lgx_head_bwd", "lgx_head_bwd_finalize", "lgx_colsum_partials_floats", "lgx_elu_bwd_colsum",
-            "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_ppo_act", "lgx_ppo_store", "lgx_ppo_act_store",
+            "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_adam_clip_mirror_sq", "lgx_reduce_slices_blocks", "lgx_reduce_slices_sq", "lgx_ppo_act", "lgx_ppo_store", "lgx_ppo_act_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
             "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward",

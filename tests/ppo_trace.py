@@ -20,11 +20,12 @@ class _LibSpy:
 
     def __getattr__(self, name):
         fn = getattr(self._lib, name)
-        if name not in ("lgx_adam_clip", "lgx_adam_clip_mirror"):
+        if name not in ("lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_adam_clip_mirror_sq"):
             return fn
 
         def wrapped(*args):
-            grad_scale = float(args[7].value if hasattr(args[7], "value") else args[7])
+            # (the _sq entry takes the reductions' sums of squares and no grad_scale: 1)
+            grad_scale = 1.0 if name.endswith("_sq") else float(args[7].value if hasattr(args[7], "value") else args[7])
             self._sink.append((self._fused.flat_g.clone(), grad_scale))
             return fn(*args)
         return wrapped

@@ -120,11 +120,44 @@ def test_fused_update_single_stream(gpu, monkeypatch):
     assert getattr(fus._fused, "_side", None) is None
 
 
-@pytest.mark.parametrize("var,val", [("LGX_PPO_TN_COLSUM", "0"), ("LGX_PPO_DEV_EVENTS", "0")])
+def test_reduce_slices_sum_of_squares(gpu):
+    """lgx_reduce_slices_sq: the slice sums as lgx_reduce_slices, and per workgroup the sum of squares
+    of what it wrote (float4 and scalar jobs), which together give the gradient's squared norm."""
+    import ctypes as C
+    from legged_gym_amd.sim import abi
+    from legged_gym_amd.sim import lib as lgxlib
+    lib = lgxlib.load()
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    S, n1, n2 = 16, 4096 + 256, 1001
+    src1 = torch.randn(S, n1, device="cuda:0", generator=g)
+    src2 = torch.randn(S, n2, device="cuda:0", generator=g)
+    dst = torch.zeros(n1 + n2 + 4, device="cuda:0")
+    jobs = (abi.LgxReduceJob * 2)()
+    for j, (src, off, n) in enumerate(((src1, 0, n1), (src2, n1 + 4, n2))):
+        jobs[j].src, jobs[j].dst = src.data_ptr(), dst.data_ptr() + 4 * off
+        jobs[j].n, jobs[j].count, jobs[j].job_stride, jobs[j].slices = n, 1, 0, S
+        jobs[j].slice_stride, jobs[j].dst_stride = n, 0
+    nb = int(lib.lgx_reduce_slices_blocks(jobs, 2, 0))
+    assert nb > 2
+    sq = torch.full((nb + 1,), -1.0, device="cuda:0")
+    stream = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    lgxlib.check(lib.lgx_reduce_slices_sq(jobs, 2, None, C.c_void_p(sq.data_ptr()), None, stream), "reduce_sq")
+    torch.cuda.synchronize()
+    ref1, ref2 = src1.sum(0), src2.sum(0)
+    assert torch.allclose(dst[:n1], ref1, atol=1e-5) and torch.allclose(dst[n1 + 4:], ref2, atol=1e-5)
+    assert (sq[:nb] >= 0).all() and sq[nb].item() == -1.0   # every workgroup wrote its entry, no more
+    want = float((dst.double() ** 2).sum())
+    assert abs(float(sq[:nb].double().sum()) - want) <= 1e-5 * want
+    assert lib.lgx_reduce_slices_sq(jobs, 2, None, None, None, stream) != 0   # (null output refused)
+
+
+@pytest.mark.parametrize("var,val", [("LGX_PPO_TN_COLSUM", "0"), ("LGX_PPO_DEV_EVENTS", "0"),
+                                     ("LGX_PPO_FUSED_SQ", "0")])
 def test_fused_update_ab_variants(gpu, monkeypatch, var, val):
     """The update's variants against autograd: the hidden-layer bias gradients from the dA GEMMs'
-    ELU' + column-sum epilogue instead of lgx_gemm_tn's column sums (LGX_PPO_TN_COLSUM=0), and torch
-    events for the cross-stream joins (LGX_PPO_DEV_EVENTS=0)."""
+    ELU' + column-sum epilogue instead of lgx_gemm_tn's column sums (LGX_PPO_TN_COLSUM=0), torch
+    events for the cross-stream joins (LGX_PPO_DEV_EVENTS=0), and the clip norm from its own
+    sum-of-squares launch instead of the reductions' (LGX_PPO_FUSED_SQ=0)."""
     monkeypatch.setenv(var, val)
     ref, fus = make_pair()
     torch.manual_seed(11)
