@@ -468,6 +468,15 @@ int lgx_ppo_store(const lgx_ppo_store_args* args, void* stream);
  * PPO.act + PPO.process_env_step of the runner's collection loop; the store reads only step t's
  * env outputs and storage row t, which the act does not touch); same envs. */
 int lgx_ppo_act_store(const lgx_ppo_act_args* args, const lgx_ppo_store_args* prev, void* stream);
+/* The rollout step's policy inference and lgx_ppo_act_store in ONE launch (rsl_rl PPO.act:
+ * ActorCritic.act + evaluate + RolloutStorage.add_transitions, and process_env_step of the previous
+ * step): lgx_mlp_x3_forward of descs[0] (actor, output = the action means into descs[0].y) and
+ * descs[1] (critic, output = the storage values row) with lgx_ppo_act's arithmetic done in the
+ * actor's last-layer epilogue; bit-identical rows to lgx_mlp_x3_forward + lgx_ppo_act(_store).
+ * count == 2, rows == args->num_envs, num_actions <= LGX_PPO_MAX_ACTIONS, args->value NULL, args->mu
+ * unused (the means come from the epilogue); prev NULL: no store. */
+int lgx_mlp_x3_forward_act(const lgx_mlp_x3_desc* descs, int32_t count, const lgx_ppo_act_args* args,
+                           const lgx_ppo_store_args* prev, void* stream);
 
 /* dst[r, :] = src[idx[r], :] for r < rows (minibatch gather of storage rows) */
 int lgx_ppo_gather_rows(const float* src, float* dst, const int64_t* idx, int64_t rows, int32_t width, void* stream);

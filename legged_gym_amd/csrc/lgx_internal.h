@@ -113,4 +113,18 @@ struct lgx_reduce_jobs {
 // with the operand splits for the MFMA issue gaps (measured: layer-1 forward 54 -> 61 us with
 // an expm1-accurate polynomial form).
 __device__ __forceinline__ float lgx_elu(float x) { return x > 0.f ? x : __expf(x) - 1.f; }
+// Normal(mu, sd).sample() from a standard-normal draw (torch.normal = normal_(0, 1) * std + mu) and
+// the log-prob term of one action dimension (Normal.log_prob); shared by lgx_ppo_act and the
+// rollout MLP's fused act epilogue so both write bit-identical rows.  Explicit fma, no contraction.
+__device__ __forceinline__ float lgx_ppo_sample(float mu, float sd, float eps) { return __builtin_fmaf(sd, eps, mu); }
+__device__ __forceinline__ float lgx_ppo_logp_term(float d, float sd) {
+#pragma clang fp contract(off)
+  const float half_log_2pi = 0.91893853320467274178f;
+  return -(d * d) / (2.f * sd * sd) - logf(sd) - half_log_2pi;
+}
+// PPO.process_env_step's time-out bootstrap: rew + gamma * (V * time_out), as torch evaluates it
+__device__ __forceinline__ float lgx_ppo_reward(float rew, float gamma, float value, bool time_out) {
+#pragma clang fp contract(off)
+  return rew + gamma * (value * (time_out ? 1.f : 0.f));
+}
 #endif

@@ -38,6 +38,8 @@ constexpr int XM_NT = 64 * XM_NW;
 constexpr int XM_MAXL = 6;
 constexpr int XM_MAXW = 512;
 constexpr int XM_LDS_MAX = 160 * 1024;
+constexpr int XM_ACT_A = 16;        // act epilogue: action columns per row in LDS (LGX_PPO_MAX_ACTIONS)
+constexpr int XM_ACT_LDS = (2 * XM_BM * XM_ACT_A + XM_ACT_A) * 4;   // means, draws (then log-prob terms), std
 
 __host__ __device__ inline int xm_kp(int k) { return (k + 63) & ~63; }         // padded width (image / weight K)
 __host__ __device__ inline int xm_rs(int k) { return xm_kp(k) * 2 + 16; }       // image row stride, bytes
@@ -57,6 +59,16 @@ struct XmBatch {
   XmNet m[2];
   int32_t region;   // byte offset of the second image region (the first at 0)
   int32_t bias_region;   // byte offset of the biases (each layer's zero-padded to 32 columns)
+  int32_t act_region;    // byte offset of the act epilogue's rows (lgx_mlp_x3_forward_act)
+};
+// rsl_rl PPO.act + RolloutStorage.add_transitions (+ the previous step's process_env_step) fused
+// into the rollout launch (lgx_mlp_x3_forward_act): the actor's wave 0 finishes its rows in the last
+// layer's epilogue (lgx_ppo_act's arithmetic, the same helpers); the waves a late layer leaves idle
+// copy the observation rows into storage (actor) and the critic rows + the store (critic)
+struct XmAct {
+  lgx_ppo_act_args a;
+  lgx_ppo_store_args s;
+  int32_t store;
 };
 
 // three RNE bf16 limbs of two floats, packed (low half = first element); both subtractions exact
@@ -160,7 +172,8 @@ __device__ __forceinline__ void xm_layer(const char* __restrict__ img, int rs, c
   }
 }
 
-__global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_t count) {
+template <bool ACT>
+__global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_t count, XmAct xa) {
   extern __shared__ __attribute__((aligned(16))) char xm_lds[];
   // two networks: XCDs 0-3 (workgroup id % 8) run the first, 4-7 the second, so each XCD's L2
   // holds one network's weight limbs (1.7 MB) instead of both
@@ -174,6 +187,20 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
   char* const img0 = xm_lds;
   char* const img1 = xm_lds + batch.region;
   float* const bias_lds = reinterpret_cast<float*>(xm_lds + batch.bias_region);
+  float* const act_lds = reinterpret_cast<float*>(xm_lds + batch.act_region);   // [32][16] means
+  float* const eps_lds = act_lds + XM_BM * XM_ACT_A;                             // [32][16] draws
+  float* const sd_lds = eps_lds + XM_BM * XM_ACT_A;                              // [16] std
+  if constexpr (ACT) {   // the act epilogue's draws and std, staged with the input rows (clamped loads)
+    static_assert(XM_BM * XM_ACT_A <= XM_NT, "one draw per thread");
+    if (net == 0) {
+      const int A = (int)xa.a.num_actions, rr = tid / XM_ACT_A, c = tid % XM_ACT_A;
+      const int64_t gr = std::min<int64_t>(r0 + rr, a.rows - 1);
+      const float e = xa.a.noise[gr * A + std::min(c, A - 1)];
+      const float sd = xa.a.std[std::min(c, A - 1)];
+      eps_lds[tid] = e;
+      if (tid < XM_ACT_A) sd_lds[tid] = sd;
+    }
+  }
   LGX_CLK_DECL(8)
   bf16x8 pre[XM_PF];   // the next layer's first weight load group (xm_prefetch)
   xm_prefetch(pre, a, 0, wave, lane);
@@ -193,6 +220,7 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
   {
     constexpr int XM_SU = 8;
     const int K0 = a.dims[0], rs = xm_rs(K0), pairs = xm_kp(K0) / 2, total = XM_BM * pairs;
+    float* const st_rows = !ACT ? nullptr : net == 0 ? xa.a.st_obs : xa.a.st_cobs;   // (the inputs, host-checked)
     for (int base = 0; base < total; base += XM_SU * XM_NT) {
       float v[XM_SU][2];
 #pragma unroll
@@ -206,6 +234,12 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
         const float x0 = a.x[gc + std::min(k, K0 - 1)], x1 = a.x[gc + std::min(k + 1, K0 - 1)];
         v[u][0] = in && k < K0 ? x0 : 0.f;
         v[u][1] = in && k + 1 < K0 ? x1 : 0.f;
+        if constexpr (ACT) {   // RolloutStorage.add_transitions: the observation rows (actor) / the
+          if (st_rows && in) {  // critic's rows (privileged observations) into storage row t
+            if (k < K0) st_rows[gr * K0 + k] = x0;
+            if (k + 1 < K0) st_rows[gr * K0 + k + 1] = x1;
+          }
+        }
       }
 #pragma unroll
       for (int u = 0; u < XM_SU; ++u) {
@@ -282,6 +316,8 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
             for (int i = 0; i < 4; ++i)
               if (c0 + i < N) a.y[gr * N + c0 + i] = v[i];
           }
+          if (ACT && net == 0 && c0 < XM_ACT_A)   // the means for the act epilogue
+            *reinterpret_cast<float4*>(act_lds + row * XM_ACT_A + c0) = make_float4(v[0], v[1], v[2], v[3]);
         }
       }
     }
@@ -297,6 +333,39 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
     LGX_CLK(5);
     __syncthreads();   // the output image is complete; the input region is free for the next layer
     LGX_CLK(6);
+  }
+  if constexpr (ACT) {
+    const XmAct* xp = &xa;
+    if (net == 1 && xp->store && tid < XM_BM && r0 + tid < a.rows) {   // the previous step's process_env_step rows
+      const lgx_ppo_store_args& ps = xp->s;
+      const int64_t n = r0 + tid;
+      ps.st_rew[n] = ps.time_outs ? lgx_ppo_reward(ps.rew[n], ps.gamma, ps.st_values[n], ps.time_outs[n] != 0)
+                                  : ps.rew[n];
+      ps.st_dones[n] = ps.reset[n] ? 1 : 0;
+    }
+    // lgx_ppo_act's arithmetic on the actor's rows (ppo_act_kernel: one thread per (env, action),
+    // then the log-prob summed per env in action order) from the means / draws / std in LDS
+    if (net == 0) {
+      const lgx_ppo_act_args& p = xp->a;
+      const int A = (int)p.num_actions, nr = (int)std::min<int64_t>(XM_BM, a.rows - r0);
+      const int rr = tid / XM_ACT_A, c = tid % XM_ACT_A;
+      if (rr < nr && c < A) {
+        const int64_t e = (r0 + rr) * A + c;
+        const float mu = act_lds[tid], sd = sd_lds[c];
+        const float act = lgx_ppo_sample(mu, sd, eps_lds[tid]);
+        p.actions_out[e] = act;
+        p.st_actions[e] = act;
+        p.st_mu[e] = mu;
+        p.st_sigma[e] = sd;
+        eps_lds[tid] = lgx_ppo_logp_term(act - mu, sd);
+      }
+      __syncthreads();
+      if (tid < nr) {
+        float logp = 0.f;
+        for (int j = 0; j < A; ++j) logp += eps_lds[tid * XM_ACT_A + j];
+        p.st_logp[r0 + tid] = logp;
+      }
+    }
   }
   LGX_CLK_PRINT("mlp_x3", 7)
 }
@@ -336,7 +405,8 @@ __device__ __forceinline__ void xm_split_one(const float* __restrict__ W, int N,
   d[512] = l2;
 }
 
-int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region, int32_t* bias_region = nullptr) {
+int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region, int32_t* bias_region = nullptr,
+                  int32_t* act_region = nullptr, bool act = false) {
   int64_t r0 = 0, r1 = 0, rb = 0;
   for (int i = 0; i < count; ++i) {
     const lgx_mlp_x3_desc& m = d[i];
@@ -354,7 +424,9 @@ int64_t lds_bytes(const lgx_mlp_x3_desc* d, int32_t count, int32_t* region, int3
   }
   if (region) *region = (int32_t)r0;
   if (bias_region) *bias_region = (int32_t)(r0 + r1);
-  return r0 + r1 + rb <= XM_LDS_MAX ? r0 + r1 + rb : -1;
+  if (act_region) *act_region = (int32_t)(r0 + r1 + rb);
+  const int64_t total = r0 + r1 + rb + (act ? XM_ACT_LDS : 0);
+  return total <= XM_LDS_MAX ? total : -1;
 }
 
 }  // namespace
@@ -394,10 +466,11 @@ extern "C" int64_t lgx_mlp_x3_lds_bytes(const lgx_mlp_x3_desc* d, int32_t count)
   return lds_bytes(d, count, nullptr);
 }
 
-extern "C" int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* d, int32_t count, void* stream) {
+namespace {
+int mlp_x3_launch(const lgx_mlp_x3_desc* d, int32_t count, const XmAct* xa, void* stream) {
   if (!d || count < 1 || count > 2) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: count must be 1 or 2");
   XmBatch b{};
-  const int64_t lds = lds_bytes(d, count, &b.region, &b.bias_region);
+  const int64_t lds = lds_bytes(d, count, &b.region, &b.bias_region, &b.act_region, xa != nullptr);
   if (lds < 0) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: bad dims or activations exceed the LDS (160 KB)");
   int64_t rows = 0;
   for (int i = 0; i < count; ++i) {
@@ -420,13 +493,55 @@ extern "C" int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* d, int32_t count, void*
     rows = std::max(rows, m.rows);
   }
   if (rows == 0) return LGX_OK;
-  static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&lgx_mlp_x3_kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, XM_LDS_MAX) == hipSuccess;
+  static const bool attr =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&lgx_mlp_x3_kernel<false>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, XM_LDS_MAX) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&lgx_mlp_x3_kernel<true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, XM_LDS_MAX) == hipSuccess;
   if (!attr) return lgx_fail(LGX_EHIP, "lgx_mlp_x3_forward: hipFuncSetAttribute (dynamic LDS) failed");
   const int64_t tiles = (rows + XM_BM - 1) / XM_BM;
   const int64_t grid = count == 2 ? 8 * ((tiles + 3) / 4) : tiles;
   if (grid >= (1ll << 31)) return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward: too many rows");
-  LGX_LAUNCH(lgx_mlp_x3_kernel, dim3((unsigned)grid), dim3(XM_NT), (size_t)lds, reinterpret_cast<hipStream_t>(stream), b,
-             count);
-  return lgx_hip_status("lgx_mlp_x3_forward");
+  if (xa) {
+    LGX_LAUNCH(lgx_mlp_x3_kernel<true>, dim3((unsigned)grid), dim3(XM_NT), (size_t)lds,
+               reinterpret_cast<hipStream_t>(stream), b, count, *xa);
+  } else {
+    LGX_LAUNCH(lgx_mlp_x3_kernel<false>, dim3((unsigned)grid), dim3(XM_NT), (size_t)lds,
+               reinterpret_cast<hipStream_t>(stream), b, count, XmAct{});
+  }
+  return lgx_hip_status(xa ? "lgx_mlp_x3_forward_act" : "lgx_mlp_x3_forward");
+}
+}  // namespace
+
+extern "C" int lgx_mlp_x3_forward(const lgx_mlp_x3_desc* d, int32_t count, void* stream) {
+  return mlp_x3_launch(d, count, nullptr, stream);
+}
+
+extern "C" int lgx_mlp_x3_forward_act(const lgx_mlp_x3_desc* d, int32_t count, const lgx_ppo_act_args* act,
+                                      const lgx_ppo_store_args* prev, void* stream) {
+  if (!d || count != 2 || !act)
+    return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward_act: needs the actor and critic descriptors and act args");
+  const lgx_ppo_act_args& p = *act;
+  const lgx_mlp_x3_desc &ad = d[0], &cd = d[1];
+  if (ad.nl < 1 || ad.nl > XM_MAXL || cd.nl < 1 || cd.nl > XM_MAXL)
+    return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward_act: bad layer count");
+  if (p.num_envs <= 0 || p.num_envs != ad.rows || p.num_envs != cd.rows || p.num_actions < 1 ||
+      p.num_actions > LGX_PPO_MAX_ACTIONS || ad.dims[ad.nl] != p.num_actions || cd.dims[cd.nl] != 1 ||
+      p.num_obs <= 0 || !p.std || !p.noise || !p.obs || !p.actions_out || !p.st_obs || !p.st_actions || p.value ||
+      !p.st_logp || !p.st_mu || !p.st_sigma || ((p.cobs != nullptr) != (p.st_cobs != nullptr)) ||
+      (p.cobs && p.num_cobs <= 0))
+    return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward_act: bad act args (rows = envs, actor output = actions <= 16, "
+                                "critic output 1, value NULL: the critic writes its storage row)");
+  if (p.obs != ad.x || (p.cobs && p.cobs != cd.x) || p.num_obs != ad.dims[0] || (p.cobs && p.num_cobs != cd.dims[0]))
+    return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward_act: args->obs / cobs must be the actor / critic inputs");
+  XmAct xa{};
+  xa.a = p;
+  if (prev) {
+    const lgx_ppo_store_args& s = *prev;
+    if (s.num_envs != p.num_envs || !s.rew || !s.reset || !s.st_values || !s.st_rew || !s.st_dones)
+      return lgx_fail(LGX_EINVAL, "lgx_mlp_x3_forward_act: bad store args (the store must cover the same envs)");
+    xa.s = s;
+    xa.store = 1;
+  }
+  return mlp_x3_launch(d, count, &xa, stream);
 }

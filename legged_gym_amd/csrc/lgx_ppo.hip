@@ -82,9 +82,7 @@ ppo_act_kernel(lgx_ppo_act_args a, lgx_ppo_store_args ps) {
   const int64_t nn = min((int64_t)ACT_ENVS, a.num_envs - n0);
   if (STORE && threadIdx.x < nn) {
     const int64_t n = n0 + threadIdx.x;
-    float r = ps.rew[n];
-    if (ps.time_outs) r += ps.gamma * (ps.st_values[n] * (ps.time_outs[n] ? 1.f : 0.f));
-    ps.st_rew[n] = r;
+    ps.st_rew[n] = ps.time_outs ? lgx_ppo_reward(ps.rew[n], ps.gamma, ps.st_values[n], ps.time_outs[n] != 0) : ps.rew[n];
     ps.st_dones[n] = ps.reset[n] ? 1 : 0;
   }
   copy_rows(a.obs + n0 * a.num_obs, a.st_obs + n0 * a.num_obs, nn * a.num_obs);
@@ -95,7 +93,7 @@ ppo_act_kernel(lgx_ppo_act_args a, lgx_ppo_store_args ps) {
     const int j = (int)(k % A);
     const float sd = a.std[j];
     const float mu = a.mu[e];
-    const float act = mu + sd * a.noise[e];
+    const float act = lgx_ppo_sample(mu, sd, a.noise[e]);
     a.actions_out[e] = act;
     a.st_actions[e] = act;
     a.st_mu[e] = mu;
@@ -104,13 +102,8 @@ ppo_act_kernel(lgx_ppo_act_args a, lgx_ppo_store_args ps) {
   __syncthreads();
   if (threadIdx.x < nn) {
     const int64_t n = n0 + threadIdx.x;
-    const float half_log_2pi = 0.91893853320467274178f;
     float logp = 0.f;
-    for (int j = 0; j < A; ++j) {
-      float sd = a.std[j];
-      float d = a.st_actions[n * A + j] - a.mu[n * A + j];
-      logp += -(d * d) / (2.f * sd * sd) - logf(sd) - half_log_2pi;
-    }
+    for (int j = 0; j < A; ++j) logp += lgx_ppo_logp_term(a.st_actions[n * A + j] - a.mu[n * A + j], a.std[j]);
     a.st_logp[n] = logp;
     if (a.value) a.st_values[n] = a.value[n];
   }
@@ -121,9 +114,7 @@ __global__ void __launch_bounds__(TPB)
 ppo_store_kernel(lgx_ppo_store_args a) {
   const int64_t n = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (n >= a.num_envs) return;
-  float r = a.rew[n];
-  if (a.time_outs) r += a.gamma * (a.st_values[n] * (a.time_outs[n] ? 1.f : 0.f));
-  a.st_rew[n] = r;
+  a.st_rew[n] = a.time_outs ? lgx_ppo_reward(a.rew[n], a.gamma, a.st_values[n], a.time_outs[n] != 0) : a.rew[n];
   a.st_dones[n] = a.reset[n] ? 1 : 0;
 }
 

@@ -93,8 +93,11 @@ class PPO:
                 and self.storage.step < self.storage.num_transitions_per_env)
 
     def _act_fused(self, obs, critic_obs):
-        """act() + add_transitions' row writes in two launches: the rollout MLP (actor and critic
-        in one launch; the critic writes its storage row directly) and lgx_ppo_act."""
+        """act() + add_transitions' row writes (+ the deferred process_env_step store of the previous
+        step) in ONE launch: lgx_mlp_x3_forward_act runs the actor and critic MLPs and lgx_ppo_act's
+        arithmetic in the actor's last-layer epilogue (the critic writes its storage row directly).
+        LGX_FUSED_ACT=0, or a network pair the fused launch does not take: the MLP launch, then
+        lgx_ppo_act(_store) - bit-identical rows either way."""
         ac = self.actor_critic
         if not (ac._fused_ok(obs, ac._fused_actor) and ac._fused_critic.ok):
             return None
@@ -107,7 +110,6 @@ class PPO:
             self._mean_buf = torch.empty(obs.shape[0], A, device=obs.device)
         mean = self._mean_buf
         descs = make_descs([(ac._fused_actor, obs, mean), (ac._fused_critic, critic_obs, st.values[s])])
-        launch_forward(descs, 2, C.c_void_p(main.cuda_stream))   # actor and critic in one launch
         if getattr(self, "_act_out", None) is None or self._act_out.shape != mean.shape:
             self._act_out = torch.empty_like(mean)
         # Normal.sample's standard-normal draws from torch's generator.  Default: one [N, A] draw
@@ -126,10 +128,8 @@ class PPO:
         a = abi.LgxPpoActArgs()
         a.num_envs, a.num_actions, a.num_obs = mean.shape[0], mean.shape[1], obs.shape[1]
         a.mu, a.value, a.std, a.noise = mean.data_ptr(), None, self.actor_critic.std.data_ptr(), noise.data_ptr()
-        obs = obs.contiguous()
         a.obs = obs.data_ptr()
         if st.privileged_observations is not None:
-            critic_obs = critic_obs.contiguous()
             a.num_cobs, a.cobs, a.st_cobs = critic_obs.shape[1], critic_obs.data_ptr(), \
                 st.privileged_observations[s].data_ptr()
         a.actions_out = self._act_out.data_ptr()
@@ -137,14 +137,27 @@ class PPO:
             st.values[s].data_ptr()
         a.st_logp, a.st_mu, a.st_sigma = st.actions_log_prob[s].data_ptr(), st.mu[s].data_ptr(), st.sigma[s].data_ptr()
         lib = self._fused.lib
-        stream = C.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)
+        stream = C.c_void_p(main.cuda_stream)
         pend = getattr(self, "_pending_store", None)
-        if pend is not None and pend[0].num_envs == a.num_envs:   # the previous step's store rides along
-            self._pending_store = None
-            self._fused.check(lib.lgx_ppo_act_store(C.byref(a), C.byref(pend[0]), stream), "lgx_ppo_act_store")
-        else:
+        prev = pend[0] if pend is not None and pend[0].num_envs == a.num_envs else None
+        if prev is None:
             self.flush_store()
-            self._fused.check(lib.lgx_ppo_act(C.byref(a), stream), "lgx_ppo_act")
+        fused = (isinstance(descs[0], abi.LgxMlpX3Desc) and not getattr(self, "_fused_act_off", False)
+                 and os.environ.get("LGX_FUSED_ACT", "1") != "0")
+        if fused and lib.lgx_mlp_x3_forward_act(descs, 2, C.byref(a), C.byref(prev) if prev is not None else None,
+                                                stream) != 0:
+            # (validated before any launch) a pair the fused launch does not take, e.g. the act
+            # rows past the LDS: the two-launch form from now on
+            self._fused_act_off = fused = False
+        if not fused:
+            launch_forward(descs, 2, stream)   # actor and critic in one launch
+            if prev is not None:   # the previous step's store rides along
+                self._fused.check(lib.lgx_ppo_act_store(C.byref(a), C.byref(prev), stream), "lgx_ppo_act_store")
+            else:
+                self._fused.check(lib.lgx_ppo_act(C.byref(a), stream), "lgx_ppo_act")
+        self.last_act_fused = fused
+        if prev is not None:
+            self._pending_store = None
         t = self.transition
         t.actions, t.values = self._act_out, st.values[s]
         t.actions_log_prob, t.action_mean, t.action_sigma = st.actions_log_prob[s], st.mu[s], st.sigma[s]

@@ -218,6 +218,8 @@ def declare(lib, prefix="lgx"):
             "mlp_x3_split_layers": (C.c_int, [C.POINTER(vp), C.POINTER(i32), i32, C.POINTER(vp), vp]),
             "mlp_x3_lds_bytes": (i64, [C.POINTER(LgxMlpX3Desc), i32]),
             "mlp_x3_forward": (C.c_int, [C.POINTER(LgxMlpX3Desc), i32, vp]),
+            "mlp_x3_forward_act": (C.c_int, [C.POINTER(LgxMlpX3Desc), i32, C.POINTER(LgxPpoActArgs),
+                                             C.POINTER(LgxPpoStoreArgs), vp]),
             "gemm_partials_floats": (i64, [i64, i32, i32]),
             "gemm_nt": (C.c_int, [C.POINTER(LgxGemmArgs), vp]),
             "gemm_tn": (C.c_int, [C.POINTER(LgxGemmTnArgs), vp]),
@@ -253,7 +255,7 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trim
             "lgx_reduce_slices", "lgx_reduce_slices_finalize", "lgx_ppo_loss_bwd_layout", "lgx_ppo_loss_bwd", "lgx_adam_clip", "lgx_adam_clip_mirror", "lgx_adam_clip_mirror_sq", "lgx_reduce_slices_blocks", "lgx_reduce_slices_sq", "lgx_ppo_act", "lgx_ppo_store", "lgx_ppo_act_store",
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
-            "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward",
+            "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward", "lgx_mlp_x3_forward_act",
             "lgx_event_create", "lgx_event_destroy", "lgx_event_record", "lgx_stream_wait_event"]
 
 

@@ -360,6 +360,45 @@ def test_fused_rollout_act_and_store(gpu, monkeypatch, batched):
     assert torch.equal(st.dones[0, :, 0], dones.byte())
 
 
+@pytest.mark.parametrize("n,cobs", [(1024, None), (1000, None), (1000, 252)])
+def test_fused_act_launch_matches_two_launch_form(gpu, monkeypatch, n, cobs):
+    """lgx_mlp_x3_forward_act (the rollout MLP with lgx_ppo_act's arithmetic in the actor's last
+    layer and the previous step's deferred store in the critic's workgroups) == lgx_mlp_x3_forward +
+    lgx_ppo_act(_store), bit for bit: actions, every storage row of three steps (the second and third
+    carry the store of the step before), rows not a multiple of the 32-row tile, with and without
+    privileged critic observations."""
+    names = ("observations", "privileged_observations", "actions", "values", "actions_log_prob", "mu", "sigma",
+             "rewards", "dones")
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("LGX_FUSED_ACT", fused)
+        _, fus = make_pair(cobs=cobs, N=n)
+        fus.defer_store = True
+        st = fus.storage
+        st.clear()
+        g = torch.Generator(device="cuda:0").manual_seed(7)
+        acts = []
+        with torch.inference_mode():
+            torch.manual_seed(5)
+            for _ in range(3):
+                obs = torch.randn(n, OBS, device="cuda:0", generator=g)
+                cob = torch.randn(n, cobs, device="cuda:0", generator=g) if cobs else obs
+                acts.append(fus.act(obs, cob).clone())
+                assert fus.last_act_fused == (fused == "1")
+                rew = torch.randn(n, device="cuda:0", generator=g)
+                dones = torch.rand(n, device="cuda:0", generator=g) < 0.2
+                time_outs = (torch.rand(n, device="cuda:0", generator=g) < 0.5) & dones
+                fus.process_env_step(rew, dones, {"time_outs": time_outs})
+            fus.flush_store()
+        torch.cuda.synchronize()
+        outs.append((acts, {k: getattr(st, k)[:3].clone() for k in names if getattr(st, k) is not None}))
+    (fa, fs), (ua, us) = outs
+    assert all(torch.equal(x, y) for x, y in zip(fa, ua))
+    assert fs.keys() == us.keys()
+    for k in fs:
+        assert torch.equal(fs[k], us[k]), k
+
+
 def test_fused_minibatch_gradient_matches_numpy_oracle(gpu):
     """The fused minibatch gradient (HIP kernels) against oracle/ppo_oracle.py's hand-derived
     float64 gradient of rsl_rl's PPO loss (independent of torch autograd and of rl/ppo.py):
