@@ -393,6 +393,11 @@ int lgx_event_create(void** ev);
 int lgx_event_destroy(void* ev);
 int lgx_event_record(void* ev, void* stream);
 int lgx_stream_wait_event(void* stream, void* ev);
+/* Record `ev` with the completion of the next lgx kernel launch of the calling thread (bound to the
+ * dispatch: no separate record packet on the producer stream); lgx_launch_bind_pending returns 1
+ * when no launch has taken it yet (record it with lgx_event_record then) and disarms. */
+int lgx_launch_bind_event(void* ev);
+int lgx_launch_bind_pending(void);
 
 /* Generalised advantage estimation (rsl_rl RolloutStorage.compute_returns, before the
  * advantage normalisation): rewards/values/dones [T,N] (dones uint8), last_values [N] ->

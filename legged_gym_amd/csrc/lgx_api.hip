@@ -481,6 +481,20 @@ extern "C" int lgx_event_record(void* ev, void* stream) {
              ? LGX_OK
              : lgx_fail(LGX_EHIP, "lgx_event_record: hipEventRecord failed");
 }
+// Bind a device event to the completion of the NEXT lgx launch on this thread (its dispatch records
+// it: hipExtLaunchKernelGGL's stop event - no separate marker packet on the producer stream, whose
+// processing leaves the stream idle ~5 us between two kernels); lgx_launch_bind_pending: 1 when
+// no launch has taken the event since (the caller then records it itself), and disarms.
+extern "C" int lgx_launch_bind_event(void* ev) {
+  if (!ev) return lgx_fail(LGX_EINVAL, "lgx_launch_bind_event: null event");
+  lgx_timing = lgx_timing_slot{nullptr, reinterpret_cast<hipEvent_t>(ev)};
+  return LGX_OK;
+}
+extern "C" int lgx_launch_bind_pending(void) {
+  const int pending = (lgx_timing.start || lgx_timing.stop) ? 1 : 0;
+  lgx_timing = lgx_timing_slot{};
+  return pending;
+}
 extern "C" int lgx_stream_wait_event(void* stream, void* ev) {
   if (!ev) return lgx_fail(LGX_EINVAL, "lgx_stream_wait_event: null event");
   return hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<hipEvent_t>(ev), 0) == hipSuccess

@@ -65,7 +65,7 @@ struct lgx_timing_slot { hipEvent_t start = nullptr, stop = nullptr; };
 extern thread_local lgx_timing_slot lgx_timing;
 #define LGX_LAUNCH(kern, grid, block, shmem, stream, ...)                                          \
   do {                                                                                           \
-    if (lgx_timing.start) {                                                                      \
+    if (lgx_timing.start || lgx_timing.stop) {                                                   \
       hipExtLaunchKernelGGL(kern, grid, block, shmem, stream, lgx_timing.start, lgx_timing.stop, 0, \
                             __VA_ARGS__);                                                        \
       lgx_timing = lgx_timing_slot{};                                                            \

@@ -1067,14 +1067,23 @@ extern "C" int lgx_ppo_loss_bwd(const lgx_ppo_loss_args* args, float* head_parti
   }();
   if (!attr_ok) return lgx_fail(LGX_EHIP, "lgx_ppo_loss_bwd: hipFuncSetAttribute failed");
   const int blocks = (int)((a.rows + LB_ROWS - 1) / LB_ROWS);
-  if (a.num_actions <= 12)
-    hipLaunchKernelGGL(ppo_loss_bwd_kernel<12>, dim3(blocks), dim3(TPB), (size_t)lay[2], LGX_STREAM(stream), a,
-                       head_partials);
-  else
-    hipLaunchKernelGGL(ppo_loss_bwd_kernel<LGX_PPO_MAX_ACTIONS>, dim3(blocks), dim3(TPB), (size_t)lay[2],
-                       LGX_STREAM(stream), a, head_partials);
-  if (!a.defer_finalize)
-    hipLaunchKernelGGL(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
+  // (LGX_LAUNCH on the call's last launch: a bound event, lgx_launch_bind_event, marks its end)
+  if (a.defer_finalize) {
+    if (a.num_actions <= 12)
+      LGX_LAUNCH(ppo_loss_bwd_kernel<12>, dim3(blocks), dim3(TPB), (size_t)lay[2], LGX_STREAM(stream), a,
+                 head_partials);
+    else
+      LGX_LAUNCH(ppo_loss_bwd_kernel<LGX_PPO_MAX_ACTIONS>, dim3(blocks), dim3(TPB), (size_t)lay[2],
+                 LGX_STREAM(stream), a, head_partials);
+  } else {
+    if (a.num_actions <= 12)
+      hipLaunchKernelGGL(ppo_loss_bwd_kernel<12>, dim3(blocks), dim3(TPB), (size_t)lay[2], LGX_STREAM(stream), a,
+                         head_partials);
+    else
+      hipLaunchKernelGGL(ppo_loss_bwd_kernel<LGX_PPO_MAX_ACTIONS>, dim3(blocks), dim3(TPB), (size_t)lay[2],
+                         LGX_STREAM(stream), a, head_partials);
+    LGX_LAUNCH(ppo_loss_finalize_kernel, dim3(1), dim3(TPB), 0, LGX_STREAM(stream), a, blocks);
+  }
   return lgx_hip_status("lgx_ppo_loss_bwd");
 }
 
@@ -1128,8 +1137,8 @@ static int reduce_slices_launch(const lgx_reduce_job* jobs, int32_t njobs, const
     *blocks_out = grid;
     return LGX_OK;
   }
-  hipLaunchKernelGGL(reduce_slices_kernel, dim3((unsigned)grid), dim3(TPB), 0, LGX_STREAM(stream), J, njobs,
-                     (int32_t)ntiles, f, fin_blocks, sq, step);
+  LGX_LAUNCH(reduce_slices_kernel, dim3((unsigned)grid), dim3(TPB), 0, LGX_STREAM(stream), J, njobs,
+             (int32_t)ntiles, f, fin_blocks, sq, step);
   return lgx_hip_status("lgx_reduce_slices");
 }
 

@@ -759,6 +759,24 @@ class FusedPPOUpdate:
         """"device" (lgx_event_*) or "system" (torch events): the event kind _join uses."""
         return "device" if (os.environ.get("LGX_PPO_DEV_EVENTS", "1") != "0" and self.ppo.dist is None) else "system"
 
+    def _device_events(self):
+        if getattr(self, "_dev_ev", None) is None:
+            self._dev_ev = []
+            for _ in range(self.L + 1):
+                e = C.c_void_p()
+                self.check(self.lib.lgx_event_create(C.byref(e)), "event_create")
+                self._dev_ev.append(e)
+        return self._dev_ev
+
+    def _arm(self, slot):
+        """Bind join `slot`'s device event to the next lgx launch (the producer's last one), so the
+        join records no separate event packet on the producer stream: each record left the stream
+        idle ~5 us between two kernels.  LGX_PPO_BIND=0: recorded at the join as before."""
+        if self.join_events != "device" or os.environ.get("LGX_PPO_BIND", "1") == "0":
+            return
+        self.check(self.lib.lgx_launch_bind_event(self._device_events()[slot]), "launch_bind_event")
+        self._armed = slot
+
     def _join(self, src, dst, slot):
         """Order `dst` after the work issued so far on `src` (slot: 0..L-1 the side stream's inputs,
         L its output).  Device-scope events (lgx_event_*: no system-scope cache write-back and
@@ -766,14 +784,13 @@ class FusedPPOUpdate:
         read per call for same-process A/B runs).  Data-parallel runs keep the system-scope events:
         the joins there also order the collectives' buffers, which peers write over xGMI."""
         if self.join_events == "device":
-            if getattr(self, "_dev_ev", None) is None:
-                self._dev_ev = []
-                for _ in range(self.L + 1):
-                    e = C.c_void_p()
-                    self.check(self.lib.lgx_event_create(C.byref(e)), "event_create")
-                    self._dev_ev.append(e)
-            e = self._dev_ev[slot]
-            self.check(self.lib.lgx_event_record(e, C.c_void_p(src.cuda_stream)), "event_record")
+            e = self._device_events()[slot]
+            armed, self._armed = getattr(self, "_armed", None), None
+            # bound to the producer's last launch by _arm (no record packet on `src`), else recorded
+            if armed != slot or self.lib.lgx_launch_bind_pending():
+                if armed is not None:
+                    self.lib.lgx_launch_bind_pending()   # (a stale binding: disarm)
+                self.check(self.lib.lgx_event_record(e, C.c_void_p(src.cuda_stream)), "event_record")
             self.check(self.lib.lgx_stream_wait_event(C.c_void_p(dst.cuda_stream), e), "stream_wait_event")
         else:
             e = self._ev_in[slot] if slot < self.L else self._ev_out
@@ -883,8 +900,11 @@ class FusedPPOUpdate:
         # ---- loss, gradient at the heads, KL -> adaptive learning rate
         args.idx = idx.data_ptr()
         adaptive = ppo.desired_kl is not None and ppo.schedule == "adaptive"   # (single process: in the loss finalize)
+        side_on = self.tn and os.environ.get("LGX_PPO_DW_SIDE", "1") != "0"
         if self.loss_bwd:
             # loss + output-layer backward in one launch (dZ3 over Y[L-1]); finalize in the reduction
+            if side_on and (L - 1) in self.gemm_dw:
+                self._arm(L - 1)   # (the first join's producer)
             chk(lib.lgx_ppo_loss_bwd(C.byref(args), _vp(self.head_parts), stream), "lgx_ppo_loss_bwd")
         else:
             chk(lib.lgx_ppo_loss(C.byref(args), stream), "lgx_ppo_loss")
@@ -896,7 +916,6 @@ class FusedPPOUpdate:
         # one (both only read dZ_k and Y_{k-1}): the weight-gradient tiles fill the CUs that the
         # dA launch's last round leaves idle (measured 19.3 -> 19.0 ms per iteration);
         # LGX_PPO_DW_SIDE=0 keeps every launch on one stream
-        side_on = self.tn and os.environ.get("LGX_PPO_DW_SIDE", "1") != "0"
         side_used = False
         for k in range(L - 1, 0, -1):
             # dW_k = dZ_k^T Y_{k-1}, split-K over S row slices (partials reduced below); each dW on
@@ -921,6 +940,8 @@ class FusedPPOUpdate:
                 torch.bmm(dZ.view(2 * Sl, M // Sl, h[k]).transpose(1, 2),
                           self.Y[k - 1].view(2 * Sl, M // Sl, h[k - 1]), out=self.P[k])
             if fused:
+                if side_on and k - 1 >= 1 and (k - 1) in self.gemm_dw:
+                    self._arm(k - 1)   # (the next join's producer: this dA launch)
                 self._gemm(self.gemm_bwd[k], stream)
             else:
                 torch.bmm(dZ, self.W[k], out=self.D[k - 1])
@@ -939,6 +960,7 @@ class FusedPPOUpdate:
             # runs here - the memory-bound reduction next to the MFMA-bound GEMM
             if not self.rest_on_side:   # (skipping the join when possible: 10.478 -> 10.468 ms per update)
                 self._join(torch.cuda.current_stream(self.dev), self._side, 0)
+            self._arm(L)   # (the final join's producer: the side stream's last launch)
             if use_sq:
                 chk(lib.lgx_reduce_slices_sq(self.jobs_rest, len(self.jobs_rest), C.byref(args), C.c_void_p(sq), step_p,
                                              C.c_void_p(self._side.cuda_stream)), "reduce")

@@ -238,6 +238,8 @@ def declare(lib, prefix="lgx"):
             "event_destroy": (C.c_int, [vp]),
             "event_record": (C.c_int, [vp, vp]),
             "stream_wait_event": (C.c_int, [vp, vp]),
+            "launch_bind_event": (C.c_int, [vp]),
+            "launch_bind_pending": (C.c_int, []),
         })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}")
@@ -256,7 +258,8 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trim
             "lgx_gemm_partials_floats", "lgx_gemm_nt", "lgx_copy2d", "lgx_ppo_gather_rows_padded",
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
             "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward", "lgx_mlp_x3_forward_act",
-            "lgx_event_create", "lgx_event_destroy", "lgx_event_record", "lgx_stream_wait_event"]
+            "lgx_event_create", "lgx_event_destroy", "lgx_event_record", "lgx_stream_wait_event",
+            "lgx_launch_bind_event", "lgx_launch_bind_pending"]
 
 
 def check_layout(sizes_fn, n=12):
