@@ -174,6 +174,27 @@ def test_fused_update_ab_variants(gpu, monkeypatch, var, val):
     assert big <= 1e-3 * total, (big, total)
 
 
+def test_bound_join_events_match_recorded_events(gpu, monkeypatch):
+    """The backward's cross-stream joins with their device events bound to the producer launches
+    (lgx_launch_bind_event, the default) and recorded after them (LGX_PPO_BIND=0): the same kernels
+    in the same order, so a full update gives bitwise the same parameters, moments and losses; every
+    armed binding was taken by a launch."""
+    out = []
+    for bind in ("1", "0"):
+        monkeypatch.setenv("LGX_PPO_BIND", bind)
+        _, fus = make_pair()
+        torch.manual_seed(11)
+        losses = fus.update()
+        torch.cuda.synchronize()
+        assert getattr(fus._fused, "_armed", None) is None
+        assert fus._fused.lib.lgx_launch_bind_pending() == 0
+        o = fus.optimizer
+        out.append(([p.detach().clone() for p in fus.actor_critic.parameters()], o.m.clone(), o.v.clone(), losses))
+    (pa, ma, va, la), (pb, mb, vb, lb) = out
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))
+    assert torch.equal(ma, mb) and torch.equal(va, vb) and la == lb
+
+
 def test_fused_minibatch_gradient_separate_loss_and_head(gpu, monkeypatch):
     """lgx_ppo_loss + lgx_head_bwd_finalize as two launches (LGX_PPO_LOSS_BWD=0) instead of
     lgx_ppo_loss_bwd: minibatch gradient and a full update against autograd."""
