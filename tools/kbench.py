@@ -113,6 +113,40 @@ def env_env_ab(task=os.environ.get("KB_TASK", "go1_rough"), n=int(os.environ.get
         print(f"{task} N={n} {var}={m}: env.step median {v[len(v) // 2]:.1f} us, min {v[0]:.1f} us", flush=True)
 
 
+def env_create_ab(task=os.environ.get("KB_TASK", "go1_rough"), n=int(os.environ.get("KB_N", "4096")),
+                  var=os.environ.get("KB_VAR", "LGX_ACT_OVERLAP"), modes=tuple(os.environ.get("KB_VALUES", "2,3").split(",")),
+                  rounds=int(os.environ.get("KB_ROUNDS", "10")), steps=24):
+    """A/B of an env switch read when the sim is created (env var `var`): one env per value, env
+    steps interleaved round by round in ONE process (HIP events); prints median / min us per step."""
+    from oracle_backend import make_env
+    envs = {}
+    prev = os.environ.get(var)
+    for m in modes:
+        os.environ[var] = m
+        envs[m] = make_env(task, num_envs=n, device="cuda:0", backend="lgx")
+        envs[m].reset()
+    if prev is None:
+        os.environ.pop(var)
+    else:
+        os.environ[var] = prev
+    a = torch.randn(n, 12, device="cuda:0")
+    res = {m: [] for m in modes}
+    for r in range(rounds + 1):
+        for m in modes:
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                envs[m].step(a)
+            e1.record()
+            e1.synchronize()
+            if r:
+                res[m].append(e0.elapsed_time(e1) * 1e3 / steps)
+    for m in modes:
+        v = sorted(res[m])
+        print(f"{task} N={n} {var}={m}: env.step median {v[len(v) // 2]:.1f} us, min {v[0]:.1f} us", flush=True)
+
+
 def phys_ab():
     """A/B the physics kernel lanes-per-leg variants (LGX_PHYS_PP, read when a sim is created)."""
     from oracle_backend import make_env
@@ -413,5 +447,7 @@ if __name__ == "__main__":
         update_plan_ab()
     if "env_env" in what:
         env_env_ab()
+    if "env_create" in what:
+        env_create_ab()
 
 
