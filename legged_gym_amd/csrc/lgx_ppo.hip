@@ -853,6 +853,16 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
                  Mirrors mir) {
   __shared__ float red[TPB];
   __shared__ float coef_s, step_size_s, bc2_sqrt_s;
+  // this thread's first AE elements loaded before the prologue: their HBM latency overlaps the
+  // partial-sum reduction and the bias corrections instead of following them (clamped addresses)
+  constexpr int AE = 3;
+  const int64_t stride = (int64_t)gridDim.x * TPB, i0 = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  float pp[AE], gg[AE], mm[AE], vv[AE];
+#pragma unroll
+  for (int u = 0; u < AE; ++u) {
+    const int64_t i = min(i0 + u * stride, n - 1);
+    pp[u] = p[i]; gg[u] = g[i]; mm[u] = m[i]; vv[u] = v[i];
+  }
   float s = 0.f;
   {   // (lgx_adam_clip_mirror_sq reads up to ~1k partials: 16-byte loads)
     const int n4 = ((uintptr_t)partials & 15) == 0 ? nparts / 4 : 0;
@@ -880,15 +890,15 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
   }
   __syncthreads();
   const float coef = coef_s, step_size = step_size_s, bc2_sqrt = bc2_sqrt_s;
-  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * TPB) {
-    const float gi = g[i] * coef;
+  auto update = [&](int64_t i, float p0, float g0, float m0, float v0) {
+    const float gi = g0 * coef;
     g[i] = gi;
-    const float mi = beta1 * m[i] + (1.f - beta1) * gi;
-    const float vi = beta2 * v[i] + (1.f - beta2) * gi * gi;
+    const float mi = beta1 * m0 + (1.f - beta1) * gi;
+    const float vi = beta2 * v0 + (1.f - beta2) * gi * gi;
     m[i] = mi;
     v[i] = vi;
     const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pi = p[i] - step_size * mi / denom;
+    const float pi = p0 - step_size * mi / denom;
     p[i] = pi;
     for (int q = 0; q < mir.n; ++q) {
       const Mirror& J = mir.mj[q];
@@ -899,7 +909,11 @@ adam_clip_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict
         mirror_store(J, b, rr, cc, pi);
       }
     }
-  }
+  };
+#pragma unroll
+  for (int u = 0; u < AE; ++u)
+    if (i0 + u * stride < n) update(i0 + u * stride, pp[u], gg[u], mm[u], vv[u]);
+  for (int64_t i = i0 + AE * stride; i < n; i += stride) update(i, p[i], g[i], m[i], v[i]);
 }
 
 }  // namespace
