@@ -148,7 +148,7 @@ class PPO:
                                                 stream) != 0:
             # (validated before any launch) a pair the fused launch does not take, e.g. the act
             # rows past the LDS: the two-launch form from now on
-            self._fused_act_off = fused = False
+            self._fused_act_off, fused = True, False
         if not fused:
             launch_forward(descs, 2, stream)   # actor and critic in one launch
             if prev is not None:   # the previous step's store rides along

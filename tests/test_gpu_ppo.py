@@ -420,6 +420,33 @@ def test_fused_act_launch_matches_two_launch_form(gpu, monkeypatch, n, cobs):
         assert torch.equal(fs[k], us[k]), k
 
 
+def test_fused_act_launch_refused_falls_back(gpu):
+    """A network pair the fused act launch refuses (its entry returns an error before launching)
+    switches that PPO object to the two-launch form for good, with the same rows."""
+    _, a = make_pair(N=1000)
+    _, b = make_pair(N=1000)
+    lib = b._fused.lib
+
+    class Refusing:   # the library with lgx_mlp_x3_forward_act refusing
+        def __getattr__(self, name):
+            return (lambda *args: -1) if name == "lgx_mlp_x3_forward_act" else getattr(lib, name)
+    b._fused.lib = Refusing()
+    for p in (a, b):
+        p.storage.clear()
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    obs = torch.randn(1000, OBS, device="cuda:0", generator=g)
+    with torch.inference_mode():
+        torch.manual_seed(4)
+        xa = a.act(obs, obs).clone()
+        torch.manual_seed(4)
+        xb = b.act(obs, obs).clone()
+    torch.cuda.synchronize()
+    assert a.last_act_fused and not b.last_act_fused and b._fused_act_off
+    assert torch.equal(xa, xb)
+    for k in ("observations", "actions", "values", "actions_log_prob", "mu", "sigma"):
+        assert torch.equal(getattr(a.storage, k)[0], getattr(b.storage, k)[0]), k
+
+
 def test_fused_minibatch_gradient_matches_numpy_oracle(gpu):
     """The fused minibatch gradient (HIP kernels) against oracle/ppo_oracle.py's hand-derived
     float64 gradient of rsl_rl's PPO loss (independent of torch autograd and of rl/ppo.py):
