@@ -253,6 +253,44 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
                    int device, lgx_sim** out);
 int lgx_sim_destroy(lgx_sim* sim);
 
+/* The sim's state tensors by id (SURVEY §8(b) lgx_sim_buffer): the device pointer bound at
+ * lgx_sim_create (or the latest lgx_rebind_obs), its shape (ndim <= 4, row-major, contiguous) and
+ * element type.  Replaces the gym tensor acquisition + wrap_tensor of the reference
+ * (legged_robot.py:507-524: actor_root_state, dof_state, net_contact_force) and the buffers
+ * _init_buffers allocates (legged_robot.py:525-565); a binding wraps them without copies (DLPack /
+ * from_blob).  Unbound (NULL) buffers are reported with a NULL pointer and their shape. */
+enum lgx_buffer_id {
+  LGX_BUF_ROOT_STATES = 0,  /* f32 [N,13] */
+  LGX_BUF_DOF_STATE,        /* f32 [N,12,2] */
+  LGX_BUF_DOF_TARGETS,      /* f32 [N,12] */
+  LGX_BUF_TORQUES,          /* f32 [N,12] */
+  LGX_BUF_CONTACT_FORCES,   /* f32 [N,LGX_MAX_BODIES,3] */
+  LGX_BUF_ACTIONS,          /* f32 [N,12] */
+  LGX_BUF_LAST_ACTIONS,     /* f32 [N,12] */
+  LGX_BUF_LAST_DOF_VEL,     /* f32 [N,12] */
+  LGX_BUF_LAST_ROOT_VEL,    /* f32 [N,6] */
+  LGX_BUF_COMMANDS,         /* f32 [N,4] */
+  LGX_BUF_BASE_LIN_VEL,     /* f32 [N,3] */
+  LGX_BUF_BASE_ANG_VEL,     /* f32 [N,3] */
+  LGX_BUF_PROJECTED_GRAVITY,/* f32 [N,3] */
+  LGX_BUF_FEET_AIR_TIME,    /* f32 [N,4] */
+  LGX_BUF_OBS,              /* f32 [N,num_obs] */
+  LGX_BUF_REW,              /* f32 [N] */
+  LGX_BUF_RESET,            /* u8 [N] */
+  LGX_BUF_TIME_OUT,         /* u8 [N] */
+  LGX_BUF_EPISODE_LENGTH,   /* i64 [N] */
+  LGX_BUF_EPISODE_SUMS,     /* f32 [T,N], T = num_terms (+1 with a termination slot) */
+  LGX_BUF_MEASURED_HEIGHTS, /* f32 [N,num_height_points] */
+  LGX_BUF_ENV_ORIGINS,      /* f32 [N,3] */
+  LGX_BUF_TERRAIN_LEVELS,   /* i64 [N] */
+  LGX_BUF_TERRAIN_TYPES,    /* i64 [N] */
+  LGX_BUF_EXTRAS,           /* f32 [T+2] */
+  LGX_BUF_COUNT
+};
+enum lgx_dtype { LGX_F32 = 0, LGX_U8 = 1, LGX_I64 = 2 };
+int lgx_sim_buffer(lgx_sim* sim, int32_t buffer_id, void** dev_ptr, int64_t shape[4], int32_t* ndim,
+                   int32_t* dtype);
+
 /* Full env step: clip actions, `decimation` x (targets -> physics substep), then the fused
  * post-physics step.  Replaces LeggedRobot.step (legged_robot.py:79-107) including
  * set_dof_position_target_tensor / simulate / refresh_* and post_physics_step.

@@ -236,6 +236,47 @@ int lgx_sim_destroy(lgx_sim* s) {
   return 0;
 }
 
+int lgx_sim_buffer(lgx_sim* s, int32_t id, void** ptr, int64_t shape[4], int32_t* ndim, int32_t* dtype) {
+  if (!s || !ptr || !shape || !ndim || !dtype) return fail(LGX_EINVAL, "lgx_sim_buffer: null argument");
+  const int64_t N = s->params.num_envs;
+  const lgx_buffers& b = s->bufs;
+  struct Entry { void* p; int nd; int64_t d[3]; int dt; };
+  Entry e;
+  switch (id) {
+    case LGX_BUF_ROOT_STATES: e = {b.root_states, 2, {N, 13}, LGX_F32}; break;
+    case LGX_BUF_DOF_STATE: e = {b.dof_state, 3, {N, LGX_NUM_DOF, 2}, LGX_F32}; break;
+    case LGX_BUF_DOF_TARGETS: e = {b.dof_targets, 2, {N, LGX_NUM_DOF}, LGX_F32}; break;
+    case LGX_BUF_TORQUES: e = {b.torques, 2, {N, LGX_NUM_DOF}, LGX_F32}; break;
+    case LGX_BUF_CONTACT_FORCES: e = {b.contact_forces, 3, {N, LGX_MAX_BODIES, 3}, LGX_F32}; break;
+    case LGX_BUF_ACTIONS: e = {b.actions, 2, {N, LGX_NUM_DOF}, LGX_F32}; break;
+    case LGX_BUF_LAST_ACTIONS: e = {b.last_actions, 2, {N, LGX_NUM_DOF}, LGX_F32}; break;
+    case LGX_BUF_LAST_DOF_VEL: e = {b.last_dof_vel, 2, {N, LGX_NUM_DOF}, LGX_F32}; break;
+    case LGX_BUF_LAST_ROOT_VEL: e = {b.last_root_vel, 2, {N, 6}, LGX_F32}; break;
+    case LGX_BUF_COMMANDS: e = {b.commands, 2, {N, 4}, LGX_F32}; break;
+    case LGX_BUF_BASE_LIN_VEL: e = {b.base_lin_vel, 2, {N, 3}, LGX_F32}; break;
+    case LGX_BUF_BASE_ANG_VEL: e = {b.base_ang_vel, 2, {N, 3}, LGX_F32}; break;
+    case LGX_BUF_PROJECTED_GRAVITY: e = {b.projected_gravity, 2, {N, 3}, LGX_F32}; break;
+    case LGX_BUF_FEET_AIR_TIME: e = {b.feet_air_time, 2, {N, 4}, LGX_F32}; break;
+    case LGX_BUF_OBS: e = {b.obs, 2, {N, s->params.num_obs}, LGX_F32}; break;
+    case LGX_BUF_REW: e = {b.rew, 1, {N}, LGX_F32}; break;
+    case LGX_BUF_RESET: e = {b.reset, 1, {N}, LGX_U8}; break;
+    case LGX_BUF_TIME_OUT: e = {b.time_out, 1, {N}, LGX_U8}; break;
+    case LGX_BUF_EPISODE_LENGTH: e = {b.episode_length, 1, {N}, LGX_I64}; break;
+    case LGX_BUF_EPISODE_SUMS: e = {b.episode_sums, 2, {s->n_term_rows, N}, LGX_F32}; break;
+    case LGX_BUF_MEASURED_HEIGHTS: e = {b.measured_heights, 2, {N, s->params.num_height_points}, LGX_F32}; break;
+    case LGX_BUF_ENV_ORIGINS: e = {b.env_origins, 2, {N, 3}, LGX_F32}; break;
+    case LGX_BUF_TERRAIN_LEVELS: e = {b.terrain_levels, 1, {N}, LGX_I64}; break;
+    case LGX_BUF_TERRAIN_TYPES: e = {b.terrain_types, 1, {N}, LGX_I64}; break;
+    case LGX_BUF_EXTRAS: e = {b.extras, 1, {s->n_term_rows + 2}, LGX_F32}; break;
+    default: return fail(LGX_EINVAL, "lgx_sim_buffer: unknown buffer id");
+  }
+  *ptr = e.p;
+  *ndim = e.nd;
+  *dtype = e.dt;
+  for (int i = 0; i < 4; ++i) shape[i] = i < e.nd ? e.d[i] : 1;
+  return 0;
+}
+
 int lgx_set_draws(lgx_sim* s, const float* draws) {
   if (!s) return fail(LGX_EINVAL, "lgx_set_draws: null sim");
   s->draws = draws;

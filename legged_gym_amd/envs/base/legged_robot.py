@@ -78,6 +78,20 @@ class LgxBackend:
     def sync_aux(self):
         self._check(self.lib.lgx_sync_aux(self.handle, self.stream()), "lgx_sync_aux")
 
+    BUFFER_IDS = ("root_states", "dof_state", "dof_targets", "torques", "contact_forces", "actions",
+                  "last_actions", "last_dof_vel", "last_root_vel", "commands", "base_lin_vel", "base_ang_vel",
+                  "projected_gravity", "feet_air_time", "obs", "rew", "reset", "time_out", "episode_length",
+                  "episode_sums", "measured_heights", "env_origins", "terrain_levels", "terrain_types", "extras")
+    DTYPES = (torch.float32, torch.uint8, torch.int64)
+
+    def buffer(self, name):
+        """lgx_sim_buffer: (device pointer, shape, torch dtype) of a state tensor the sim writes
+        (enum lgx_buffer_id order = BUFFER_IDS)."""
+        ptr, shape, nd, dt = C.c_void_p(), (C.c_int64 * 4)(), C.c_int32(), C.c_int32()
+        self._check(self.lib.lgx_sim_buffer(self.handle, self.BUFFER_IDS.index(name), C.byref(ptr), shape,
+                                            C.byref(nd), C.byref(dt)), "lgx_sim_buffer")
+        return ptr.value or 0, tuple(shape[:nd.value]), self.DTYPES[dt.value]
+
     def rebind_extras(self, snapshot):
         self._check(self.lib.lgx_rebind_extras(self.handle, C.c_void_p(snapshot.data_ptr())), "lgx_rebind_extras")
 

@@ -868,3 +868,36 @@ def test_dense_kernel_on_quadrupeds_matches_float64(gpu, monkeypatch, task):
     ov = {k: f(ora) for k, f in PHYS_QTY.items()}
     check_derived(t64, ov, {k: f(dense) for k, f in PHYS_QTY.items()})
     check_derived(t64, ov, {k: f(arrow) for k, f in PHYS_QTY.items()})
+
+
+def test_sim_buffer_reports_the_bound_tensors(gpu):
+    """lgx_sim_buffer: every id names the tensor the env bound at lgx_sim_create
+    (obs: the one rebound by the latest step), with its shape and dtype; an unknown id fails."""
+    env = make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
+    env.step(torch.zeros(env.num_envs, env.num_actions, device=env.device))
+    torch.cuda.synchronize()
+    be = env._backend
+    bound = {"root_states": env.root_states, "dof_state": env.dof_state, "dof_targets": env.target_poses,
+             "torques": env.torques, "contact_forces": env._contact_forces_full, "actions": env.actions,
+             "last_actions": env.last_actions, "last_dof_vel": env.last_dof_vel, "last_root_vel": env.last_root_vel,
+             "commands": env.commands, "base_lin_vel": env.base_lin_vel, "base_ang_vel": env.base_ang_vel,
+             "projected_gravity": env.projected_gravity, "feet_air_time": env._feet_air_time_full,
+             "obs": env.obs_buf, "rew": env.rew_buf, "reset": env.reset_buf, "time_out": env.time_out_buf,
+             "episode_length": env._episode_length_buf, "episode_sums": env._episode_sums_buf,
+             "measured_heights": env.measured_heights, "env_origins": env.env_origins,
+             "terrain_levels": env.terrain_levels, "terrain_types": env.terrain_types, "extras": env._extras_buf}
+    assert set(bound) == set(be.BUFFER_IDS)
+    for name in be.BUFFER_IDS:
+        ptr, shape, dtype = be.buffer(name)
+        t = bound[name]
+        assert ptr == t.data_ptr(), name
+        assert dtype == (torch.uint8 if t.dtype == torch.bool else t.dtype), name
+        assert int(np.prod(shape)) == t.numel(), (name, shape, tuple(t.shape))
+        if name != "dof_state":   # (the reference's view is [N * 12, 2], gymtorch's wrap of the same memory)
+            assert shape[0] == t.shape[0], name
+    assert be.buffer("dof_state")[1] == (64, 12, 2)
+    assert be.buffer("contact_forces")[1] == (64, 17, 3)
+    assert be.buffer("obs")[1] == (64, env.num_obs)
+    ptr, shape, nd, dt = C.c_void_p(), (C.c_int64 * 4)(), C.c_int32(), C.c_int32()
+    assert be.lib.lgx_sim_buffer(be.handle, len(be.BUFFER_IDS), C.byref(ptr), shape, C.byref(nd), C.byref(dt)) != 0
+    assert b"unknown buffer id" in be.lib.lgx_last_error()
