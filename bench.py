@@ -377,6 +377,7 @@ def data_parallel_check(runner, fused, comm_t, world, backend, device, dist):
     if fused is not None:
         out["bucketed_allreduce"] = bool(fused.bucketed)
         out["join_events"] = fused.join_events   # cross-stream joins: "system" whenever data-parallel
+        out["allreduce_impl"] = fused.allreduce_impl   # "lgx" = lgx_allreduce_grads (LGX_NATIVE_ALLREDUCE=1)
         n, ms, nbytes, mbs = comm_t
         mb_per_iter = alg.num_learning_epochs * alg.num_mini_batches
         out["allreduce"] = {"collectives_timed": n, "bytes_per_minibatch": (nbytes / mbs) if mbs else 0,
@@ -615,6 +616,8 @@ def main():
     if rank == 0:
         print(json.dumps(out))
     if distributed:
+        if fused is not None:
+            fused.close_comm()
         dist.destroy_process_group()
 
 

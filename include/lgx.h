@@ -22,6 +22,7 @@
 #ifndef LGX_H
 #define LGX_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -306,6 +307,22 @@ int lgx_step_from(lgx_sim* sim, const float* actions, int64_t common_step_counte
  * rebinds obs_buf every step (`self.obs_buf = torch.cat(...)`, legged_robot.py:218), so rsl_rl
  * keeps the previous step's tensor alive across env.step(); callers double-buffer with this. */
 int lgx_rebind_obs(lgx_sim* sim, float* obs);
+
+/* Data-parallel gradient all-reduce over RCCL (SURVEY §8(b) lgx_allreduce_grads; §8(e): the
+ * gradient average of a multi-GPU PPO update, one rank per GPU).  One communicator per rank,
+ * created collectively from a unique id that rank 0 draws and the caller distributes (e.g. over
+ * its torch.distributed group).  The all-reduce is issued on `stream` itself (in place, float32),
+ * so it is ordered by that stream like any kernel.  RCCL is loaded at run time from `rccl_path`
+ * (the process's own RCCL, e.g. torch's bundled librccl.so; NULL = librccl.so.1); LGX_EINVAL if it
+ * cannot be loaded, LGX_EHIP for an RCCL error (message in lgx_last_error). */
+#define LGX_COMM_ID_BYTES 128
+enum lgx_reduce_op { LGX_REDUCE_SUM = 0, LGX_REDUCE_AVG = 1 };
+typedef struct lgx_comm lgx_comm;
+int lgx_comm_unique_id(const char* rccl_path, uint8_t id[LGX_COMM_ID_BYTES]);
+int lgx_comm_create(const char* rccl_path, const uint8_t id[LGX_COMM_ID_BYTES], int32_t nranks, int32_t rank,
+                    int32_t device, lgx_comm** out);
+int lgx_comm_destroy(lgx_comm* comm);
+int lgx_allreduce_grads(lgx_comm* comm, float* buf, size_t count, int32_t op, void* stream);
 
 /* Per-call copy of the episode extras (device float[T + 2], lgx_buffers.extras layout) written by
  * the next lgx_step / lgx_post_physics / lgx_reset_idx, stale values included.  The reference

@@ -729,10 +729,54 @@ class FusedPPOUpdate:
         if rec:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(torch_stream)
-        self.ppo.dist.all_reduce(buf)
+        comm = self._lgx_comm()
+        if comm is not None:   # lgx_allreduce_grads: RCCL on this stream itself (sum; 1/world in Adam)
+            assert buf.dtype == torch.float32 and buf.is_contiguous()
+            self.check(self.lib.lgx_allreduce_grads(comm, _vp(buf), buf.numel(), 0,
+                                                    C.c_void_p(torch_stream.cuda_stream)), "allreduce_grads")
+        else:
+            self.ppo.dist.all_reduce(buf)
         if rec:
             e1.record(torch_stream)
             self._c_events.append((buf.numel() * buf.element_size(), e0, e1))
+
+    @property
+    def allreduce_impl(self):
+        """"lgx" (lgx_allreduce_grads on the library's own RCCL communicator, LGX_NATIVE_ALLREDUCE=1
+        with the nccl backend) or "torch" (torch.distributed.all_reduce, the default)."""
+        return "lgx" if getattr(self, "_comm", None) is not None else "torch"
+
+    def _lgx_comm(self):
+        """The rank's lgx_comm, created collectively at the first gradient all-reduce when
+        LGX_NATIVE_ALLREDUCE=1 and the process group is nccl (RCCL): rank 0 draws the unique id,
+        the group broadcasts it; the RCCL library is torch's own (one RCCL instance per process)."""
+        if hasattr(self, "_comm"):
+            return self._comm
+        self._comm = None
+        dist = self.ppo.dist
+        if os.environ.get("LGX_NATIVE_ALLREDUCE", "0") != "1" or dist.get_backend() != "nccl":
+            return None
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        path = path.encode() if os.path.exists(path) else None
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if dist.get_rank() == 0:
+            self.check(self.lib.lgx_comm_unique_id(path, C.cast(uid.data_ptr(), C.POINTER(C.c_uint8))),
+                       "comm_unique_id")
+        dev_uid = uid.to(self.dev)
+        dist.broadcast(dev_uid, src=0)
+        uid = dev_uid.cpu()
+        comm = C.c_void_p()
+        self.check(self.lib.lgx_comm_create(path, C.cast(uid.data_ptr(), C.POINTER(C.c_uint8)), dist.get_world_size(),
+                                            dist.get_rank(), self.dev.index or 0, C.byref(comm)), "comm_create")
+        self._comm = comm
+        return comm
+
+    def close_comm(self):
+        """Destroy the lgx_comm (collective: every rank calls it after its last update)."""
+        comm, self._comm = getattr(self, "_comm", None), None
+        if comm is not None:
+            torch.cuda.synchronize(self.dev)
+            self.check(self.lib.lgx_comm_destroy(comm), "comm_destroy")
 
     def comm_timings(self):
         """(collectives timed, total ms, total bytes, timed minibatches) of the all-reduces of the

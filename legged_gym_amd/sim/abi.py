@@ -241,6 +241,10 @@ def declare(lib, prefix="lgx"):
             "stream_wait_event": (C.c_int, [vp, vp]),
             "launch_bind_event": (C.c_int, [vp]),
             "launch_bind_pending": (C.c_int, []),
+            "comm_unique_id": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8)]),
+            "comm_create": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint8), i32, i32, i32, C.POINTER(vp)]),
+            "comm_destroy": (C.c_int, [vp]),
+            "allreduce_grads": (C.c_int, [vp, vp, C.c_size_t, i32, vp]),
         })
     for name, (res, args) in sigs.items():
         fn = getattr(lib, f"{prefix}_{name}")
@@ -260,7 +264,8 @@ EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trim
             "lgx_ppo_gather_rows_padded_dup", "lgx_split_bf16_elems", "lgx_split_bf16", "lgx_gemm_tn",
             "lgx_mlp_x3_weight_elems", "lgx_mlp_x3_split", "lgx_mlp_x3_split_layers", "lgx_mlp_x3_lds_bytes", "lgx_mlp_x3_forward", "lgx_mlp_x3_forward_act",
             "lgx_event_create", "lgx_event_destroy", "lgx_event_record", "lgx_stream_wait_event",
-            "lgx_launch_bind_event", "lgx_launch_bind_pending"]
+            "lgx_launch_bind_event", "lgx_launch_bind_pending",
+            "lgx_comm_unique_id", "lgx_comm_create", "lgx_comm_destroy", "lgx_allreduce_grads"]
 
 
 def check_layout(sizes_fn, n=12):

@@ -36,6 +36,22 @@ def test_library_loads_and_exports_every_symbol():
     assert lib.lgx_version() == 1
 
 
+def test_comm_entry_points_validate_without_a_gpu():
+    """lgx_comm_* / lgx_allreduce_grads argument and library checks (host-side only: no RCCL call
+    and no device is reached)."""
+    import torch  # noqa: F401
+    from legged_gym_amd.sim import abi
+    lib = abi.declare(C.CDLL(os.path.join(ROOT, "legged_gym_amd", "liblgx.so")))
+    uid = (C.c_uint8 * 128)()
+    assert lib.lgx_comm_unique_id(b"/nonexistent/librccl.so", uid) == -1
+    assert b"not loadable" in lib.lgx_last_error()
+    comm = C.c_void_p()
+    assert lib.lgx_comm_create(None, uid, 2, 2, 0, C.byref(comm)) == -1      # rank >= nranks
+    assert lib.lgx_comm_create(None, None, 1, 0, 0, C.byref(comm)) == -1     # no id
+    assert lib.lgx_allreduce_grads(None, None, 4, 0, None) == -1
+    assert lib.lgx_comm_destroy(None) == 0
+
+
 def test_oracle_layout_matches():
     from oracle_backend import load_oracle
     load_oracle()  # check_layout inside

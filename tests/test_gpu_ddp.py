@@ -201,3 +201,106 @@ def test_bench_rccl_rehearsal_one_rank(gpu, tmp_path):
     assert dp["join_events"] == "system"
     assert dp["bucketed_allreduce"] is True
     assert dp["allreduce"]["collectives_timed"] >= 2 and dp["allreduce"]["ms_per_iteration"] > 0
+
+
+def _comm_worker(q):
+    """One-rank lgx_comm in a fresh process (RCCL state dies with it)."""
+    import ctypes as C
+    from legged_gym_amd.sim import lib as lgxlib
+    lib = lgxlib.load()
+    torch.cuda.set_device(0)
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    path = path.encode() if os.path.exists(path) else None
+    uid = (C.c_uint8 * 128)()
+    lgxlib.check(lib.lgx_comm_unique_id(path, uid), "comm_unique_id")
+    comm = C.c_void_p()
+    lgxlib.check(lib.lgx_comm_create(path, uid, 1, 0, 0, C.byref(comm)), "comm_create")
+    x = torch.randn(1 << 20, device="cuda:0")
+    want = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    for op in (0, 1):   # sum, average over one rank: the identity
+        lgxlib.check(lib.lgx_allreduce_grads(comm, C.c_void_p(x.data_ptr()), x.numel(), op,
+                                             C.c_void_p(s.cuda_stream)), "allreduce_grads")
+    s.synchronize()
+    ok = bool(torch.equal(x, want))
+    bad = lib.lgx_allreduce_grads(comm, C.c_void_p(x.data_ptr()), x.numel(), 7, C.c_void_p(s.cuda_stream))
+    lgxlib.check(lib.lgx_comm_destroy(comm), "comm_destroy")
+    q.put((ok, bad))
+
+
+@pytest.mark.timeout(200)
+def test_lgx_comm_one_rank_allreduce(gpu):
+    """lgx_comm_create / lgx_allreduce_grads over a one-rank RCCL communicator on the caller's
+    stream (RCCL refuses two ranks on one device): sum and average leave the buffer bitwise
+    unchanged; an unknown op is refused."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_comm_worker, args=(q,))
+    p.start()
+    ok, bad = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0 and ok and bad == -1
+
+
+def _native_worker(port, q):
+    """One-rank nccl group (LGX_DIST_REHEARSAL=1): the same update with torch.distributed's
+    all-reduce and with lgx_allreduce_grads, from the same state, in one process."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                      LGX_DIST_REHEARSAL="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        out = {}
+        for native in ("0", "1"):
+            os.environ["LGX_NATIVE_ALLREDUCE"] = native
+            ppo = _make(2 * B, slice(0, 2 * B))
+            assert ppo._fused is not None and ppo.dist is not None
+            ppo.update()
+            out[native] = ([p.detach().cpu().numpy() for p in ppo.actor_critic.parameters()],
+                           ppo.learning_rate, ppo._fused.allreduce_impl)
+            ppo._fused.close_comm()
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(200)
+def test_native_allreduce_update_matches_torch_allreduce(gpu):
+    """The data-parallel update over a one-rank RCCL group: with LGX_NATIVE_ALLREDUCE=1 the
+    gradient buckets go through lgx_allreduce_grads on the update's own streams, and the parameters
+    and learning rate after the update are bitwise those of the torch.distributed path."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_native_worker, args=(_free_port(), q))
+    p.start()
+    out = q.get(timeout=180)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    (pt, lrt, it), (pn, lrn, inn) = out["0"], out["1"]
+    assert it == "torch" and inn == "lgx"
+    assert lrt == lrn
+    for a, b in zip(pt, pn):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.timeout(280)
+def test_bench_rccl_rehearsal_native_allreduce(gpu, tmp_path):
+    """bench.py's one-rank RCCL rehearsal with LGX_NATIVE_ALLREDUCE=1 reports the native all-reduce
+    (event-timed, both buckets) and the data-parallel self-check."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, LGX_DIST_BACKEND="nccl", LGX_DIST_REHEARSAL="1", HSA_ENABLE_IPC_MODE_LEGACY="0",
+               LGX_BENCH_GEMM_TIMING="1", LGX_NATIVE_ALLREDUCE="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "1", "--steps", "2", "--warmup", "1", "--task", "go1_flat_bench", "--num_envs", "1024",
+           "--no_cpu_baseline"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    dp = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["data_parallel"]
+    assert dp["allreduce_impl"] == "lgx" and dp["ranks_seen"] == 1 and dp["param_fingerprint_spread"] == 0
+    assert dp["bucketed_allreduce"] is True and dp["allreduce"]["collectives_timed"] >= 2
