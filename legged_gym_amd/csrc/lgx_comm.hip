@@ -5,7 +5,8 @@
 //
 // RCCL is resolved at run time from the library the caller names (the process's own RCCL, e.g.
 // the one torch.distributed already loaded), so one RCCL instance serves both communicators and
-// liblgx.so carries no link-time dependency on it.
+// liblgx.so carries no link-time dependency on it.  A loaded RCCL is never unloaded again (its
+// bootstrap and proxy threads live in it).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -72,7 +73,8 @@ int lgx_comm_unique_id(const char* rccl_path, uint8_t id[LGX_COMM_ID_BYTES]) {
   ncclUniqueId u;
   rc = rccl_status(api, api.get_unique_id(&u), "ncclGetUniqueId");
   if (!rc) memcpy(id, &u, sizeof u);
-  dlclose(api.handle);   // (the process keeps the library loaded while its communicators live)
+  // the library stays loaded (never dlclose'd once used): the unique id's bootstrap root thread
+  // runs inside it until the ranks have connected in lgx_comm_create
   return rc;
 }
 
@@ -86,14 +88,13 @@ int lgx_comm_create(const char* rccl_path, const uint8_t id[LGX_COMM_ID_BYTES], 
   int rc = rccl_open(rccl_path, c->api);
   if (rc) { delete c; return rc; }
   if (hipSetDevice(device) != hipSuccess) {
-    dlclose(c->api.handle);
     delete c;
     return lgx_fail(LGX_EHIP, "lgx_comm_create: hipSetDevice failed");
   }
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   rc = rccl_status(c->api, c->api.comm_init_rank(&c->comm, nranks, u, rank), "ncclCommInitRank");
-  if (rc) { dlclose(c->api.handle); delete c; return rc; }
+  if (rc) { delete c; return rc; }
   c->nranks = nranks;
   c->rank = rank;
   c->device = device;
@@ -104,7 +105,6 @@ int lgx_comm_create(const char* rccl_path, const uint8_t id[LGX_COMM_ID_BYTES], 
 int lgx_comm_destroy(lgx_comm* c) {
   if (!c) return 0;
   const int rc = rccl_status(c->api, c->api.comm_destroy(c->comm), "ncclCommDestroy");
-  dlclose(c->api.handle);
   delete c;
   return rc;
 }
