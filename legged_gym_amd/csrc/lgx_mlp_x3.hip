@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "lgx_device.h"
 #include "lgx_internal.h"
@@ -81,10 +82,11 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_
   l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
 }
 
-__device__ __forceinline__ float xm_act(float v, int act) {
-  if (act == 1) return lgx_elu(v);
-  if (act == 2) return tanhf(v);
-  return v;
+template <int ACT>
+__device__ __forceinline__ float xm_act_c(float v) {
+  if constexpr (ACT == 1) return lgx_elu(v);
+  else if constexpr (ACT == 2) return tanhf(v);
+  else return v;
 }
 
 // One load group of a wave's weight fragments: G = 4 / TPW k blocks x TPW column blocks x 3 limbs
@@ -286,41 +288,49 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
     LGX_CLK(1 + (l < 4 ? l : 3));
     // epilogue: lane holds row `row`, columns cb*32 + 8q + 4h + (0..3) in acc[t][4q .. 4q+3]
     const int rs_out = xm_rs(N);
+    // (the activation is dispatched once per layer, not per value: a per-value test of a.act
+    // reloaded it from the kernel arguments with an lgkmcnt(0) wait behind the LDS stores)
+    auto epilogue = [&](auto act_c) {
+      constexpr int AC = decltype(act_c)::value;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (t >= tpw) break;
-      const int cb = wave + XM_NW * t;
+      for (int t = 0; t < 2; ++t) {
+        if (t >= tpw) break;
+        const int cb = wave + XM_NW * t;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int c0 = cb * 32 + 8 * q + 4 * h;
-        float v[4];
-        const float4 bq = *reinterpret_cast<const float4*>(bias_lds + boff + c0);   // (zero past N)
-        v[0] = acc[t][4 * q] + bq.x;
-        v[1] = acc[t][4 * q + 1] + bq.y;
-        v[2] = acc[t][4 * q + 2] + bq.z;
-        v[3] = acc[t][4 * q + 3] + bq.w;
-        if (!last) {   // padding columns: zero weights and bias -> act(0) = 0
+        for (int q = 0; q < 4; ++q) {
+          const int c0 = cb * 32 + 8 * q + 4 * h;
+          float v[4];
+          const float4 bq = *reinterpret_cast<const float4*>(bias_lds + boff + c0);   // (zero past N)
+          v[0] = acc[t][4 * q] + bq.x;
+          v[1] = acc[t][4 * q + 1] + bq.y;
+          v[2] = acc[t][4 * q + 2] + bq.z;
+          v[3] = acc[t][4 * q + 3] + bq.w;
+          if (!last) {   // padding columns: zero weights and bias -> act(0) = 0
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = xm_act(v[i], a.act);
-          uint32_t a0, a1, a2, b0, b1, b2;
-          split2(v[0], v[1], a0, a1, a2);
-          split2(v[2], v[3], b0, b1, b2);
-          char* p = out + row * rs_out + 2 * c0;
-          *reinterpret_cast<uint2*>(p) = make_uint2(a0, b0);
-          *reinterpret_cast<uint2*>(p + XM_BM * rs_out) = make_uint2(a1, b1);
-          *reinterpret_cast<uint2*>(p + 2 * XM_BM * rs_out) = make_uint2(a2, b2);
-        } else {
-          const int64_t gr = r0 + row;
-          if (gr < a.rows) {
+            for (int i = 0; i < 4; ++i) v[i] = xm_act_c<AC>(v[i]);
+            uint32_t a0, a1, a2, b0, b1, b2;
+            split2(v[0], v[1], a0, a1, a2);
+            split2(v[2], v[3], b0, b1, b2);
+            char* p = out + row * rs_out + 2 * c0;
+            *reinterpret_cast<uint2*>(p) = make_uint2(a0, b0);
+            *reinterpret_cast<uint2*>(p + XM_BM * rs_out) = make_uint2(a1, b1);
+            *reinterpret_cast<uint2*>(p + 2 * XM_BM * rs_out) = make_uint2(a2, b2);
+          } else {
+            const int64_t gr = r0 + row;
+            if (gr < a.rows) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-              if (c0 + i < N) a.y[gr * N + c0 + i] = v[i];
+              for (int i = 0; i < 4; ++i)
+                if (c0 + i < N) a.y[gr * N + c0 + i] = v[i];
+            }
+            if (ACT && net == 0 && c0 < XM_ACT_A)   // the means for the act epilogue
+              *reinterpret_cast<float4*>(act_lds + row * XM_ACT_A + c0) = make_float4(v[0], v[1], v[2], v[3]);
           }
-          if (ACT && net == 0 && c0 < XM_ACT_A)   // the means for the act epilogue
-            *reinterpret_cast<float4*>(act_lds + row * XM_ACT_A + c0) = make_float4(v[0], v[1], v[2], v[3]);
         }
       }
-    }
+    };
+    if (!last && a.act == 1) epilogue(std::integral_constant<int, 1>{});
+    else if (!last && a.act == 2) epilogue(std::integral_constant<int, 2>{});
+    else epilogue(std::integral_constant<int, 0>{});   // (the output layer has no activation)
     if (!last) {   // image columns past the column blocks (up to the 64-padded width) are zero
       const int c_lo = ncb * 32, kpo = xm_kp(N);
       const int wpairs = (kpo - c_lo) / 2;
