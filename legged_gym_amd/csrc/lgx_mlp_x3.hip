@@ -296,11 +296,17 @@ __global__ void __launch_bounds__(XM_NT) lgx_mlp_x3_kernel(XmBatch batch, int32_
       for (int t = 0; t < 2; ++t) {
         if (t >= tpw) break;
         const int cb = wave + XM_NW * t;
+        // the block's four bias quads read before any image store: the stores may alias the bias
+        // rows as far as the compiler knows, so a read after them waits for all of them
+        float4 bqs[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          bqs[q] = *reinterpret_cast<const float4*>(bias_lds + boff + cb * 32 + 8 * q + 4 * h);   // (zero past N)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int c0 = cb * 32 + 8 * q + 4 * h;
           float v[4];
-          const float4 bq = *reinterpret_cast<const float4*>(bias_lds + boff + c0);   // (zero past N)
+          const float4 bq = bqs[q];
           v[0] = acc[t][4 * q] + bq.x;
           v[1] = acc[t][4 * q + 1] + bq.y;
           v[2] = acc[t][4 * q + 2] + bq.z;
