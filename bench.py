@@ -201,6 +201,10 @@ def parse():
     p.add_argument("--cpu_envs", type=int, default=4096)
     p.add_argument("--actuator_net_torques", action="store_true",
                    help="ANYmal: the SEA actuator network as the torque source (cfg.control.explicit_torques)")
+    p.add_argument("--rendezvous_only", action="store_true",
+                   help="launch contract check without a GPU: every rank joins a gloo group, the ranks are counted "
+                        "with an all-reduce, rank 0 prints them; LGX_BENCH_FAIL_RANK=r makes rank r exit with code 3 "
+                        "after the count (tests/test_bench_cli.py: the launcher's exit code carries one rank's failure)")
     return p.parse_args()
 
 
@@ -409,6 +413,27 @@ def launch_ranks(n):
     return subprocess.run(cmd, env=env).returncode
 
 
+def rendezvous_check(world, rank):
+    """--rendezvous_only: the ranks' gloo rendezvous on CPU (no GPU touched); returns the rank's
+    exit code."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    seen = torch.ones(1)
+    if world > 1:
+        dist.all_reduce(seen)
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"rendezvous": "gloo", "world": world, "ranks_seen": int(seen.item())}))
+        sys.stdout.flush()
+    fail = os.environ.get("LGX_BENCH_FAIL_RANK")
+    code = 3 if fail is not None and int(fail) == rank else 0
+    if world > 1:
+        dist.destroy_process_group()
+    return code
+
+
 def main():
     args = parse()
     if args.gpus < 1:
@@ -427,6 +452,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rendezvous_only:
+        sys.exit(rendezvous_check(world, rank))
     # one rank per GPU (identity on a full node); LGX_DIST_BACKEND=gloo with more ranks than GPUs
     # rehearses the data-parallel path on a single device
     backend = os.environ.get("LGX_DIST_BACKEND", "nccl")
@@ -616,8 +643,7 @@ def main():
     if rank == 0:
         print(json.dumps(out))
     if distributed:
-        if fused is not None:
-            fused.close_comm()
+        runner.close()
         dist.destroy_process_group()
 
 

@@ -360,6 +360,14 @@ int lgx_ground_contact(lgx_sim* sim, const float* points, int32_t n, float* out,
 /* post_physics_step only (legged_robot.py:109-141) on the current state buffers. */
 int lgx_post_physics(lgx_sim* sim, int64_t common_step_counter, void* stream);
 
+/* The post-physics half of lgx_step_from exactly as the step issues it after its physics launch
+ * (legged_robot.py:100-107 -> post_physics_step :109-141, with Go1's actuator_advance / UniNet,
+ * go1.py:79-107): for a task with the Go1 actuator net, ONE launch of post-physics workgroups plus
+ * actuator-net workgroups over the step's model_ins rows (into act_dvel); otherwise the same launch
+ * as lgx_post_physics.  On the current state buffers, so a golden replay (lgx_drive_inputs, scripted
+ * state, this call) pins the product step's own launch to the reference. */
+int lgx_post_physics_fused(lgx_sim* sim, int64_t common_step_counter, void* stream);
+
 /* reset_idx for the listed envs (legged_robot.py:150-193): dof/root reset, commands,
  * buffers, episode extras.  env_ids: device int32[n]. */
 int lgx_reset_idx(lgx_sim* sim, const int32_t* env_ids, int32_t n, int64_t common_step_counter,

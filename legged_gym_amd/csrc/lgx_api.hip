@@ -192,7 +192,11 @@ int lgx_sim_create(const lgx_model* model, const lgx_env_params* params, const l
   // of its own inside the post-physics launch, 1 = its own launch on an auxiliary stream, 0 = its
   // own launch on the caller's stream (the PMC passes that measure it alone)
   const char* am = getenv("LGX_ACT_OVERLAP");
-  s->act_mode = am ? atoi(am) : 2;
+  s->act_mode = am && *am ? atoi(am) : 2;
+  if (s->act_mode < 0 || s->act_mode > 2 || (am && *am && (am[0] < '0' || am[0] > '2' || am[1]))) {
+    delete s;
+    return fail(LGX_EINVAL, "lgx_sim_create: LGX_ACT_OVERLAP must be 0, 1 or 2");
+  }
   s->num_points = model->num_points;
   s->params = *params;
   s->bufs = *bufs;
@@ -342,6 +346,8 @@ int lgx_post_physics(lgx_sim* s, int64_t step, void* stream) {
                       "lgx_post_physics: launch");
 }
 
+static int post_physics_fused(lgx_sim* s, int64_t step, hipStream_t st, bool sample);
+
 int lgx_step(lgx_sim* s, int64_t step, void* stream) { return lgx_step_from(s, nullptr, step, stream); }
 
 int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) {
@@ -356,6 +362,14 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
   arm(s, 0, sample);
   rc = launch_check(physics(s, p.decimation, 1, actions, st, 0), "lgx_step: physics launch");
   if (rc) return rc;
+  return post_physics_fused(s, step, st, sample);
+}
+
+// the second launch(es) of lgx_step_from: post-physics with the Go1 actuator net over this step's
+// model_ins - one launch by default (act_mode 2), or the actuator on its own launch / stream
+static int post_physics_fused(lgx_sim* s, int64_t step, hipStream_t st, bool sample) {
+  const lgx_env_params& p = s->params;
+  int rc = 0;
   const bool act_net = p.use_actuator_history && s->bufs.act_net_w && s->bufs.act_dvel;
   const int mode = s->act_mode;
   if (act_net && mode == 2) {
@@ -397,9 +411,14 @@ int lgx_step_from(lgx_sim* s, const float* actions, int64_t step, void* stream) 
     }
   }
   arm(s, 2, sample);
-  rc = lgx_post_physics(s, step, stream);
+  rc = lgx_post_physics(s, step, st);
   lgx_timing = lgx_timing_slot{};
   return rc;
+}
+
+int lgx_post_physics_fused(lgx_sim* s, int64_t step, void* stream) {
+  if (!s) return fail(LGX_EINVAL, "lgx_post_physics_fused: null sim");
+  return post_physics_fused(s, step, (hipStream_t)stream, false);
 }
 
 int lgx_profile_enable(lgx_sim* s, int32_t on) {

@@ -65,8 +65,11 @@ class LgxBackend:
         self._check(self.lib.lgx_drive_inputs(self.handle, C.c_void_p(actions.data_ptr()) if actions is not None
                                               else None, self.stream()), "lgx_drive_inputs")
 
-    def post_physics(self, counter):
-        self._check(self.lib.lgx_post_physics(self.handle, counter, self.stream()), "lgx_post_physics")
+    def post_physics(self, counter, fused=False):
+        if fused:   # the post-physics launch of lgx_step_from (with the Go1 actuator net when configured)
+            self._check(self.lib.lgx_post_physics_fused(self.handle, counter, self.stream()), "lgx_post_physics_fused")
+        else:
+            self._check(self.lib.lgx_post_physics(self.handle, counter, self.stream()), "lgx_post_physics")
 
     def reset_idx(self, ids_i32, counter, init_done):
         self._check(self.lib.lgx_reset_idx(self.handle, C.c_void_p(ids_i32.data_ptr()), ids_i32.numel(), counter,
@@ -139,12 +142,17 @@ class LeggedRobot(BaseTask):
         self._publish_extras(snap)
         return self.obs_buf, self.privileged_obs_buf, self.rew_buf, self.reset_buf, self.extras
 
-    def post_physics_step(self):
-        """legged_robot.py:109-141 on the current physics state (no physics)."""
+    def post_physics_step(self, fused=False):
+        """legged_robot.py:109-141 on the current physics state (no physics).  fused=True issues it
+        as `step` does after its physics launch (lgx_post_physics_fused: the Go1 actuator net over
+        this step's model_ins in the same launch)."""
         self._next_obs_buffer()
         snap = self._next_extras_snapshot()
         self.common_step_counter += 1
-        self._backend.post_physics(self.common_step_counter)
+        if fused:
+            self._backend.post_physics(self.common_step_counter, fused=True)
+        else:
+            self._backend.post_physics(self.common_step_counter)
         self._publish_extras(snap)
 
     def simulate(self, n=1):

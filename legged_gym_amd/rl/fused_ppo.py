@@ -516,6 +516,15 @@ class FusedPPOUpdate:
         colsum = getattr(self, "colsum", {})
         if 0 in colsum:   # db_1 from dW1's column sums: complete with dW1
             job(colsum[0], self.bo[0], h[0], 2, Sk[0] * h[0], Sk[0], h[0], h[0])
+        elif self.L > 1:
+            # db_1 from the dA_1 GEMM's ELU' + column-sum partials (dW1 not on lgx_gemm_tn: e.g. 48 or
+            # 169 observations, whose padded rows are narrower than dW1's 128-column tiles).  dA_1 runs
+            # on the main stream after the side stream's last join, so this job belongs with dW1's on
+            # the main stream: reduced after dA_1, and inside the [0, nW1) all-reduce bucket that is
+            # issued from the main stream (in the side stream's early reduction it would read the
+            # partials before dA_1 wrote them)
+            cchunks = self.col_parts[0].numel() // (2 * h[0])
+            job(self.col_parts[0], self.bo[0], 2 * h[0], 1, 0, cchunks, 2 * h[0], 0)
         n_dw1 = len(jobs)   # (the layer-1 jobs come first: the rest can be reduced before dW1 is done)
         for k in range(1, self.L):
             nk = h[k] * h[k - 1]
@@ -525,10 +534,9 @@ class FusedPPOUpdate:
         job(self.head_parts, self.Wg[self.L], (A + 1) * h[-1], 1, 0, hchunks, nh, 0)  # dW head (actor | critic)
         hp_b = self.head_parts[(A + 1) * h[-1]:]
         job(hp_b, self.bo[self.L - 1], 2 * h[-1], 1, 0, hchunks, nh, 0)              # db of the last hidden layer
-        for k in range(self.L - 1):
-            if k in colsum:
-                if k > 0:                                                            # db_k from dW_k's column sums
-                    job(colsum[k], self.bo[k], h[k], 2, Sk[k] * h[k], Sk[k], h[k], h[k])
+        for k in range(1, self.L - 1):   # (db_1 is with the layer-1 jobs above)
+            if k in colsum:                                                          # db_k from dW_k's column sums
+                job(colsum[k], self.bo[k], h[k], 2, Sk[k] * h[k], Sk[k], h[k], h[k])
                 continue
             cchunks = self.col_parts[k].numel() // (2 * h[k])
             job(self.col_parts[k], self.bo[k], 2 * h[k], 1, 0, cchunks, 2 * h[k], 0)  # db_k
@@ -540,7 +548,9 @@ class FusedPPOUpdate:
         self.jobs_rest = (abi.LgxReduceJob * (len(jobs) - n_dw1))(*jobs[n_dw1:])
         # every input of jobs_rest comes from the side stream's dW launches (partials, column sums)
         # or from launches on the main stream before the side stream's first join (loss): the
-        # early reduction then needs no join after the dA GEMMs
+        # early reduction then needs no join after the dA GEMMs.  (db_k from a dA epilogue, k >= 2,
+        # is written on the main stream after a join: then the join is needed; db_1 is never in
+        # jobs_rest.)
         self.rest_on_side = all(k in colsum for k in range(1, self.L - 1))
         # the clip norm's sums of squares written by the reduction launches themselves
         # (lgx_reduce_slices_sq; single-process updates with the fused loss): one launch less per minibatch
@@ -754,10 +764,17 @@ class FusedPPOUpdate:
             return self._comm
         self._comm = None
         dist = self.ppo.dist
-        if os.environ.get("LGX_NATIVE_ALLREDUCE", "0") != "1" or dist.get_backend() != "nccl":
+        if os.environ.get("LGX_NATIVE_ALLREDUCE", "0") != "1":
             return None
+        # asked for: fail loudly rather than fall back to torch.distributed (the 8-GPU run must use
+        # the path it was configured for) or load an RCCL other than the one torch's nccl backend runs
+        if dist.get_backend() != "nccl":
+            raise RuntimeError(f"LGX_NATIVE_ALLREDUCE=1 needs the nccl (RCCL) process group, got {dist.get_backend()!r}")
         path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        path = path.encode() if os.path.exists(path) else None
+        if not os.path.exists(path):
+            raise RuntimeError(f"LGX_NATIVE_ALLREDUCE=1: torch's RCCL ({path}) is missing; refusing to load another "
+                               "RCCL instance into the process")
+        path = path.encode()
         uid = torch.zeros(128, dtype=torch.uint8)
         if dist.get_rank() == 0:
             self.check(self.lib.lgx_comm_unique_id(path, C.cast(uid.data_ptr(), C.POINTER(C.c_uint8))),

@@ -233,3 +233,10 @@ class OnPolicyRunner:
         if device is not None:
             self.alg.actor_critic.to(device)
         return self.alg.actor_critic.act_inference
+
+    def close(self):
+        """Release the update's collective resources (the lgx RCCL communicator of
+        LGX_NATIVE_ALLREDUCE=1; collective: every rank calls it after its last learn())."""
+        fused = getattr(self.alg, "_fused", None)
+        if fused is not None:
+            fused.close_comm()

@@ -24,7 +24,12 @@ def train(args):
     env, env_cfg = task_registry.make_env(name=args.task, args=args)
     log_root = None if (world > 1 and int(os.environ.get("RANK", "0")) != 0) else "default"
     ppo_runner, train_cfg = task_registry.make_alg_runner(env=env, name=args.task, args=args, log_root=log_root)
-    ppo_runner.learn(num_learning_iterations=train_cfg.runner.max_iterations, init_at_random_ep_len=True)
+    try:
+        ppo_runner.learn(num_learning_iterations=train_cfg.runner.max_iterations, init_at_random_ep_len=True)
+    finally:
+        ppo_runner.close()
+        if world > 1:
+            torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

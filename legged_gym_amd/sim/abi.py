@@ -170,6 +170,7 @@ def declare(lib, prefix="lgx"):
         "step": (C.c_int, [vp, i64, vp]),
         "simulate": (C.c_int, [vp, i32, vp]),
         "post_physics": (C.c_int, [vp, i64, vp]),
+        "post_physics_fused": (C.c_int, [vp, i64, vp]),
         "reset_idx": (C.c_int, [vp, vp, i32, i64, i32, vp]),
         "set_draws": (C.c_int, [vp, vp]),
         "rebind_obs": (C.c_int, [vp, vp]),
@@ -254,7 +255,7 @@ def declare(lib, prefix="lgx"):
 
 
 EXPORTED = ["lgx_last_error", "lgx_version", "lgx_physics_lane_split", "lgx_trimesh_build", "lgx_struct_sizes", "lgx_scratch_floats", "lgx_sim_create",
-            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_sim_buffer", "lgx_step_from", "lgx_drive_inputs", "lgx_ground_contact", "lgx_sync_aux",
+            "lgx_sim_destroy", "lgx_step", "lgx_simulate", "lgx_post_physics", "lgx_post_physics_fused", "lgx_reset_idx", "lgx_set_draws", "lgx_rebind_obs", "lgx_rebind_extras", "lgx_sim_buffer", "lgx_step_from", "lgx_drive_inputs", "lgx_ground_contact", "lgx_sync_aux",
             "lgx_actuator_mlp", "lgx_actuator_lstm", "lgx_mlp_forward", "lgx_gae", "lgx_gae_norm_scratch", "lgx_gae_norm", "lgx_gae_parts", "lgx_adv_norm",
             "lgx_profile_enable", "lgx_profile_collect", "lgx_mlp_forward_batch",
             "lgx_ppo_gather_rows", "lgx_bias_act", "lgx_ppo_loss_partials_floats", "lgx_ppo_loss", "lgx_ppo_adapt_lr",

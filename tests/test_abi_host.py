@@ -52,6 +52,30 @@ def test_comm_entry_points_validate_without_a_gpu():
     assert lib.lgx_comm_destroy(None) == 0
 
 
+def test_native_allreduce_refuses_to_fall_back(monkeypatch):
+    """LGX_NATIVE_ALLREDUCE=1 on a process group that is not RCCL raises instead of silently using
+    torch.distributed; unset, the torch path is taken (no communicator)."""
+    import pytest
+    from legged_gym_amd.rl.fused_ppo import FusedPPOUpdate
+
+    class Dist:
+        @staticmethod
+        def get_backend():
+            return "gloo"
+
+    class Ppo:
+        dist = Dist()
+    f = FusedPPOUpdate.__new__(FusedPPOUpdate)
+    f.ppo = Ppo()
+    monkeypatch.delenv("LGX_NATIVE_ALLREDUCE", raising=False)
+    assert f._lgx_comm() is None and f.allreduce_impl == "torch"
+    f = FusedPPOUpdate.__new__(FusedPPOUpdate)
+    f.ppo = Ppo()
+    monkeypatch.setenv("LGX_NATIVE_ALLREDUCE", "1")
+    with pytest.raises(RuntimeError, match="nccl"):
+        f._lgx_comm()
+
+
 def test_oracle_layout_matches():
     from oracle_backend import load_oracle
     load_oracle()  # check_layout inside

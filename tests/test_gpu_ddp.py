@@ -18,25 +18,25 @@ pytestmark = pytest.mark.gpu
 T, B, OBS, ACT = 4, 512, 235, 12
 
 
-def _data():
+def _data(obs=OBS):
     g = torch.Generator().manual_seed(3)
-    return dict(obs=torch.randn(T, 2 * B, OBS, generator=g), act=torch.randn(T, 2 * B, ACT, generator=g),
+    return dict(obs=torch.randn(T, 2 * B, obs, generator=g), act=torch.randn(T, 2 * B, ACT, generator=g),
                 rew=torch.randn(T, 2 * B, 1, generator=g), done=(torch.rand(T, 2 * B, 1, generator=g) < 0.1).byte(),
                 val=torch.randn(T, 2 * B, 1, generator=g), logp=torch.randn(T, 2 * B, 1, generator=g) * 0.3 - 17,
                 mu=torch.randn(T, 2 * B, ACT, generator=g) * 0.1, sigma=torch.rand(T, 2 * B, ACT, generator=g) * .5 + .75,
                 last=torch.randn(2 * B, 1, generator=g))
 
 
-def _make(n_envs, sl):
+def _make(n_envs, sl, obs=OBS):
     from legged_gym_amd.rl.actor_critic import ActorCritic
     from legged_gym_amd.rl.ppo import PPO
     torch.manual_seed(0)
-    ac = ActorCritic(OBS, OBS, ACT, [512, 256, 128], [512, 256, 128])
+    ac = ActorCritic(obs, obs, ACT, [512, 256, 128], [512, 256, 128])
     ppo = PPO(ac, num_learning_epochs=2, num_mini_batches=1, learning_rate=1e-3, gamma=0.99, lam=0.95,
               schedule="adaptive", entropy_coef=0.01, device="cuda:0")
     assert ppo._fused is not None
-    ppo.init_storage(n_envs, T, [OBS], [None], [ACT])
-    d = _data()
+    ppo.init_storage(n_envs, T, [obs], [None], [ACT])
+    d = _data(obs)
     st = ppo.storage
     for name, key in (("observations", "obs"), ("actions", "act"), ("rewards", "rew"), ("dones", "done"),
                       ("values", "val"), ("actions_log_prob", "logp"), ("mu", "mu"), ("sigma", "sigma")):
@@ -46,7 +46,7 @@ def _make(n_envs, sl):
     return ppo
 
 
-def _worker(rank, world, port, q, early):
+def _worker(rank, world, port, q, early, obs=OBS):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0",
                       LGX_PPO_EARLY_REDUCE=early)
@@ -54,7 +54,7 @@ def _worker(rank, world, port, q, early):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from ppo_trace import StepTrace
-        ppo = _make(B, slice(rank * B, (rank + 1) * B))
+        ppo = _make(B, slice(rank * B, (rank + 1) * B), obs)
         tr = StepTrace(ppo._fused)
         vl, sl = ppo.update()
         tr.close()
@@ -80,22 +80,27 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("early", ["1", "0"])
-def test_fused_update_two_ranks_equal_one_process(gpu, early):
+@pytest.mark.parametrize("early,obs", [("1", OBS), ("0", OBS), ("1", 48)])
+def test_fused_update_two_ranks_equal_one_process(gpu, early, obs):
     """Rank 0's trace of both optimizer steps (tests/ppo_trace.py): the averaged all-reduced
     gradient of step 1 (same parameters in both runs) == the one-process gradient per coordinate
     to 1e-6 + 1e-4 |g| (only the order of the two ranks' partial sums differs), every step ==
     float64 clip + Adam of its gradient (1e-6 + 1e-3 lr), the learning rate sequence identical, and
-    at the end all but <= 0.1 % of the coordinates within 1e-5 of the one-process run."""
+    at the end all but <= 0.1 % of the coordinates within 1e-5 of the one-process run.
+    obs = 48 (Go1 flat): the layer-1 weight gradient is not on lgx_gemm_tn (its padded rows are
+    narrower than the 128-column tiles), so db_1 comes from the dA_1 epilogue on the main stream
+    and is reduced and all-reduced there (it sat in the side stream's early reduction)."""
     from ppo_trace import StepTrace, adam64
-    ref = _make(2 * B, slice(0, 2 * B))
+    ref = _make(2 * B, slice(0, 2 * B), obs)
     tr = StepTrace(ref._fused)
     ref.update()
     tr.close()
+    if obs != OBS:
+        assert 0 not in ref._fused.gemm_dw and 0 not in ref._fused.colsum
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, early)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, early, obs)) for r in range(2)]
     for p in procs:
         p.start()
     got, steps = q.get(timeout=300)

@@ -495,6 +495,16 @@ def test_rough_terrain_step_matches_oracle(gpu, monkeypatch, act_mode):
     assert torch.equal(dev._extras_time_outs.cpu(), ora._extras_time_outs)
 
 
+@pytest.mark.parametrize("bad", ["3", "-1", "2x"])
+def test_unknown_act_overlap_is_refused(gpu, monkeypatch, bad):
+    """LGX_ACT_OVERLAP outside {0, 1, 2} (e.g. the removed split-bf16 actuator body, 3) is refused
+    by lgx_sim_create instead of silently running another mode."""
+    from legged_gym_amd.sim.lib import LgxError
+    monkeypatch.setenv("LGX_ACT_OVERLAP", bad)
+    with pytest.raises(LgxError, match="LGX_ACT_OVERLAP"):
+        make_env("go1_rough", num_envs=64, device="cuda:0", backend="lgx")
+
+
 def test_mlp_forward_batch_actor_critic(gpu):
     """act_and_evaluate (one batched launch) == torch autograd modules."""
     from legged_gym_amd.rl.actor_critic import ActorCritic

@@ -21,12 +21,12 @@ pytestmark = pytest.mark.gpu
 T, N, OBS, ACT = 6, 1024, 235, 12
 
 
-def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128), T=T, N=N, epochs=2):
+def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128), T=T, N=N, epochs=2, obs=OBS):
     """Reference (autograd) and fused PPO on identical storage; cobs = privileged critic
     observation width (None: the critic reads the actor's observations); T x N transitions in
     4 minibatches, `epochs` learning epochs."""
     torch.manual_seed(0)
-    ac = ActorCritic(OBS, cobs or OBS, ACT, list(hidden), list(hidden))
+    ac = ActorCritic(obs, cobs or obs, ACT, list(hidden), list(hidden))
     ac2 = copy.deepcopy(ac)
     kw = dict(num_learning_epochs=epochs, num_mini_batches=4, clip_param=0.2, gamma=0.99, lam=0.95, value_loss_coef=1.0,
               entropy_coef=0.01, learning_rate=1e-3, max_grad_norm=1.0, schedule=schedule, desired_kl=0.01,
@@ -35,10 +35,10 @@ def make_pair(schedule="adaptive", cobs=None, hidden=(512, 256, 128), T=T, N=N, 
     fus = PPO(ac2, use_fused_update=True, **kw)
     assert fus._fused is not None and ref._fused is None
     for p in (ref, fus):
-        p.init_storage(N, T, [OBS], [cobs], [ACT])
+        p.init_storage(N, T, [obs], [cobs], [ACT])
     g = torch.Generator(device="cuda:0").manual_seed(3)
     st = ref.storage
-    st.observations.copy_(torch.randn(T, N, OBS, device="cuda:0", generator=g))
+    st.observations.copy_(torch.randn(T, N, obs, device="cuda:0", generator=g))
     st.actions.copy_(torch.randn(T, N, ACT, device="cuda:0", generator=g))
     st.rewards.copy_(torch.randn(T, N, 1, device="cuda:0", generator=g))
     st.dones.copy_((torch.rand(T, N, 1, device="cuda:0", generator=g) < 0.1).byte())
@@ -519,6 +519,43 @@ def test_fused_update_every_step_is_exact(gpu, monkeypatch, schedule, cobs, algo
         assert ((rec["v1"].double() - v_want).abs() <= 2e-5 * v_want.abs() + 1e-18).all(), t
         if t > 0:   # every step starts from the previous step's result
             assert torch.equal(rec["p0"], tr.steps[t - 1]["p1"])
+
+
+@pytest.mark.parametrize("obs,cobs", [(48, None), (169, None), (48, 187)])
+def test_fused_update_narrow_inputs_every_step_is_exact(gpu, obs, cobs):
+    """Input widths whose padded layer-1 rows are narrower than lgx_gemm_tn's 128-column tiles
+    (Go1 flat 48, Cassie 169; a privileged critic of 187): dW1 then runs on the library bmm and db_1
+    comes from the dA_1 GEMM's column-sum epilogue on the main stream, after the side stream's last
+    join.  Its reduction goes with dW1's on the main stream (in the side stream's early
+    reduction it read the partials before dA_1 wrote them).  The default two-stream schedule, every
+    coordinate of every step as test_fused_update_every_step_is_exact."""
+    from ppo_trace import StepTrace, adam64, flat_view
+    for var in ("LGX_PPO_DW_SIDE", "LGX_PPO_EARLY_REDUCE", "LGX_PPO_SPLITS"):
+        assert var not in os.environ, var
+    ref, fus = make_pair("adaptive", cobs, T=24, N=1024, epochs=1, obs=obs)
+    f = fus._fused
+    tr = StepTrace(f)
+    torch.manual_seed(11)
+    fus.update()
+    tr.close()
+    assert 0 not in f.gemm_dw and 0 not in f.colsum and getattr(f, "_side", None) is not None
+    assert f.bo[0] in [j.dst // 4 - f.flat_g.data_ptr() // 4 for j in f.jobs_dw1]   # db_1 with dW1, main stream
+    torch.manual_seed(11)
+    ref.update()
+    assert fus.learning_rate == ref.learning_rate
+    params = list(ref.actor_critic.parameters())
+    for t, rec in enumerate(tr.steps):
+        with torch.no_grad():
+            for p, q in zip(params, f.optimizer.params):
+                off = f.off[id(q)]
+                p.copy_(rec["p0"][off:off + q.numel()].view_as(p))
+        g_ref = flat_view(f, list(autograd_grads(ref, rec["idx"]).values()))
+        g = rec["g"].double()
+        bad = ((g - g_ref).abs() > 1e-5 + 2e-3 * g_ref.abs()).sum().item()
+        assert bad == 0, (obs, t, bad, (g - g_ref).abs().max().item())
+        p_want, _, _ = adam64(rec, fus.max_grad_norm)
+        dp = (rec["p1"].double() - p_want).abs()
+        assert (dp <= 1e-6 + 1e-3 * rec["lr"]).all(), (obs, t, dp.max().item())
 
 
 @pytest.mark.parametrize("n_envs", [4096, 8192])
