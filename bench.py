@@ -71,7 +71,7 @@ def gemm_kernel_info(key, split):
     PPO GEMM launches timed under `key` (an lgx_gemm_nt epilogue, or "tn" = lgx_gemm_tn)."""
     pipe = "bf16 MFMA (v_mfma_f32_32x32x16_bf16), split-bf16: 6 limb products per f32 product"
     if key == "tn":
-        return "gemm_tn_x3_kernel<*>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
+        return "gemm_tn_*_kernel<*>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     if split:   # the pipelined kernel (lgx_gemm_x3p.hip)
         return f"gemm_nt_x3p_kernel<{key}, *>", pipe, MI355X_BF16_PEAK_TFLOPS / SPLIT_PRODUCTS
     return f"gemm_nt_kernel<8, {key}>", "f32 MFMA (v_mfma_f32_32x32x2_f32)", MI355X_F32_PEAK_TFLOPS
@@ -81,11 +81,12 @@ GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor 
               3: "lgx_gemm_nt LGX_GEMM_DELU: backward dA of the hidden layers (512x256 and 256x128 weights; the "
                  "bias gradients come from lgx_gemm_tn's column sums)",
               "tn": "lgx_gemm_tn: weight gradients dW_k = dZ_k^T Y_{k-1} of the hidden layers over row slices "
-                    "(512x235, 256x512, 128x256 per network)"}
+                    "(512x235, 256x512 on gemm_tn_x3_kernel<8>; 128x256 on the warp-specialised gemm_tn_ws_kernel<128>; "
+                    "per network)"}
 
 
 # the MFMA kernels of one iteration whose utilisation the bench line reports (PMC pass "mfma")
-MFMA_KERNELS = ["gemm_tn_x3_kernel<*>", "gemm_nt_x3p_kernel<1, *>", "gemm_nt_x3p_kernel<3, *>", "lgx_mlp_x3_kernel*",
+MFMA_KERNELS = ["gemm_tn_*_kernel<*>", "gemm_nt_x3p_kernel<1, *>", "gemm_nt_x3p_kernel<3, *>", "lgx_mlp_x3_kernel*",
                 "lgx_post_physics_act_kernel*"]
 
 
@@ -303,6 +304,12 @@ def cpu_baseline(task, n_envs):
                        f"ActorCritic/PPO, {share} threads; `runs` adds C1 / C2 and 1-thread runs "
                        f"({time.time() - t_all:.0f} s of baseline in total, warm-ups included)",
                 runs=runs, host=info)
+
+
+# LGX_BENCH_POSTHOC=0: skip the launches bench.py times after the timed region (the isolated dW and
+# standalone actuator-net launches), so that a rocprofv3 --stats summary of the run holds in-situ
+# launches only (tools/gpu_profile.sh prof step)
+POSTHOC = os.environ.get("LGX_BENCH_POSTHOC", "1") != "0"
 
 
 def isolated_tn(fused, torch, reps=20):
@@ -541,7 +548,7 @@ def main():
     if fused_act:
         # the actuator net shares the post-physics launch in the rollout; its own roofline is
         # measured on the same rows with the standalone launch (after the timed region)
-        avg[1], launches = standalone_actuator_ms(lib, env, torch)
+        avg[1], launches = standalone_actuator_ms(lib, env, torch) if POSTHOC else (0.0, 0)
         act_note = (f"standalone lgx_actuator_ws_kernel on this step's model_ins rows, {launches} launches after the "
                     "timed region (in the rollout it runs on workgroups of lgx_post_physics_act_kernel)")
     decim = env.cfg.control.decimation
@@ -591,7 +598,7 @@ def main():
             gemm_roofs[-1]["concurrent"] = True
             gemm_roofs[-1]["note"] += ("; launched on a second stream concurrently with the dA GEMMs: durations "
                                        "are co-resident times (the CUs are shared), not the isolated kernel rate")
-            iso = isolated_tn(fused, torch)
+            iso = isolated_tn(fused, torch) if POSTHOC else None
             if iso:
                 f_iso, ms_iso, n_iso = iso
                 gemm_roofs[-1]["isolated"] = {

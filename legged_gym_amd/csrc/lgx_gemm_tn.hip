@@ -73,12 +73,7 @@ struct TnArgs {
 };
 
 __device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
-  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){x0, x1}, bf16x2));
-  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
-  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
-  r0 -= __uint_as_float(l1 << 16);
-  r1 -= __uint_as_float(l1 & 0xffff0000u);
-  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+  lgx_split2(x0, x1, l0, l1, l2);   // (lgx_internal.h)
 }
 
 // staged row (m, column quad cq) of one operand into its limb image [limb][32 m][W cols]: split,
@@ -295,6 +290,258 @@ __global__ void __launch_bounds__(64 * NWV, 1) gemm_tn_x3_kernel(TnArgs g) {
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Warp-specialised form, used for the 128-row tiles (dW3 of the update; LGX_TN_WS=0 selects the
+// 4-wave gemm_tn_x3_kernel<4> there, LGX_TN_WS=2 this form for the 256-row tiles too).  In the form
+// above every wave both stages operands (global loads, the f32 -> limb split, LDS image writes) and
+// issues MFMAs.  Here the roles are split between the two waves of each SIMD:
+//   * consumers, waves 0-3 (one per SIMD, the older: they win issue arbitration): 32 WI x 128
+//     output block each, an instruction stream of transposed fragment reads and MFMAs only - the
+//     next B column block's fragments (and at j = 1 the next half's A fragments) are read under the
+//     current block's 6 WI MFMAs;
+//   * producers, waves 4-7: the global loads two stages ahead, the split and the limb-image writes
+//     of the next stage, the column sums - in the consumers' MFMA gaps.
+// Same LDS images (two stage buffers), one barrier per stage for all 8 waves, and the same products
+// in the same order per output element: bitwise the results of gemm_tn_x3_kernel.
+// Measured (round 6, isolated, half-GPU row slices, s_memtime per stage of workgroup 0):
+//   * 128-row tiles (dW3, R = 128): 64.6 vs 69.2 us for the 4-wave kernel (S = 16), 36.4 vs 38.8 us (S = 32);
+//   * 256-row tiles (dW1 / dW2): 122 vs 115-120 us (S = 16) - the producers are the bound: 4,877 cycles
+//     per stage to stage 12,288 floats (4,824 with the consumers' MFMAs running, 2,726 without them)
+//     against the consumers' 3,706 (96 MFMAs: 3,072-cycle floor).  The split VALU of a 256 x 128 tile
+//     stage does not fit one wave per SIMD; the 8-wave kernel spreads it over both waves.
+template <int RA>
+struct TW {
+  static constexpr int WI = RA / 128;                // 32-row A blocks per consumer wave (2 | 1)
+  static constexpr int IMGA = 3 * TK * RA * 2;
+  static constexpr int IMGB = 3 * TK * TT * 2;
+  static constexpr int STAGE = IMGA + IMGB;
+  static constexpr int AQ = RA / 4;                  // A column quads per row (64 | 32)
+  static constexpr int AR = TK * AQ / 256;           // staged A rows per producer thread (8 | 4)
+  static constexpr int BR = TK * (TT / 4) / 256;     // staged B rows per producer thread (4)
+  static constexpr int AROW = 256 / AQ;              // producer row groups (4 | 8)
+  static constexpr int CS = AROW * AQ * 16;          // column-sum scratch
+  static constexpr int LDS = 2 * STAGE + CS;         // 148 KB | 100 KB
+  static_assert(WI * 128 == RA && AR * AROW == TK && BR == 4, "layout");
+};
+
+// Tile coordinates of persistent tile `tile` (column tiles of one (n, s, z) adjacent)
+struct TnTile {
+  int ctile, ntile, s, z;
+};
+__device__ __forceinline__ TnTile tn_tile(const TnArgs& g, int32_t t) {
+  TnTile T;
+  T.ctile = t % g.ct;
+  t /= g.ct;
+  T.ntile = t % g.rt;
+  t /= g.rt;
+  T.s = t % g.S;
+  T.z = t / g.S;
+  return T;
+}
+
+// The two roles run separate loops over the same tiles and stages (so that neither role's
+// registers are live in the other's: the accumulators and the staging registers would not fit one
+// wave together) with the same barrier sequence: per tile one after the first stage's image
+// writes, one per stage, and one before the column sums are combined.
+template <int RA>
+__device__ __forceinline__ void tn_ws_consumer(const TnArgs& g, char* tlds, int wave, int lane, int32_t lo, int32_t hi,
+                                               int32_t stride, int nst) {
+  using X = TW<RA>;
+  constexpr int WI = X::WI;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = (lane >> 2) & 3, p = lane & 3, gb = (lane >> 4) & 1;
+  const int lane_a = (8 * h + q) * (RA * 2) + (4 * gb + p) * 8;
+  const int lane_b = (8 * h + q) * (TT * 2) + (4 * gb + p) * 8;
+  int xa[WI], xb[4];
+#pragma unroll
+  for (int i = 0; i < WI; ++i) xa[i] = 64 * ((WI * wave + i) ^ q);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) xb[j] = 64 * (j ^ q);
+  for (int32_t tile = lo + (blockIdx.x >> 3); tile < hi; tile += stride) {
+    const TnTile T = tn_tile(g, tile);
+    f32x16 acc[WI][4];
+#pragma unroll
+    for (int i = 0; i < WI; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    __syncthreads();   // stage 0 written
+#ifdef TN_WS_CLOCK   // A/B instrumentation: s_memtime at each stage's start / end (after / before its
+                     // barriers) of workgroup 0's first tile, waves 0 and 4, into the tail of g.C
+    uint64_t* clk = (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && tile == lo + (blockIdx.x >> 3) && wave == 0)
+                        ? reinterpret_cast<uint64_t*>(g.C + (int64_t)g.batch * g.S * g.R * g.ldc) : nullptr;
+#endif
+    for (int k = 0; k < nst; ++k) {
+#ifdef TN_WS_CLOCK
+      if (clk && k < 32) clk[k * 4 + 0] = __builtin_amdgcn_s_memtime();
+#endif
+      const char* ia = tlds + (k & 1) * X::STAGE;
+      const char* ib = ia + X::IMGA;
+      bf16x8 fa[2][WI][3], fb[2][3];
+      auto read_a = [&](int buf, int hs) {
+#pragma unroll
+        for (int i = 0; i < WI; ++i)
+#pragma unroll
+          for (int l = 0; l < 3; ++l) fa[buf][i][l] = tn_frag<RA>(ia, l, hs, lane_a, xa[i]);
+      };
+      auto read_b = [&](int buf, int hs, int j) {
+#pragma unroll
+        for (int l = 0; l < 3; ++l) fb[buf][l] = tn_frag<TT>(ib, l, hs, lane_b, xb[j]);
+      };
+      read_a(0, 0);
+      read_b(0, 0, 0);
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int cb = (4 * hs + j) & 1;   // B fragment buffer of (hs, j)
+          // the next block's fragments under this block's MFMAs
+          if (j < 3) read_b(cb ^ 1, hs, j + 1);
+          else if (hs == 0) read_b(cb ^ 1, 1, 0);
+          if (hs == 0 && j == 1) read_a(1, 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int i = 0; i < WI; ++i) {
+            f32x16 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs][i][2], fb[cb][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs][i][1], fb[cb][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs][i][0], fb[cb][2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs][i][1], fb[cb][0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs][i][0], fb[cb][1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[hs][i][0], fb[cb][0], c, 0, 0, 0);
+            acc[i][j] = c;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#ifdef TN_WS_CLOCK
+      if (clk && k < 32) clk[k * 4 + 1] = __builtin_amdgcn_s_memtime();
+#endif
+      __syncthreads();   // stage k read; stage k+1 written
+    }
+    if (g.colsum != nullptr && T.ctile == 0) __syncthreads();   // (the producers' column-sum exchange)
+    // acc[i][j][e] = C[n0 + 32 i + 8 (e >> 2) + 4 h + (e & 3)][c0 + 32 j + r]
+    float* Cb = g.C + ((int64_t)(T.z * g.S + T.s) * g.R + T.ntile * RA + wave * 32 * WI) * g.ldc;
+    const int c0 = T.ctile * TT + r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + 32 * j;
+      if (c >= g.Cc) continue;
+#pragma unroll
+      for (int i = 0; i < WI; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+          Cb[(int64_t)n * g.ldc + c] = acc[i][j][e];
+        }
+    }
+  }
+}
+
+// Producer: the staged rows of TWO stages in registers (loads two stages ahead of their image
+// writes: measured alone, the producers with one stage in flight took as long per stage as the
+// consumers' MFMA floor - latency-bound on the global loads)
+template <int RA>
+__device__ __forceinline__ void tn_ws_producer(const TnArgs& g, char* tlds, int pt, int32_t lo, int32_t hi,
+                                               int32_t stride, int nst) {
+  using X = TW<RA>;
+  const int aq = pt % X::AQ, am = pt / X::AQ;   // A thread: column quad aq, rows AR am ..
+  const int bq = pt & 31, bm = pt >> 5;         // B thread: column quad bq, rows 4 bm ..
+  const uint32_t sta = (uint32_t)(g.lda * 4), stb = (uint32_t)(g.ldb * 4);
+  for (int32_t tile = lo + (blockIdx.x >> 3); tile < hi; tile += stride) {
+    const TnTile T = tn_tile(g, tile);
+    const int64_t m0 = (int64_t)T.s * g.Ms;
+    const char* Ab = reinterpret_cast<const char*>(g.A + T.z * g.sa + m0 * g.lda + T.ntile * RA);
+    const char* Bb = reinterpret_cast<const char*>(g.B + T.z * g.sb + m0 * g.ldb + T.ctile * TT);
+    const uint32_t oa = (X::AR * am) * sta + aq * 16, ob = (X::BR * bm) * stb + bq * 16;
+    const bool csum = g.colsum != nullptr && T.ctile == 0;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 sa[2][X::AR], sb[2][X::BR];   // register ring of two stages
+    auto load = [&](float4 (&ra)[X::AR], float4 (&rb)[X::BR], int k) {
+      const uint32_t la = oa + min(k, nst - 1) * TK * sta, lb = ob + min(k, nst - 1) * TK * stb;
+#pragma unroll
+      for (int i = 0; i < X::AR; ++i) ra[i] = *reinterpret_cast<const float4*>(Ab + la + i * sta);
+#pragma unroll
+      for (int i = 0; i < X::BR; ++i) rb[i] = *reinterpret_cast<const float4*>(Bb + lb + i * stb);
+    };
+    // stage k (registers ra / rb) into buffer k & 1; each staged row's reload for stage k + 2 right
+    // after its write (past the last stage: re-loads of stage nst - 1, never written)
+    auto write_reload = [&](float4 (&ra)[X::AR], float4 (&rb)[X::BR], int k) {
+      char* nb = tlds + (k & 1) * X::STAGE;
+      const int kl = min(k + 2, nst - 1);
+      const uint32_t la = oa + kl * TK * sta, lb = ob + kl * TK * stb;
+#pragma unroll
+      for (int i = 0; i < X::AR; ++i) {
+        cs.x += ra[i].x; cs.y += ra[i].y; cs.z += ra[i].z; cs.w += ra[i].w;
+        tn_store_row<RA>(nb, ra[i], aq, X::AR * am + i);
+        ra[i] = *reinterpret_cast<const float4*>(Ab + la + i * sta);
+      }
+#pragma unroll
+      for (int i = 0; i < X::BR; ++i) {
+        tn_store_row<TT>(nb + X::IMGA, rb[i], bq, X::BR * bm + i);
+        rb[i] = *reinterpret_cast<const float4*>(Bb + lb + i * stb);
+      }
+    };
+    load(sa[0], sb[0], 0);
+    load(sa[1], sb[1], 1);
+    // stage 0 into buffer 0 (its readers finished at the previous tile's last barrier); stage 2 in
+    // flight behind stage 1
+    write_reload(sa[0], sb[0], 0);
+    __syncthreads();   // stage 0 written
+    // iteration k: stage k + 1 into the other buffer (its readers finished stage k - 1 at the last
+    // barrier) from ring entry (k + 1) & 1, which then loads stage k + 3
+#ifdef TN_WS_CLOCK
+    uint64_t* clk = (blockIdx.x == 0 && (pt & 63) == 0 && tile == lo + (blockIdx.x >> 3) && pt == 0)
+                        ? reinterpret_cast<uint64_t*>(g.C + (int64_t)g.batch * g.S * g.R * g.ldc) : nullptr;
+#define TN_PSTAMP(kk, e) if (clk && (kk) < 32) clk[(kk) * 4 + (e)] = __builtin_amdgcn_s_memtime()
+#else
+#define TN_PSTAMP(kk, e)
+#endif
+    for (int k = 0; k < nst; k += 2) {
+      TN_PSTAMP(k, 2);
+      if (k + 1 < nst) write_reload(sa[1], sb[1], k + 1);
+      TN_PSTAMP(k, 3);
+      __syncthreads();   // stage k read; stage k+1 written
+      if (k + 1 < nst) {
+        TN_PSTAMP(k + 1, 2);
+        if (k + 2 < nst) write_reload(sa[0], sb[0], k + 2);
+        TN_PSTAMP(k + 1, 3);
+        __syncthreads();
+      }
+    }
+    if (csum) {   // the AROW row groups' partial column sums, combined in a fixed order
+      float4* scr = reinterpret_cast<float4*>(tlds + 2 * X::STAGE);
+      scr[am * X::AQ + aq] = cs;
+      __syncthreads();
+      if (pt < X::AQ) {
+        float4 v = scr[pt];
+#pragma unroll
+        for (int i = 1; i < X::AROW; ++i) {
+          const float4 u = scr[i * X::AQ + pt];
+          v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+        }
+        *reinterpret_cast<float4*>(g.colsum + (int64_t)(T.z * g.S + T.s) * g.R + T.ntile * RA + 4 * pt) = v;
+      }
+    }
+  }
+}
+
+template <int RA>
+__global__ void __launch_bounds__(512, 1) gemm_tn_ws_kernel(TnArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char tlds[];
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int xcd = blockIdx.x & 7;
+  const int32_t stride = gridDim.x >> 3;
+  const int32_t lo = (int32_t)((int64_t)xcd * g.tiles / 8), hi = (int32_t)((int64_t)(xcd + 1) * g.tiles / 8);
+  const int nst = (int)(g.Ms / TK);
+  if (wave < 4)
+    tn_ws_consumer<RA>(g, tlds, wave, tid & 63, lo, hi, stride, nst);
+  else
+    tn_ws_producer<RA>(g, tlds, tid & 255, lo, hi, stride, nst);
+}
+
 }  // namespace
 
 extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
@@ -324,9 +571,14 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   g.ldc = a.ldc;
   g.colsum = a.colsum;
   if (a.colsum && ((uintptr_t)a.colsum & 15)) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: colsum must be 16-byte aligned");
-  // 256-row tiles (8 waves) when R allows, else 128-row tiles (4 waves)
+  // 256-row tiles (8 waves) when R allows, else 128-row tiles on the warp-specialised kernel
+  // (LGX_TN_WS, read per call for same-process A/B: 0 = the 4-wave kernel for 128-row tiles,
+  // 2 = the warp-specialised kernel for 256-row tiles too)
+  const char* wsv = getenv("LGX_TN_WS");
+  const int wsm = wsv && *wsv ? atoi(wsv) : 1;
   const int nwv = a.R % 256 == 0 ? 8 : 4;
   const int RA = nwv == 8 ? 256 : 128;
+  const bool ws = RA == 128 ? wsm != 0 : wsm == 2;
   g.rt = a.R / RA;
   g.ct = (a.Cc + TT - 1) / TT;
   const int64_t tiles = (int64_t)g.rt * g.ct * a.slices * a.batch;
@@ -336,13 +588,21 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x3_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           TC<4>::LDS) == hipSuccess &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_x3_kernel<8>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          TC<8>::LDS) == hipSuccess;
+                          TC<8>::LDS) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ws_kernel<256>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TW<256>::LDS) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ws_kernel<128>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TW<128>::LDS) == hipSuccess;
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
-  if (nwv == 8)
+  if (ws && RA == 256)
+    LGX_LAUNCH(gemm_tn_ws_kernel<256>, dim3((unsigned)wgs), dim3(512), TW<256>::LDS, reinterpret_cast<hipStream_t>(stream), g);
+  else if (ws)
+    LGX_LAUNCH(gemm_tn_ws_kernel<128>, dim3((unsigned)wgs), dim3(512), TW<128>::LDS, reinterpret_cast<hipStream_t>(stream), g);
+  else if (nwv == 8)
     LGX_LAUNCH(gemm_tn_x3_kernel<8>, dim3((unsigned)wgs), dim3(512), TC<8>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else
     LGX_LAUNCH(gemm_tn_x3_kernel<4>, dim3((unsigned)wgs), dim3(256), TC<4>::LDS, reinterpret_cast<hipStream_t>(stream), g);

@@ -136,14 +136,8 @@ __device__ __forceinline__ void p_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// three RNE bf16 limbs of two floats, packed (low half = first element); both subtractions exact
 __device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
-  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){x0, x1}, bf16x2));
-  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
-  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
-  r0 -= __uint_as_float(l1 << 16);
-  r1 -= __uint_as_float(l1 & 0xffff0000u);
-  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((fx2){r0, r1}, bf16x2));
+  lgx_split2(x0, x1, l0, l1, l2);   // (lgx_internal.h)
 }
 
 __device__ __forceinline__ void split8(const float4& x, const float4& y, bf16x8 (&o)[3]) {

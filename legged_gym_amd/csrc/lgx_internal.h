@@ -122,6 +122,22 @@ __device__ __forceinline__ float lgx_ppo_logp_term(float d, float sd) {
   const float half_log_2pi = 0.91893853320467274178f;
   return -(d * d) / (2.f * sd * sd) - logf(sd) - half_log_2pi;
 }
+// Three RNE bf16 limbs of two f32 values, packed (low half = first value): x = l0 + l1 + l2 + e,
+// |e| <= 2^-24 |x|; both subtractions are exact.  The split-bf16 GEMMs' operand split (lgx_gemm_x3p
+// / _tn / _split, lgx_mlp_x3).  (Round 6 measured the residuals as v_dot2c_f32_bf16 with a -1 in the
+// limb's half - 7 VALU per pair instead of 11, bitwise the same limbs - and the PPO update was
+// slower, 10.83 vs 10.46 ms, same box, alternated: the dot instruction does not issue at the rate of
+// the shift / subtract it replaces.)
+typedef __bf16 lgx_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float lgx_fx2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void lgx_split2(float x0, float x1, uint32_t& l0, uint32_t& l1, uint32_t& l2) {
+  l0 = __builtin_bit_cast(uint32_t, __builtin_convertvector((lgx_fx2){x0, x1}, lgx_bf16x2));
+  float r0 = x0 - __uint_as_float(l0 << 16), r1 = x1 - __uint_as_float(l0 & 0xffff0000u);
+  l1 = __builtin_bit_cast(uint32_t, __builtin_convertvector((lgx_fx2){r0, r1}, lgx_bf16x2));
+  r0 -= __uint_as_float(l1 << 16);
+  r1 -= __uint_as_float(l1 & 0xffff0000u);
+  l2 = __builtin_bit_cast(uint32_t, __builtin_convertvector((lgx_fx2){r0, r1}, lgx_bf16x2));
+}
 // PPO.process_env_step's time-out bootstrap: rew + gamma * (V * time_out), as torch evaluates it
 __device__ __forceinline__ float lgx_ppo_reward(float rew, float gamma, float value, bool time_out) {
 #pragma clang fp contract(off)

@@ -10,6 +10,6 @@ for r in 1 2; do
     if [ $v = default ]; then unset LGX_LIB_PATH; else export LGX_LIB_PATH=$PWD/tools/_tmp/ab/$v/liblgx.so; fi
     rm -rf gpurun_out/abp_$v
     timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/abp_$v -o run --output-format csv -- python tools/kbench.py ppo_lgx > gpurun_out/abp_$v.log 2>&1 || { echo "$v failed"; tail -5 gpurun_out/abp_$v.log; exit 1; }
-    echo "$v: $(grep 'PPO update' gpurun_out/abp_$v.log) | $(grep -h -E 'gemm_nt_x3p|gemm_tn_x3' gpurun_out/abp_$v/run_kernel_stats.csv | awk -F'",' '{print $1 "|" $2}' | sed 's/.*kernel<//; s/>((anonymous namespace)::[A-Za-z]*Args)//' | cut -d, -f1,3 | tr '\n' ' ')"
+    echo "$v: $(grep 'PPO update' gpurun_out/abp_$v.log) | $(grep -h -E 'gemm_nt_x3p|gemm_tn_' gpurun_out/abp_$v/run_kernel_stats.csv | awk -F'",' '{print $1 "|" $2}' | sed 's/.*kernel<//; s/>((anonymous namespace)::[A-Za-z]*Args)//' | cut -d, -f1,3 | tr '\n' ' ')"
   done
 done

@@ -7,7 +7,9 @@
 #   ppopmc  - one bench iteration's PPO-update and rollout kernels: HBM FETCH/WRITE and MFMA
 #             utilisation (SQ_VALU_MFMA_BUSY_CYCLES, SQ_BUSY_CYCLES, GRBM_GUI_ACTIVE, ...)
 #   bench   - bench.py with the fresh PMC files (-> gpurun_out/<tag>_bench.json)
-#   prof    - rocprofv3 --kernel-trace --stats of bench.py --steps 3 (-> gpurun_out/<tag>_prof)
+#   prof    - rocprofv3 --kernel-trace --stats of bench.py --steps 5 (-> gpurun_out/<tag>_prof), without
+#             bench.py's post-timed isolated dW / standalone actuator launches (LGX_BENCH_POSTHOC=0):
+#             every kernel average in the summary is an in-situ figure
 # One --pmc counter group per pass, --kernel-trace only; every GPU step has its own time limit and
 # the first failure ends the session.  BENCH_ARGS / LGX_PMC_TASK / LGX_PMC_ENVS select another
 # workload (e.g. BENCH_ARGS="--task anymal_c_rough --num_envs 8192" LGX_PMC_TASK=anymal_c_rough
@@ -53,7 +55,7 @@ for step in $STEPS; do
     cat gpurun_out/${TAG}_bench.json ;;
   prof)
     rm -rf gpurun_out/${TAG}_prof
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no_cpu_baseline $BENCH_ARGS > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err || { echo "prof failed"; tail -20 gpurun_out/${TAG}_prof.err; exit 1; }
+    LGX_BENCH_POSTHOC=0 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no_cpu_baseline $BENCH_ARGS > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err || { echo "prof failed"; tail -20 gpurun_out/${TAG}_prof.err; exit 1; }
     find gpurun_out/${TAG}_prof -name "*stats*" ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac

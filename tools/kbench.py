@@ -394,6 +394,17 @@ def tn_bench(M=24576, iters=20):
                     seg = [(d[:, e + 1] - d[:, e]).mean().item() for e in range(3)]
                     print(f"  wave {w}: stages {len(d)} per-stage {per:.0f}: compute {seg[0]:.0f} split+write {seg[1]:.0f} "
                           f"load-issue {seg[2]:.0f} barrier {per - sum(seg):.0f}", flush=True)
+            if os.environ.get("KB_WSCLOCK"):   # TN_WS_CLOCK build: consumer start/end, producer start/end per stage
+                Cbuf.zero_()
+                lgxlib.check(lib.lgx_gemm_tn(C.byref(a), stream), "tn")
+                torch.cuda.synchronize()
+                st = Cbuf[2 * S * R * Cc:].view(torch.int64)[:32 * 4].view(32, 4).double().cpu()
+                v = st[(st > 0).all(1)]
+                if len(v) > 2:
+                    per = (v[1:, 0] - v[:-1, 0]).mean().item()
+                    print(f"  per-stage {per:.0f}: consumer compute {(v[:, 1] - v[:, 0]).mean().item():.0f}, "
+                          f"producer write {(v[:, 3] - v[:, 2]).mean().item():.0f}, producer start - consumer start "
+                          f"{(v[:, 2] - v[:, 0]).mean().item():.0f}", flush=True)
             P = torch.empty(2 * S, R, Cc, device=dev)
             Bv = B[..., :Cc].reshape(2 * S, M // S, Cc) if ldb == Cc else B.view(2 * S, M // S, ldb)[..., :Cc]
             t2 = timeit(lambda: torch.bmm(A.view(2 * S, M // S, R).transpose(1, 2), Bv, out=P), iters=iters)
