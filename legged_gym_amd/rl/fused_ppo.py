@@ -156,8 +156,9 @@ class FusedPPOUpdate:
     def supported(ac):
         def lin(seq):
             return [m for m in seq if isinstance(m, nn.Linear)], [m for m in seq if not isinstance(m, nn.Linear)]
-        if getattr(ac, "is_recurrent", False):    # (the memories' update runs on the autograd path)
-            return False
+        if getattr(ac, "is_recurrent", False) and (os.environ.get("LGX_PPO_FUSED_RECURRENT", "1") == "0"
+                                                   or not hasattr(ac, "memory_a") or not hasattr(ac, "memory_c")):
+            return False   # (LGX_PPO_FUSED_RECURRENT=0: recurrent policies on the autograd update)
         try:
             la, aa = lin(ac.actor)
             lc, acr = lin(ac.critic)
@@ -205,6 +206,12 @@ class FusedPPOUpdate:
         for k in range(1, self.L + 1):
             order += [la[k].bias, lc[k].bias]
         order.append(ac.std)
+        # recurrent policies (ActorCriticRecurrent): the memories' parameters after the heads' (their
+        # gradients come from torch autograd through the LSTM / GRU, fed with the heads' input
+        # gradient dX = dZ_1 W_1 of the fused backward; the clip norm and Adam cover them too)
+        self.recurrent = bool(getattr(ac, "is_recurrent", False))
+        self.mem_params = (list(ac.memory_a.parameters()) + list(ac.memory_c.parameters())) if self.recurrent else []
+        order += self.mem_params
         n = sum(p.numel() for p in order)
         self.flat_p = torch.zeros(n, device=self.dev)
         # gradient buffer + one trailing slot: the minibatch KL rides in the same all-reduce as the
@@ -298,9 +305,10 @@ class FusedPPOUpdate:
         self.dMU = torch.empty(M, A, device=dev)
         self.dV = torch.empty(M, device=dev)
         Sk = self.Sk
-        # layer-1 dW partials: one [2, S, h0, K] block, or (actor, critic) blocks when the critic's
-        # (privileged) input width differs
-        p0 = (torch.empty(2, Sk[0], h[0], self.num_obs, device=dev) if self.num_cobs == self.num_obs else
+        # layer-1 dW partials: one [2, S, h0, K] block (one input for both networks), or (actor,
+        # critic) blocks when the critic reads inputs of its own (privileged observations, of any
+        # width; a recurrent policy's two memory outputs)
+        p0 = (torch.empty(2, Sk[0], h[0], self.num_obs, device=dev) if self.num_cobs == self.num_obs and not sep else
               (torch.empty(Sk[0], h[0], self.num_obs, device=dev), torch.empty(Sk[0], h[0], self.num_cobs, device=dev)))
         self.P = [p0] + \
                  [torch.empty(2 * Sk[k], h[k], h[k - 1], device=dev) for k in range(1, self.L)]
@@ -490,6 +498,8 @@ class FusedPPOUpdate:
         self.gemm_bwd = bwd
 
     def _separate_critic_obs(self):
+        if self.recurrent:   # the heads' inputs are the two memories' outputs
+            return True
         st = self.ppo.storage
         return st is not None and st.privileged_observations is not None
 
@@ -554,7 +564,8 @@ class FusedPPOUpdate:
         self.rest_on_side = all(k in colsum for k in range(1, self.L - 1))
         # the clip norm's sums of squares written by the reduction launches themselves
         # (lgx_reduce_slices_sq; single-process updates with the fused loss): one launch less per minibatch
-        self.fused_sq = self.lgx_gemm and self.loss_bwd and os.environ.get("LGX_PPO_FUSED_SQ", "1") != "0"
+        self.fused_sq = (self.lgx_gemm and self.loss_bwd and not self.recurrent
+                         and os.environ.get("LGX_PPO_FUSED_SQ", "1") != "0")
         if self.fused_sq:
             blocks = self.lib.lgx_reduce_slices_blocks
             self.nsq_rest = int(blocks(self.jobs_rest, len(self.jobs_rest), 1)) if len(self.jobs_rest) else 0
@@ -574,6 +585,8 @@ class FusedPPOUpdate:
         host can issue the next rollout while this update still runs (the GPU otherwise idles at the
         iteration boundary until the host returns from the synchronisation and issues again)."""
         self.resolve()   # (a previous deferred update finished long before this one is issued)
+        if self.recurrent:
+            return self._update_recurrent(defer)
         t_issue = time.perf_counter()
         ppo = self.ppo
         st = ppo.storage
@@ -634,6 +647,101 @@ class FusedPPOUpdate:
         self._pin_ev.record(torch.cuda.current_stream(self.dev))
         self._pending = n
         return None
+
+
+    # ------------------------------------------------------------------ recurrent policies
+    def _rec_rows(self, i, T, N, envs):
+        """Storage rows of recurrent minibatch i in the heads' row order (t-major over the envs
+        [i envs, (i + 1) envs): the unpadded memory output [T, envs, H] flattened)."""
+        cache = getattr(self, "_rec_idx", None)
+        if cache is None or cache[0] != (T, N, envs):
+            cache = ((T, N, envs), {})
+            self._rec_idx = cache
+        if i not in cache[1]:
+            t = torch.arange(T, device=self.dev, dtype=torch.int64)[:, None] * N
+            cache[1][i] = (t + i * envs + torch.arange(envs, device=self.dev, dtype=torch.int64)[None, :]).reshape(-1)
+        return cache[1][i]
+
+    def _update_recurrent(self, defer):
+        """rsl_rl PPO.update for ActorCriticRecurrent (reccurent_mini_batch_generator: minibatches of
+        whole envs in order, padded trajectories, the memories' saved first-step states).  Per
+        minibatch the LSTM / GRU runs forward on torch with autograd (the heads' inputs), the heads
+        run the fused forward / loss / backward of a feed-forward policy on those inputs, and
+        _memory_backward carries dX = dZ_1 W_1 back through the memories into the flat gradient
+        before the clip norm and Adam."""
+        t_issue = time.perf_counter()
+        ppo, ac = self.ppo, self.ppo.actor_critic
+        st = ppo.storage
+        T, N = st.num_transitions_per_env, st.num_envs
+        B = T * N
+        nmb = ppo.num_mini_batches
+        envs = N // nmb
+        M = T * envs
+        self._alloc(M)
+        self._mirrors_valid = False
+        stream = C.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+        if ppo.desired_kl is not None and ppo.schedule == "adaptive":
+            self.optimizer.lr_dev.fill_(ppo.learning_rate)
+        self.stats.zero_()
+        storage = dict(actions=st.actions.view(B, -1), old_logp=st.actions_log_prob.view(B),
+                       old_mu=st.mu.view(B, -1), old_sigma=st.sigma.view(B, -1), advantages=st.advantages.view(B),
+                       target_values=st.values.view(B), returns=st.returns.view(B))
+        args = self._loss_args(storage)
+        H = self.num_obs
+        k = 0
+        for (obs_b, cobs_b, _a, _v, _adv, _r, _lp, _mu, _sg, hid_b, masks_b) in \
+                st.reccurent_mini_batch_generator(nmb, ppo.num_learning_epochs):
+            i = k % nmb
+            k += 1
+            with torch.enable_grad():
+                xa = ac.memory_a(obs_b, masks_b, hid_b[0])       # [T, envs, H]
+                xc = ac.memory_c(cobs_b, masks_b, hid_b[1])
+            xs = []
+            for x, pad in ((xa, self.Xp), (xc, self.Xcp)):
+                x2 = x.detach().reshape(M, H)
+                if pad.shape[1] == H and x2.is_contiguous() and x2.data_ptr() % 16 == 0:
+                    xs.append(x2)
+                else:                              # (K padded to the GEMM step: zero columns stay)
+                    pad[:, :H].copy_(x2)
+                    xs.append(pad)
+            self._mem_ctx = (xa, xc)
+            self._mem_xs = xs      # (the heads' input rows stay referenced until the next minibatch)
+            self._minibatch(self._rec_rows(i, T, N, envs), None, None, args, stream, xs=(xs[0], xs[1]))
+            self._mem_ctx = None
+        n = ppo.num_learning_epochs * nmb
+        self.host_issue_s = time.perf_counter() - t_issue
+        if not defer:
+            return self._apply_readback(self.stats.tolist(), float(self.optimizer.lr_dev.item()), n)
+        if getattr(self, "_pin_stats", None) is None:
+            self._pin_stats = torch.empty(self.stats.shape, dtype=self.stats.dtype).pin_memory()
+            self._pin_lr = torch.empty(1, dtype=self.optimizer.lr_dev.dtype).pin_memory()
+            self._pin_ev = torch.cuda.Event()
+        self._pin_stats.copy_(self.stats, non_blocking=True)
+        self._pin_lr.copy_(self.optimizer.lr_dev.view(1), non_blocking=True)
+        self._pin_ev.record(torch.cuda.current_stream(self.dev))
+        self._pending = n
+        return None
+
+    def _memory_backward(self):
+        """The memories' gradients of a recurrent minibatch: dX = dZ_1 W_1 per network (the heads'
+        input gradient; dZ_1 from the fused backward), then torch autograd through the LSTM / GRU
+        forward of this minibatch, written into the memories' blocks of the flat gradient (every
+        other block is complete: this runs after the reductions, on the update's stream)."""
+        ctx = getattr(self, "_mem_ctx", None)
+        if ctx is None:
+            return
+        xa, xc = ctx
+        dz1 = self.D[0] if self.L > 1 else self.Y[self.L - 1]        # [2, M, h1]
+        wa, wc = self.W[0]                                           # [h1, H] each
+        dxa = torch.mm(dz1[0], wa).view_as(xa)
+        dxc = torch.mm(dz1[1], wc).view_as(xc)
+        with torch.enable_grad():
+            grads = torch.autograd.grad([xa, xc], self.mem_params, grad_outputs=[dxa, dxc], allow_unused=True)
+        for p, g in zip(self.mem_params, grads):
+            if g is None:
+                p.grad.zero_()
+            else:
+                p.grad.copy_(g)
 
     def _apply_readback(self, s, lr, n):
         ppo = self.ppo
@@ -920,7 +1028,7 @@ class FusedPPOUpdate:
                 if len(xs) > 2:                 # [2, M, Kp]: net 0's copy feeds the forward
                     xp = xs[0][0]
             X = Xc = xp[:, :self.num_obs]
-            if cobs is not None:
+            if cobs is not None or self.recurrent:
                 Xc = xcp[:, :self.num_cobs]
             for g, src in zip(self.gemm_fwd[0], self.fwd0_src):
                 g.A = (xp if src == "x" or xcp is None else xcp).data_ptr()
@@ -1028,7 +1136,7 @@ class FusedPPOUpdate:
             else:
                 chk(lib.lgx_reduce_slices_finalize(self.jobs_rest, len(self.jobs_rest), C.byref(args),
                                                    C.c_void_p(self._side.cuda_stream)), "reduce")
-        bucketed = early and apply and ppo.dist is not None
+        bucketed = early and apply and ppo.dist is not None and not self.recurrent
         self.bucketed = bucketed
         if bucketed:
             # data-parallel: the first gradient bucket (every block after dW1's in the layer-major
@@ -1070,6 +1178,8 @@ class FusedPPOUpdate:
             chk(lib.lgx_reduce_slices_finalize(self.jobs, self.njobs, C.byref(args), stream), "reduce")
         else:
             chk(lib.lgx_reduce_slices(self.jobs, self.njobs, stream), "reduce")
+        if self.recurrent:
+            self._memory_backward()
         if not apply:
             return
         grad_scale = 1.0
