@@ -257,8 +257,11 @@ def test_fused_other_hidden_stacks(gpu, hidden):
     assert abs(vl_f - vl_r) <= 1e-4 * abs(vl_r) + 1e-6 and abs(sl_f - sl_r) <= 1e-4 * abs(sl_r) + 1e-6
 
 
-def test_fused_minibatch_gradient_privileged_critic(gpu):
-    ref, fus = make_pair(cobs=252)
+@pytest.mark.parametrize("cobs", [252, OBS])
+def test_fused_minibatch_gradient_privileged_critic(gpu, cobs):
+    """Privileged critic observations of another width, and of the actor's width (separate rows of
+    the same width: the layer-1 weight gradients per network, not the batched shared-input dW1)."""
+    ref, fus = make_pair(cobs=cobs)
     idx = torch.randperm(T * N, device="cuda:0")[: T * N // 4]
     gref = autograd_grads(ref, idx)
     fus._fused.gradients(idx)
