@@ -634,8 +634,12 @@ class FusedPPOUpdate:
                 else:
                     mx = tuple(x[i * M:(i + 1) * M] if x is not None else None for x in xs)
                 self._minibatch(idx, obs, cobs, args, stream, xs=mx)
-        n = ppo.num_learning_epochs * nmb
         self.host_issue_s = time.perf_counter() - t_issue   # host time to issue every launch (tools/host_overhead.py)
+        return self._finish(ppo.num_learning_epochs * nmb, defer)
+
+    def _finish(self, n, defer):
+        """The update's readback (statistics, adapted learning rate) over its n minibatches: now, or
+        deferred to pinned memory behind an event (resolve())."""
         if not defer:
             return self._apply_readback(self.stats.tolist(), float(self.optimizer.lr_dev.item()), n)
         if getattr(self, "_pin_stats", None) is None:
@@ -708,19 +712,8 @@ class FusedPPOUpdate:
             self._mem_xs = xs      # (the heads' input rows stay referenced until the next minibatch)
             self._minibatch(self._rec_rows(i, T, N, envs), None, None, args, stream, xs=(xs[0], xs[1]))
             self._mem_ctx = None
-        n = ppo.num_learning_epochs * nmb
         self.host_issue_s = time.perf_counter() - t_issue
-        if not defer:
-            return self._apply_readback(self.stats.tolist(), float(self.optimizer.lr_dev.item()), n)
-        if getattr(self, "_pin_stats", None) is None:
-            self._pin_stats = torch.empty(self.stats.shape, dtype=self.stats.dtype).pin_memory()
-            self._pin_lr = torch.empty(1, dtype=self.optimizer.lr_dev.dtype).pin_memory()
-            self._pin_ev = torch.cuda.Event()
-        self._pin_stats.copy_(self.stats, non_blocking=True)
-        self._pin_lr.copy_(self.optimizer.lr_dev.view(1), non_blocking=True)
-        self._pin_ev.record(torch.cuda.current_stream(self.dev))
-        self._pending = n
-        return None
+        return self._finish(ppo.num_learning_epochs * nmb, defer)
 
     def _memory_backward(self):
         """The memories' gradients of a recurrent minibatch: dX = dZ_1 W_1 per network (the heads'
