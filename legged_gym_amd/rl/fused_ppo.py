@@ -810,6 +810,8 @@ class FusedPPOUpdate:
 
     def gradients(self, idx, apply=False):
         """Flat gradient of one minibatch (rows `idx` of the current storage), for tests."""
+        if self.recurrent:   # (a recurrent minibatch is whole envs through the memories: update())
+            raise NotImplementedError("gradients(idx) takes feed-forward policies; recurrent ones go through update()")
         st = self.ppo.storage
         T, N = st.num_transitions_per_env, st.num_envs
         B = T * N
