@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "lgx_internal.h"
 
@@ -542,6 +543,246 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ws_kernel(TnArgs g) {
     tn_ws_producer<RA>(g, tlds, tid & 255, lo, hi, stride, nst);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Ring form of the 256-row tiles (the default for R % 256 == 0; LGX_TN_RING=0 selects
+// gemm_tn_x3_kernel<8>).  Measured on gemm_tn_x3_kernel<8> (dW1 at the half-GPU slices, isolated):
+// 118 us as built, 112 us without the split, 94 us with no staging at all (stale LDS) - against a
+// 61-70 us MFMA floor: the fragment reads that open every 32-row stage after its barrier are exposed
+// with both waves of a SIMD waiting on them at once.  This form stages 16-row images in a 3-deep LDS
+// ring (36 KB per stage): stage k+1 is complete one barrier before it is computed, so each wave reads
+// stage k+1's fragments right after its last MFMA of stage k and before that barrier - the read
+// latency overlaps the barrier wait instead of following it.  Per stage and wave: 24 MFMAs (a 64 x 64
+// block of 2 x 2 accumulators, one 16-k step) with the staging of stage k+2 (2 A rows + 1 B row per
+// thread: split, limb-image writes) between the MFMA blocks; the global loads run two stages ahead in
+// a register ring.  Same products in the same order per output element: bitwise the weight gradients
+// of gemm_tn_x3_kernel.
+// Measured (round 6, isolated, kbench tn, 2 alternations): half-GPU slices (S = 16) dW1 111-112 us
+// vs 117, dW2 107-108 vs 114; S = 32 equal (75-76, 69-71); the full update 10.02 vs 10.06 ms (the
+// dW launches run beside dA there).  Per-stage clock (s_memtime, workgroup 0, waves 0 and 4 of SIMD
+// 0): 2,500 cycles per 16-row stage against the SIMD's 1,536 MFMA cycles - the later wave's MFMA
+// region 1,915 (the side work's issue), the write wait 90, the 24 fragment-read issues 250 and the
+// barrier 250; the older wave waits 650 at the barrier.  The loop must stay branch-free with the
+// register ring in fixed registers (an `if` on the second half made the compiler copy the ring at the
+// back edge behind vmcnt waits: 3 % slower than the old kernel).
+constexpr int TR = 16;   // rows per ring stage
+
+template <int W>
+__device__ __forceinline__ void tr16_store_row(char* img, const float4& v, int cq, int m) {
+  uint2 l0, l1, l2;
+  split2(v.x, v.y, l0.x, l1.x, l2.x);
+  split2(v.z, v.w, l0.y, l1.y, l2.y);
+  char* row = img + m * (W * 2) + ((cq ^ (8 * (m & 3))) << 3);
+  *reinterpret_cast<uint2*>(row) = l0;
+  *reinterpret_cast<uint2*>(row + TR * W * 2) = l1;
+  *reinterpret_cast<uint2*>(row + 2 * TR * W * 2) = l2;
+}
+
+template <int W>
+__device__ __forceinline__ bf16x8 tr16_frag(const char* img, int l, int lane_off, int xa) {
+  const char* p = img + l * (TR * W * 2) + lane_off + xa;
+  const s16x4 lo = tr_read(p), hi = tr_read(p + 4 * W * 2);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+struct TRing {
+  static constexpr int RA = 256;
+  static constexpr int IMGA = 3 * TR * RA * 2;       // 24 KB
+  static constexpr int IMGB = 3 * TR * TT * 2;       // 12 KB
+  static constexpr int STAGE = IMGA + IMGB;          // 36 KB
+  static constexpr int NB = 3;                       // ring depth
+  static constexpr int CS = 8 * 64 * 16;             // column-sum scratch: [row group][column quad] float4
+  static constexpr int LDS = NB * STAGE + CS;        // 116 KB
+};
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
+  using X = TRing;
+  constexpr int RA = X::RA;
+  extern __shared__ __attribute__((aligned(16))) char tlds[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int q = (lane >> 2) & 3, p = lane & 3, gb = (lane >> 4) & 1;
+  const int lane_a = (8 * h + q) * (RA * 2) + (4 * gb + p) * 8;
+  const int lane_b = (8 * h + q) * (TT * 2) + (4 * gb + p) * 8;
+  int xa[2], xb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    xa[i] = 64 * ((2 * wm + i) ^ q);
+    xb[i] = 64 * ((2 * wn + i) ^ q);
+  }
+  // staging: A thread = column quad aq of rows 2 am, 2 am + 1; B thread = column quad bq of row bm
+  const int aq = tid & 63, am = tid >> 6;
+  const int bq = tid & 31, bm = tid >> 5;
+  const int xcd = blockIdx.x & 7;
+  const int32_t stride = gridDim.x >> 3;
+  const int32_t lo = (int32_t)((int64_t)xcd * g.tiles / 8), hi = (int32_t)((int64_t)(xcd + 1) * g.tiles / 8);
+  const int nst = (int)(g.Ms / TR);
+  const uint32_t sta = (uint32_t)(g.lda * 4), stb = (uint32_t)(g.ldb * 4);
+  for (int32_t tile = lo + (blockIdx.x >> 3); tile < hi; tile += stride) {
+    int32_t t = tile;
+    const int ctile = t % g.ct;
+    t /= g.ct;
+    const int ntile = t % g.rt;
+    t /= g.rt;
+    const int s = t % g.S;
+    const int z = t / g.S;
+    const int64_t m0 = (int64_t)s * g.Ms;
+    const char* Ab = reinterpret_cast<const char*>(g.A + z * g.sa + m0 * g.lda + ntile * RA);
+    const char* Bb = reinterpret_cast<const char*>(g.B + z * g.sb + m0 * g.ldb + ctile * TT);
+    const uint32_t oa = (2 * am) * sta + aq * 16, ob = bm * stb + bq * 16;
+    const bool csum = g.colsum != nullptr && ctile == 0;
+    float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 ra[2][2], rb[2];          // register ring: stages k + 2 (slot k & 1) and k + 3
+    auto load = [&](int slot, int k) {
+      const int kc = min(k, nst - 1);   // (past the last stage: re-loads, never written as a stage)
+      const uint32_t la = oa + kc * TR * sta, lb = ob + kc * TR * stb;
+      ra[slot][0] = *reinterpret_cast<const float4*>(Ab + la);
+      ra[slot][1] = *reinterpret_cast<const float4*>(Ab + la + sta);
+      rb[slot] = *reinterpret_cast<const float4*>(Bb + lb);
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    bf16x8 fa[2][3], fb[2][3];
+    auto pre_a = [&](const char* ia, int i) {
+#pragma unroll
+      for (int l = 0; l < 3; ++l) fa[i][l] = tr16_frag<RA>(ia, l, lane_a, xa[i]);
+    };
+    auto pre_b = [&](const char* ia, int j) {
+#pragma unroll
+      for (int l = 0; l < 3; ++l) fb[j][l] = tr16_frag<TT>(ia + X::IMGA, l, lane_b, xb[j]);
+    };
+    auto prefetch = [&](const char* ia) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        pre_a(ia, i);
+        pre_b(ia, i);
+      }
+    };
+    __syncthreads();   // (the previous tile's readers of the ring are done)
+    // prologue: stages 0 and 1 into ring buffers 0 and 1, stages 2 and 3 in flight
+    load(0, 0);
+    load(1, 1);
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      char* wb = tlds + st * X::STAGE;
+      const float cw = st < nst ? 1.f : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        cs.x = fmaf(ra[st][i].x, cw, cs.x); cs.y = fmaf(ra[st][i].y, cw, cs.y);
+        cs.z = fmaf(ra[st][i].z, cw, cs.z); cs.w = fmaf(ra[st][i].w, cw, cs.w);
+        tr16_store_row<RA>(wb, ra[st][i], aq, 2 * am + i);
+      }
+      tr16_store_row<TT>(wb + X::IMGA, rb[st], bq, bm);
+      load(st, st + 2);
+    }
+    __syncthreads();
+    prefetch(tlds);
+#ifdef RING_CLOCK   // A/B instrumentation: per-stage s_memtime stamps of workgroup 0's first tile into g.C
+    uint64_t* clk = (blockIdx.x == 0 && lane == 0 && tile == lo && (wave & 3) == 0)
+                        ? reinterpret_cast<uint64_t*>(g.C + (int64_t)g.batch * g.S * g.R * g.ldc)
+                        : nullptr;
+#define RING_STAMP(e) \
+  if (clk && k < 32) clk[((wave >> 2) * 32 + k) * 4 + (e)] = __builtin_amdgcn_s_memtime()
+#else
+#define RING_STAMP(e)
+#endif
+    uint32_t off_c = 0, off_w = 2 * X::STAGE;   // ring offsets of stage k (compute) and k + 2 (write)
+    // stage k: MFMAs on the fragments prefetched before the last barrier; between the MFMA blocks the
+    // images of stage k + 2 (ring slot SL) and the loads of stage k + 4; then stage k + 1's fragments
+    auto step = [&](auto slot_c, int k) {
+      constexpr int SL = decltype(slot_c)::value;
+      RING_STAMP(0);
+      char* wb = tlds + off_w;
+      const uint32_t off_n = off_c == 2 * X::STAGE ? 0u : off_c + X::STAGE;   // stage k + 1
+      const float cw = k + 2 < nst ? 1.f : 0.f;   // (stage k + 2 exists: else the idle buffer is written)
+      auto side = [&](int u) {
+        if (u < 2) {
+          cs.x = fmaf(ra[SL][u].x, cw, cs.x); cs.y = fmaf(ra[SL][u].y, cw, cs.y);
+          cs.z = fmaf(ra[SL][u].z, cw, cs.z); cs.w = fmaf(ra[SL][u].w, cw, cs.w);
+          tr16_store_row<RA>(wb, ra[SL][u], aq, 2 * am + u);
+        } else if (u == 2) {
+          tr16_store_row<TT>(wb + X::IMGA, rb[SL], bq, bm);
+          load(SL, k + 4);
+        }
+      };
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
+          acc[i][j] = c;
+          side(2 * i + j);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      // this stage's image writes complete before the barrier (the prefetch reads below may stay in
+      // flight across it: their registers are waited for at the next stage's first MFMA)
+      RING_STAMP(1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      RING_STAMP(2);
+      off_c = off_n;
+      off_w = off_w == 2 * X::STAGE ? 0u : off_w + X::STAGE;
+      // stage k + 1's fragments (complete since the last barrier).  Not earlier: issued as soon as
+      // their registers die (A block 0 after MFMA block (0, 1), B block 0 after (1, 0)) they
+      // lengthened the MFMA region by 130-190 cycles per stage and the kernel by 6 %
+      prefetch(tlds + off_n);   // (after the last stage: a stale buffer, unused - no branch in the loop)
+      RING_STAMP(3);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);   // (no MFMA of stage k + 1 above the barrier)
+    };
+    for (int k = 0; k < nst; k += 2) {   // (nst = Ms / 16 is even: slots 0 and 1 stay in their registers)
+      step(std::integral_constant<int, 0>{}, k);
+      step(std::integral_constant<int, 1>{}, k + 1);
+    }
+    if (csum) {   // the 8 row groups' partial column sums, combined in a fixed order
+      float4* scr = reinterpret_cast<float4*>(tlds + X::NB * X::STAGE);
+      scr[am * 64 + aq] = cs;
+      __syncthreads();
+      if (tid < 64) {
+        float4 v = scr[tid];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) {
+          const float4 u = scr[i * 64 + tid];
+          v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+        }
+        *reinterpret_cast<float4*>(g.colsum + (int64_t)(z * g.S + s) * g.R + ntile * RA + 4 * tid) = v;
+      }
+    }
+    // acc[i][j][e] = C[n0 + 32i + 8(e >> 2) + 4h + (e & 3)][c0 + 32j + r]
+    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * RA + wm * 64) * g.ldc;
+    const int c0 = ctile * TT + wn * 64 + r;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int c = c0 + 32 * j;
+      if (c >= g.Cc) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+          Cb[(int64_t)n * g.ldc + c] = acc[i][j][e];
+        }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
@@ -579,6 +820,8 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   const int nwv = a.R % 256 == 0 ? 8 : 4;
   const int RA = nwv == 8 ? 256 : 128;
   const bool ws = RA == 128 ? wsm != 0 : wsm == 2;
+  const char* rgv = getenv("LGX_TN_RING");
+  const bool ring = RA == 256 && !ws && !(rgv && rgv[0] == '0') && (a.M / a.slices) % TR == 0;
   g.rt = a.R / RA;
   g.ct = (a.Cc + TT - 1) / TT;
   const int64_t tiles = (int64_t)g.rt * g.ct * a.slices * a.batch;
@@ -592,13 +835,17 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ws_kernel<256>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           TW<256>::LDS) == hipSuccess &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ws_kernel<128>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          TW<128>::LDS) == hipSuccess;
+                          TW<128>::LDS) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ring_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TRing::LDS) == hipSuccess;
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
-  if (ws && RA == 256)
+  if (ring)
+    LGX_LAUNCH(gemm_tn_ring_kernel, dim3((unsigned)wgs), dim3(512), TRing::LDS, reinterpret_cast<hipStream_t>(stream), g);
+  else if (ws && RA == 256)
     LGX_LAUNCH(gemm_tn_ws_kernel<256>, dim3((unsigned)wgs), dim3(512), TW<256>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else if (ws)
     LGX_LAUNCH(gemm_tn_ws_kernel<128>, dim3((unsigned)wgs), dim3(512), TW<128>::LDS, reinterpret_cast<hipStream_t>(stream), g);

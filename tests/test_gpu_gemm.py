@@ -345,6 +345,39 @@ def test_gemm_tn_warp_specialised_equals_plain(gpu, monkeypatch, M, S, R, Cc, ld
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5 * (M // S) ** 0.5)
 
 
+@pytest.mark.parametrize("M,S,R,Cc,ldb", [(2048, 4, 256, 235, 256), (96, 3, 256, 384, None), (160, 1, 256, 128, None),
+                                          (24576, 16, 512, 235, 256), (24576, 32, 256, 256, None),
+                                          (24576, 16, 256, 512, None)])
+def test_gemm_tn_ring_equals_plain(gpu, monkeypatch, M, S, R, Cc, ldb):
+    """The 256-row tiles' ring form (16-row stages in a 3-deep LDS ring, each stage's fragments read
+    before the barrier that opens it; the default) against gemm_tn_x3_kernel<8> (LGX_TN_RING=0): the
+    same products in the same order per output element, so the weight gradients are bitwise equal;
+    the column sums (other per-thread row groups) within f32 rounding.  Slices of 32 and 160 rows:
+    2 and an odd 10 ring stages."""
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(M + R + 1)
+    ldb = ldb or Cc
+    A = torch.randn(2, M, R, device=dev, generator=g)
+    B = torch.randn(2, M, ldb, device=dev, generator=g)
+    monkeypatch.setenv("LGX_TN_WS", "1")
+    outs = []
+    for ring in ("1", "0"):
+        monkeypatch.setenv("LGX_TN_RING", ring)
+        Cout = torch.full((2, S, R, Cc), float("nan"), device=dev)
+        cs = torch.full((2, S, R), float("nan"), device=dev)
+        a = abi.LgxGemmTnArgs()
+        a.M, a.R, a.Cc, a.slices, a.batch = M, R, Cc, S, 2
+        a.A, a.lda, a.sa = A.data_ptr(), R, M * R
+        a.B, a.ldb, a.sb = B.data_ptr(), ldb, M * ldb
+        a.C, a.ldc, a.colsum = Cout.data_ptr(), Cc, cs.data_ptr()
+        lgxlib.check(_lib().lgx_gemm_tn(C.byref(a), _stream()), "lgx_gemm_tn")
+        torch.cuda.synchronize()
+        outs.append((Cout, cs))
+    assert not torch.isnan(outs[0][0]).any()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5 * (M // S) ** 0.5)
+
+
 def test_gemm_tn_rejects_bad_shapes(gpu):
     a = abi.LgxGemmTnArgs()
     x = torch.zeros(4096, device="cuda:0")
