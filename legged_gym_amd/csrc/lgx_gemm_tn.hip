@@ -601,9 +601,10 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+template <int RA>   // (256: the only instantiation; a template for the profiles' name pattern gemm_tn_*_kernel<*>)
 __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
   using X = TRing;
-  constexpr int RA = X::RA;
+  static_assert(RA == X::RA, "ring tiles are 256 rows");
   extern __shared__ __attribute__((aligned(16))) char tlds[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -836,7 +837,7 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
                           TW<256>::LDS) == hipSuccess &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ws_kernel<128>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           TW<128>::LDS) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ring_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ring_kernel<256>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           TRing::LDS) == hipSuccess;
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
   int dev = 0, cus = 256;
@@ -844,7 +845,7 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
   if (ring)
-    LGX_LAUNCH(gemm_tn_ring_kernel, dim3((unsigned)wgs), dim3(512), TRing::LDS, reinterpret_cast<hipStream_t>(stream), g);
+    LGX_LAUNCH(gemm_tn_ring_kernel<256>, dim3((unsigned)wgs), dim3(512), TRing::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else if (ws && RA == 256)
     LGX_LAUNCH(gemm_tn_ws_kernel<256>, dim3((unsigned)wgs), dim3(512), TW<256>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else if (ws)
