@@ -845,8 +845,17 @@ class FusedPPOUpdate:
         comm = self._lgx_comm()
         if comm is not None:   # lgx_allreduce_grads: RCCL on this stream itself (sum; 1/world in Adam)
             assert buf.dtype == torch.float32 and buf.is_contiguous()
+            # one communicator, collectives issued from two streams (the bucketed update: side, then
+            # main): RCCL orders nothing across streams, so a collective issued from another stream
+            # than the previous one waits for it (torch's process group serialises on its own stream)
+            prev = getattr(self, "_comm_last", None)
+            if prev is not None and prev[0] != torch_stream.cuda_stream:
+                torch_stream.wait_event(prev[1])
             self.check(self.lib.lgx_allreduce_grads(comm, _vp(buf), buf.numel(), 0,
                                                     C.c_void_p(torch_stream.cuda_stream)), "allreduce_grads")
+            done = torch.cuda.Event()
+            done.record(torch_stream)
+            self._comm_last = (torch_stream.cuda_stream, done)
         else:
             self.ppo.dist.all_reduce(buf)
         if rec:

@@ -264,7 +264,7 @@ def _native_worker(port, q):
             assert ppo._fused is not None and ppo.dist is not None
             ppo.update()
             out[native] = ([p.detach().cpu().numpy() for p in ppo.actor_critic.parameters()],
-                           ppo.learning_rate, ppo._fused.allreduce_impl)
+                           ppo.learning_rate, ppo._fused.allreduce_impl, ppo._fused.bucketed)
             ppo._fused.close_comm()
         q.put(out)
     finally:
@@ -274,7 +274,8 @@ def _native_worker(port, q):
 @pytest.mark.timeout(200)
 def test_native_allreduce_update_matches_torch_allreduce(gpu):
     """The data-parallel update over a one-rank RCCL group: with LGX_NATIVE_ALLREDUCE=1 the
-    gradient buckets go through lgx_allreduce_grads on the update's own streams, and the parameters
+    gradient buckets go through lgx_allreduce_grads on the update's own streams (the main-stream
+    bucket ordered after the side-stream one by an event), and the parameters
     and learning rate after the update are bitwise those of the torch.distributed path."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -283,8 +284,9 @@ def test_native_allreduce_update_matches_torch_allreduce(gpu):
     out = q.get(timeout=180)
     p.join(timeout=60)
     assert p.exitcode == 0
-    (pt, lrt, it), (pn, lrn, inn) = out["0"], out["1"]
+    (pt, lrt, it, _), (pn, lrn, inn, bn) = out["0"], out["1"]
     assert it == "torch" and inn == "lgx"
+    assert bn   # (two buckets: collectives from the side and the main stream on one communicator)
     assert lrt == lrn
     for a, b in zip(pt, pn):
         assert np.array_equal(a, b)
