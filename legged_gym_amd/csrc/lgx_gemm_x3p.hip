@@ -141,12 +141,6 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_
 }
 
 __device__ __forceinline__ void split8(const float4& x, const float4& y, bf16x8 (&o)[3]) {
-#ifdef X3P_NO_SPLIT   // A/B only (wrong results): the A operand's limbs as raw bits, no split VALU
-  o[0] = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(x.x), __float_as_uint(x.y), __float_as_uint(x.z), __float_as_uint(x.w)));
-  o[1] = __builtin_bit_cast(bf16x8, make_uint4(__float_as_uint(y.x), __float_as_uint(y.y), __float_as_uint(y.z), __float_as_uint(y.w)));
-  o[2] = o[0];
-  return;
-#endif
   uint4 u0, u1, u2;
   split2(x.x, x.y, u0.x, u1.x, u2.x);
   split2(x.z, x.w, u0.y, u1.y, u2.y);
