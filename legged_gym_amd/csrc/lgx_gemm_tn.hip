@@ -731,6 +731,15 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
           acc[i][j] = c;
           side(2 * i + j);
+          // the side unit spread over the block's MFMA shadows: per MFMA up to 4 VALU and one LDS
+          // instruction (the compiler's own placement bunched them after the block: dW1 / dW2 at
+          // S = 16 112.7 / 111.1 -> 107.8 / 105.4 us; 2 VALU per MFMA 113 / 112, 6 VALU 108 / 107)
+#pragma unroll
+          for (int x = 0; x < 6; ++x) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);   // VALU
+            __builtin_amdgcn_sched_group_barrier(0x100 | 0x200, 1, 0);   // LDS read / write
+          }
           __builtin_amdgcn_sched_barrier(0);
         }
       // this stage's image writes complete before the barrier (the prefetch reads below may stay in
