@@ -463,6 +463,30 @@ def test_fused_minibatch_gradient_matches_numpy_oracle(gpu):
     assert worst <= 1.0, (worst, name)
 
 
+@pytest.mark.parametrize("hidden", [(512, 256, 128), (384, 128, 128, 256)])
+def test_adam_limb_mirrors_equal_a_fresh_split(gpu, hidden):
+    """The GEMM weight copies the Adam step writes (split-bf16 limb images of W_1 .. W_L and of
+    W_k^T, lgx_adam_clip_mirror*) equal a fresh lgx_split_bf16 of the updated parameters, bit for
+    bit."""
+    import ctypes as C
+    ref, fus = make_pair(hidden=hidden, epochs=1)
+    fus.update()
+    f = fus._fused
+    torch.cuda.synchronize()
+    nl, nlt = f.limb_bufs
+    bufs = [b for grp in nl if grp is not None for b in (grp if isinstance(grp, tuple) else (grp,))]
+    bufs += [b for b in nlt if b is not None]
+    assert bufs
+    kept = [b.clone() for b in bufs]
+    for b in bufs:
+        b.fill_(-1)
+    f.check(f.lib.lgx_split_bf16(f.copy_jobs, len(f.copy_jobs), C.c_void_p(torch.cuda.current_stream().cuda_stream)),
+            "split_bf16")
+    torch.cuda.synchronize()
+    for a, b in zip(kept, bufs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("schedule", ["adaptive", "fixed"])
 def test_fused_update_matches_numpy_oracle(gpu, schedule):
     """A full fused update (2 epochs x 4 minibatches, Adam, adaptive or fixed learning rate)
