@@ -77,9 +77,9 @@ __device__ __forceinline__ void split2(float x0, float x1, uint32_t& l0, uint32_
   lgx_split2(x0, x1, l0, l1, l2);   // (lgx_internal.h)
 }
 
-// staged row (m, column quad cq) of one operand into its limb image [limb][32 m][W cols]: split,
+// staged row (m, column quad cq) of one operand into its limb image [limb][ROWS m][W cols]: split,
 // three 8-byte stores; the 8-byte unit cq of row m sits at cq ^ 8 (m & 3)
-template <int W>
+template <int W, int ROWS = TK>
 __device__ __forceinline__ void tn_store_row(char* img, const float4& v, int cq, int m) {
   uint2 l0, l1, l2;
 #ifndef TN_NO_SPLIT
@@ -92,19 +92,19 @@ __device__ __forceinline__ void tn_store_row(char* img, const float4& v, int cq,
 #endif
   char* row = img + m * (W * 2) + ((cq ^ (8 * (m & 3))) << 3);
   *reinterpret_cast<uint2*>(row) = l0;
-  *reinterpret_cast<uint2*>(row + TK * W * 2) = l1;
-  *reinterpret_cast<uint2*>(row + 2 * TK * W * 2) = l2;
+  *reinterpret_cast<uint2*>(row + ROWS * W * 2) = l1;
+  *reinterpret_cast<uint2*>(row + 2 * ROWS * W * 2) = l2;
 }
 
 __device__ __forceinline__ s16x4 tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
 }
 
-// fragment of 32 columns (column block a: offset xa) for 16-k half s of an image W columns wide:
-// limb l = two transposed reads (m = 16s + 8h + 0..3 and + 4..7)
-template <int W>
+// fragment of 32 columns (column block a: offset xa) for 16-k half s of an image W columns wide
+// and ROWS rows per limb: limb l = two transposed reads (m = 16s + 8h + 0..3 and + 4..7)
+template <int W, int ROWS = TK>
 __device__ __forceinline__ bf16x8 tn_frag(const char* img, int l, int s, int lane_off, int xa) {
-  const char* p = img + l * (TK * W * 2) + s * (16 * W * 2) + lane_off + xa;
+  const char* p = img + l * (ROWS * W * 2) + s * (16 * W * 2) + lane_off + xa;
   const s16x4 lo = tr_read(p), hi = tr_read(p + 4 * W * 2);
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
@@ -567,24 +567,6 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ws_kernel(TnArgs g) {
 // back edge behind vmcnt waits: 3 % slower than the old kernel).
 constexpr int TR = 16;   // rows per ring stage
 
-template <int W>
-__device__ __forceinline__ void tr16_store_row(char* img, const float4& v, int cq, int m) {
-  uint2 l0, l1, l2;
-  split2(v.x, v.y, l0.x, l1.x, l2.x);
-  split2(v.z, v.w, l0.y, l1.y, l2.y);
-  char* row = img + m * (W * 2) + ((cq ^ (8 * (m & 3))) << 3);
-  *reinterpret_cast<uint2*>(row) = l0;
-  *reinterpret_cast<uint2*>(row + TR * W * 2) = l1;
-  *reinterpret_cast<uint2*>(row + 2 * TR * W * 2) = l2;
-}
-
-template <int W>
-__device__ __forceinline__ bf16x8 tr16_frag(const char* img, int l, int lane_off, int xa) {
-  const char* p = img + l * (TR * W * 2) + lane_off + xa;
-  const s16x4 lo = tr_read(p), hi = tr_read(p + 4 * W * 2);
-  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
 struct TRing {
   static constexpr int RA = 256;
   static constexpr int IMGA = 3 * TR * RA * 2;       // 24 KB
@@ -658,11 +640,11 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
     bf16x8 fa[2][3], fb[2][3];
     auto pre_a = [&](const char* ia, int i) {
 #pragma unroll
-      for (int l = 0; l < 3; ++l) fa[i][l] = tr16_frag<RA>(ia, l, lane_a, xa[i]);
+      for (int l = 0; l < 3; ++l) fa[i][l] = tn_frag<RA, TR>(ia, l, 0, lane_a, xa[i]);
     };
     auto pre_b = [&](const char* ia, int j) {
 #pragma unroll
-      for (int l = 0; l < 3; ++l) fb[j][l] = tr16_frag<TT>(ia + X::IMGA, l, lane_b, xb[j]);
+      for (int l = 0; l < 3; ++l) fb[j][l] = tn_frag<TT, TR>(ia + X::IMGA, l, 0, lane_b, xb[j]);
     };
     auto prefetch = [&](const char* ia) {
 #pragma unroll
@@ -683,9 +665,9 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
       for (int i = 0; i < 2; ++i) {
         cs.x = fmaf(ra[st][i].x, cw, cs.x); cs.y = fmaf(ra[st][i].y, cw, cs.y);
         cs.z = fmaf(ra[st][i].z, cw, cs.z); cs.w = fmaf(ra[st][i].w, cw, cs.w);
-        tr16_store_row<RA>(wb, ra[st][i], aq, 2 * am + i);
+        tn_store_row<RA, TR>(wb, ra[st][i], aq, 2 * am + i);
       }
-      tr16_store_row<TT>(wb + X::IMGA, rb[st], bq, bm);
+      tn_store_row<TT, TR>(wb + X::IMGA, rb[st], bq, bm);
       load(st, st + 2);
     }
     __syncthreads();
@@ -712,9 +694,9 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
         if (u < 2) {
           cs.x = fmaf(ra[SL][u].x, cw, cs.x); cs.y = fmaf(ra[SL][u].y, cw, cs.y);
           cs.z = fmaf(ra[SL][u].z, cw, cs.z); cs.w = fmaf(ra[SL][u].w, cw, cs.w);
-          tr16_store_row<RA>(wb, ra[SL][u], aq, 2 * am + u);
+          tn_store_row<RA, TR>(wb, ra[SL][u], aq, 2 * am + u);
         } else if (u == 2) {
-          tr16_store_row<TT>(wb + X::IMGA, rb[SL], bq, bm);
+          tn_store_row<TT, TR>(wb + X::IMGA, rb[SL], bq, bm);
           load(SL, k + 4);
         }
       };
