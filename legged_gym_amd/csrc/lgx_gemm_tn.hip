@@ -713,6 +713,17 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
           acc[i][j] = c;
           side(2 * i + j);
+          if (i == 1 && j == 1) {   // the last block (no side unit): stage k + 1's block-0 fragments,
+            pre_a(tlds + off_n, 0);   // dead since block (1, 0), two reads per MFMA (104 / 101 vs
+            pre_b(tlds + off_n, 0);   // 106 / 104 us for dW1 / dW2 at S = 16 with all 24 after it)
+#pragma unroll
+            for (int x = 0; x < 6; ++x) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+          }
           // the side unit spread over the block's MFMA shadows: per MFMA up to 4 VALU and one LDS
           // instruction (the compiler's own placement bunched them after the block: dW1 / dW2 at
           // S = 16 112.7 / 111.1 -> 107.8 / 105.4 us; 2 VALU per MFMA 113 / 112, 6 VALU 108 / 107)
@@ -731,10 +742,12 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
       RING_STAMP(2);
       off_c = off_n;
       off_w = off_w == 2 * X::STAGE ? 0u : off_w + X::STAGE;
-      // stage k + 1's fragments (complete since the last barrier).  Not earlier: issued as soon as
-      // their registers die (A block 0 after MFMA block (0, 1), B block 0 after (1, 0)) they
+      // the rest of stage k + 1's fragments (complete since the last barrier; after the last stage
+      // a stale buffer, unused - no branch in the loop).  Without the group schedule, issuing the
+      // block-0 fragments as their registers die (A after MFMA block (0, 1), B after (1, 0))
       // lengthened the MFMA region by 130-190 cycles per stage and the kernel by 6 %
-      prefetch(tlds + off_n);   // (after the last stage: a stale buffer, unused - no branch in the loop)
+      pre_a(tlds + off_n, 1);
+      pre_b(tlds + off_n, 1);
       RING_STAMP(3);
       raw_barrier();
       __builtin_amdgcn_sched_barrier(0);   // (no MFMA of stage k + 1 above the barrier)
