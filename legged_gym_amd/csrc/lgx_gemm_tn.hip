@@ -21,6 +21,13 @@
 //     MFMA blocks;
 //     persistent workgroups over XCD-contiguous tile ranges (column tiles of one (n, s, z) adjacent:
 //     the A rows stay in that XCD's L2).
+// Kernel forms (all bitwise equal on the same slices; tests/test_gpu_gemm.py):
+//   * gemm_tn_ring_kernel<256> - the default for R % 256 == 0 (dW1, dW2): 256 x 128 tiles on 8 waves,
+//     16-row stages in a 3-deep LDS ring, each stage's fragments read before the barrier that opens it,
+//     side work and next-stage reads placed in the MFMA shadows (sched_group_barrier);
+//   * gemm_tn_ws_kernel<128> - R % 256 != 0 (dW3): producer waves stage and split, consumer waves
+//     read fragments and issue MFMAs (LGX_TN_WS=0: gemm_tn_x3_kernel<4>);
+//   * gemm_tn_x3_kernel<NWV> - the two-buffer form described above (LGX_TN_RING=0 for 256-row tiles).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
