@@ -81,8 +81,7 @@ GEMM_NOTES = {1: "lgx_gemm_nt LGX_GEMM_BIAS_ELU: hidden-layer forwards of actor 
               3: "lgx_gemm_nt LGX_GEMM_DELU: backward dA of the hidden layers (512x256 and 256x128 weights; the "
                  "bias gradients come from lgx_gemm_tn's column sums)",
               "tn": "lgx_gemm_tn: weight gradients dW_k = dZ_k^T Y_{k-1} of the hidden layers over row slices "
-                    "(512x235, 256x512 on the LDS-ring gemm_tn_ring_kernel<256>; 128x256 on the warp-specialised "
-                    "gemm_tn_ws_kernel<128>; "
+                    "(512x235, 256x512 on the LDS-ring gemm_tn_ring_kernel<256>; 128x256 on gemm_tn_ring_kernel<128>; "
                     "per network)"}
 
 

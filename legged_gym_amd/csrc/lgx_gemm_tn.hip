@@ -22,12 +22,13 @@
 //     persistent workgroups over XCD-contiguous tile ranges (column tiles of one (n, s, z) adjacent:
 //     the A rows stay in that XCD's L2).
 // Kernel forms (all bitwise equal on the same slices; tests/test_gpu_gemm.py):
-//   * gemm_tn_ring_kernel<256> - the default for R % 256 == 0 (dW1, dW2): 256 x 128 tiles on 8 waves,
-//     16-row stages in a 3-deep LDS ring, each stage's fragments read before the barrier that opens it,
-//     side work and next-stage reads placed in the MFMA shadows (sched_group_barrier);
-//   * gemm_tn_ws_kernel<128> - R % 256 != 0 (dW3): producer waves stage and split, consumer waves
-//     read fragments and issue MFMAs (LGX_TN_WS=0: gemm_tn_x3_kernel<4>);
-//   * gemm_tn_x3_kernel<NWV> - the two-buffer form described above (LGX_TN_RING=0 for 256-row tiles).
+//   * gemm_tn_ring_kernel<RA> - the default: RA x 128 tiles on 8 waves (RA = 256 for R % 256 == 0:
+//     dW1, dW2; 128 otherwise: dW3), 16-row stages in a 3-deep LDS ring, each stage's fragments read
+//     before the barrier that opens it, side work and next-stage reads placed in the MFMA shadows
+//     (sched_group_barrier);
+//   * with LGX_TN_RING=0: gemm_tn_ws_kernel<128> for 128-row tiles (producer waves stage and split,
+//     consumer waves read fragments and issue MFMAs; LGX_TN_WS=0: gemm_tn_x3_kernel<4>) and
+//     gemm_tn_x3_kernel<8>, the two-buffer form described above, for 256-row tiles.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -574,14 +575,18 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ws_kernel(TnArgs g) {
 // back edge behind vmcnt waits: 3 % slower than the old kernel).
 constexpr int TR = 16;   // rows per ring stage
 
+template <int RA_>
 struct TRing {
-  static constexpr int RA = 256;
-  static constexpr int IMGA = 3 * TR * RA * 2;       // 24 KB
+  static constexpr int RA = RA_;
+  static constexpr int WI = RA / 128;                // 32-row accumulator blocks per wave (wave: 32 WI x 64)
+  static constexpr int AQ = RA / 4;                  // column quads of an A row
+  static constexpr int AR = RA / 128;                // A rows per thread and stage
+  static constexpr int IMGA = 3 * TR * RA * 2;       // 24 | 12 KB
   static constexpr int IMGB = 3 * TR * TT * 2;       // 12 KB
-  static constexpr int STAGE = IMGA + IMGB;          // 36 KB
+  static constexpr int STAGE = IMGA + IMGB;          // 36 | 24 KB
   static constexpr int NB = 3;                       // ring depth
-  static constexpr int CS = 8 * 64 * 16;             // column-sum scratch: [row group][column quad] float4
-  static constexpr int LDS = NB * STAGE + CS;        // 116 KB
+  static constexpr int CS = 512 * 16;                // column-sum scratch: [row group][column quad] float4
+  static constexpr int LDS = NB * STAGE + CS;        // 116 | 80 KB
 };
 
 __device__ __forceinline__ void raw_barrier() {
@@ -590,10 +595,10 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int RA>   // (256: the only instantiation; a template for the profiles' name pattern gemm_tn_*_kernel<*>)
+template <int RA>   // 256: dW1 / dW2 (wave blocks of 64 x 64); 128: wave blocks of 32 x 64
 __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
-  using X = TRing;
-  static_assert(RA == X::RA, "ring tiles are 256 rows");
+  using X = TRing<RA>;
+  constexpr int WI = X::WI, AR = X::AR, AQ = X::AQ;
   extern __shared__ __attribute__((aligned(16))) char tlds[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r = lane & 31, h = lane >> 5;
@@ -601,14 +606,13 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
   const int q = (lane >> 2) & 3, p = lane & 3, gb = (lane >> 4) & 1;
   const int lane_a = (8 * h + q) * (RA * 2) + (4 * gb + p) * 8;
   const int lane_b = (8 * h + q) * (TT * 2) + (4 * gb + p) * 8;
-  int xa[2], xb[2];
+  int xa[WI], xb[2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    xa[i] = 64 * ((2 * wm + i) ^ q);
-    xb[i] = 64 * ((2 * wn + i) ^ q);
-  }
-  // staging: A thread = column quad aq of rows 2 am, 2 am + 1; B thread = column quad bq of row bm
-  const int aq = tid & 63, am = tid >> 6;
+  for (int i = 0; i < WI; ++i) xa[i] = 64 * ((WI * wm + i) ^ q);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) xb[j] = 64 * ((2 * wn + j) ^ q);
+  // staging: A thread = column quad aq of rows AR am .. AR am + AR - 1; B thread = column quad bq of row bm
+  const int aq = tid % AQ, am = tid / AQ;
   const int bq = tid & 31, bm = tid >> 5;
   const int xcd = blockIdx.x & 7;
   const int32_t stride = gridDim.x >> 3;
@@ -626,25 +630,25 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
     const int64_t m0 = (int64_t)s * g.Ms;
     const char* Ab = reinterpret_cast<const char*>(g.A + z * g.sa + m0 * g.lda + ntile * RA);
     const char* Bb = reinterpret_cast<const char*>(g.B + z * g.sb + m0 * g.ldb + ctile * TT);
-    const uint32_t oa = (2 * am) * sta + aq * 16, ob = bm * stb + bq * 16;
+    const uint32_t oa = (AR * am) * sta + aq * 16, ob = bm * stb + bq * 16;
     const bool csum = g.colsum != nullptr && ctile == 0;
     float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 ra[2][2], rb[2];          // register ring: stages k + 2 (slot k & 1) and k + 3
+    float4 ra[2][AR], rb[2];          // register ring: stages k + 2 (slot k & 1) and k + 3
     auto load = [&](int slot, int k) {
       const int kc = min(k, nst - 1);   // (past the last stage: re-loads, never written as a stage)
       const uint32_t la = oa + kc * TR * sta, lb = ob + kc * TR * stb;
-      ra[slot][0] = *reinterpret_cast<const float4*>(Ab + la);
-      ra[slot][1] = *reinterpret_cast<const float4*>(Ab + la + sta);
+#pragma unroll
+      for (int u = 0; u < AR; ++u) ra[slot][u] = *reinterpret_cast<const float4*>(Ab + la + u * sta);
       rb[slot] = *reinterpret_cast<const float4*>(Bb + lb);
     };
-    f32x16 acc[2][2];
+    f32x16 acc[WI][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    bf16x8 fa[2][3], fb[2][3];
+    bf16x8 fa[WI][3], fb[2][3];
     auto pre_a = [&](const char* ia, int i) {
 #pragma unroll
       for (int l = 0; l < 3; ++l) fa[i][l] = tn_frag<RA, TR>(ia, l, 0, lane_a, xa[i]);
@@ -655,10 +659,9 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
     };
     auto prefetch = [&](const char* ia) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        pre_a(ia, i);
-        pre_b(ia, i);
-      }
+      for (int i = 0; i < WI; ++i) pre_a(ia, i);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) pre_b(ia, j);
     };
     __syncthreads();   // (the previous tile's readers of the ring are done)
     // prologue: stages 0 and 1 into ring buffers 0 and 1, stages 2 and 3 in flight
@@ -669,10 +672,10 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
       char* wb = tlds + st * X::STAGE;
       const float cw = st < nst ? 1.f : 0.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < AR; ++i) {
         cs.x = fmaf(ra[st][i].x, cw, cs.x); cs.y = fmaf(ra[st][i].y, cw, cs.y);
         cs.z = fmaf(ra[st][i].z, cw, cs.z); cs.w = fmaf(ra[st][i].w, cw, cs.w);
-        tn_store_row<RA, TR>(wb, ra[st][i], aq, 2 * am + i);
+        tn_store_row<RA, TR>(wb, ra[st][i], aq, AR * am + i);
       }
       tn_store_row<TT, TR>(wb + X::IMGA, rb[st], bq, bm);
       load(st, st + 2);
@@ -697,18 +700,18 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
       char* wb = tlds + off_w;
       const uint32_t off_n = off_c == 2 * X::STAGE ? 0u : off_c + X::STAGE;   // stage k + 1
       const float cw = k + 2 < nst ? 1.f : 0.f;   // (stage k + 2 exists: else the idle buffer is written)
-      auto side = [&](int u) {
-        if (u < 2) {
+      auto side = [&](int u) {   // unit u < AR: A row u; u == AR: the B row and the next loads
+        if (u < AR) {
           cs.x = fmaf(ra[SL][u].x, cw, cs.x); cs.y = fmaf(ra[SL][u].y, cw, cs.y);
           cs.z = fmaf(ra[SL][u].z, cw, cs.z); cs.w = fmaf(ra[SL][u].w, cw, cs.w);
-          tn_store_row<RA, TR>(wb, ra[SL][u], aq, 2 * am + u);
-        } else if (u == 2) {
+          tn_store_row<RA, TR>(wb, ra[SL][u], aq, AR * am + u);
+        } else if (u == AR) {
           tn_store_row<TT, TR>(wb + X::IMGA, rb[SL], bq, bm);
           load(SL, k + 4);
         }
       };
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x16 c = acc[i][j];
@@ -720,13 +723,24 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], c, 0, 0, 0);
           acc[i][j] = c;
           side(2 * i + j);
-          if (i == 1 && j == 1) {   // the last block (no side unit): stage k + 1's block-0 fragments,
-            pre_a(tlds + off_n, 0);   // dead since block (1, 0), two reads per MFMA (104 / 101 vs
-            pre_b(tlds + off_n, 0);   // 106 / 104 us for dW1 / dW2 at S = 16 with all 24 after it)
+          if (WI == 2 && i == 1 && j == 1) {   // the last block (no side unit): stage k + 1's block-0
+            pre_a(tlds + off_n, 0);   // fragments, dead since block (1, 0), two reads per MFMA (104 /
+            pre_b(tlds + off_n, 0);   // 101 vs 106 / 104 us for dW1 / dW2 at S = 16 with all 24 after it)
 #pragma unroll
             for (int x = 0; x < 6; ++x) {
               __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
               __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            continue;
+          }
+          if (WI == 1 && j == 1) {   // the last block of a 32-row wave: its side unit and B block 0
+            pre_b(tlds + off_n, 0);
+#pragma unroll
+            for (int x = 0; x < 6; ++x) {
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+              __builtin_amdgcn_sched_group_barrier(0x100 | 0x200, 2, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             continue;
@@ -753,7 +767,7 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
       // a stale buffer, unused - no branch in the loop).  Without the group schedule, issuing the
       // block-0 fragments as their registers die (A after MFMA block (0, 1), B after (1, 0))
       // lengthened the MFMA region by 130-190 cycles per stage and the kernel by 6 %
-      pre_a(tlds + off_n, 1);
+      pre_a(tlds + off_n, WI - 1);
       pre_b(tlds + off_n, 1);
       RING_STAMP(3);
       raw_barrier();
@@ -763,29 +777,30 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_ring_kernel(TnArgs g) {
       step(std::integral_constant<int, 0>{}, k);
       step(std::integral_constant<int, 1>{}, k + 1);
     }
-    if (csum) {   // the 8 row groups' partial column sums, combined in a fixed order
+    if (csum) {   // the row groups' partial column sums, combined in a fixed order
+      constexpr int NG = 512 / AQ;   // 8 | 16 row groups
       float4* scr = reinterpret_cast<float4*>(tlds + X::NB * X::STAGE);
-      scr[am * 64 + aq] = cs;
+      scr[am * AQ + aq] = cs;
       __syncthreads();
-      if (tid < 64) {
+      if (tid < AQ) {
         float4 v = scr[tid];
 #pragma unroll
-        for (int i = 1; i < 8; ++i) {
-          const float4 u = scr[i * 64 + tid];
+        for (int i = 1; i < NG; ++i) {
+          const float4 u = scr[i * AQ + tid];
           v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
         }
         *reinterpret_cast<float4*>(g.colsum + (int64_t)(z * g.S + s) * g.R + ntile * RA + 4 * tid) = v;
       }
     }
     // acc[i][j][e] = C[n0 + 32i + 8(e >> 2) + 4h + (e & 3)][c0 + 32j + r]
-    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * RA + wm * 64) * g.ldc;
+    float* Cb = g.C + ((int64_t)(z * g.S + s) * g.R + ntile * RA + wm * 32 * WI) * g.ldc;
     const int c0 = ctile * TT + wn * 64 + r;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int c = c0 + 32 * j;
       if (c >= g.Cc) continue;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < WI; ++i)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int n = 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
@@ -824,16 +839,18 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
   g.ldc = a.ldc;
   g.colsum = a.colsum;
   if (a.colsum && ((uintptr_t)a.colsum & 15)) return lgx_fail(LGX_EINVAL, "lgx_gemm_tn: colsum must be 16-byte aligned");
-  // 256-row tiles (8 waves) when R allows, else 128-row tiles on the warp-specialised kernel
-  // (LGX_TN_WS, read per call for same-process A/B: 0 = the 4-wave kernel for 128-row tiles,
-  // 2 = the warp-specialised kernel for 256-row tiles too)
+  // 256-row tiles (8 waves) when R allows, else 128-row tiles; the ring form for both (LGX_TN_RING=0,
+  // read per call for same-process A/B: the warp-specialised kernel for 128-row tiles - LGX_TN_WS=0:
+  // the 4-wave gemm_tn_x3_kernel<4> - and gemm_tn_x3_kernel<8> for 256-row tiles - LGX_TN_WS=2: the
+  // warp-specialised kernel)
   const char* wsv = getenv("LGX_TN_WS");
   const int wsm = wsv && *wsv ? atoi(wsv) : 1;
   const int nwv = a.R % 256 == 0 ? 8 : 4;
   const int RA = nwv == 8 ? 256 : 128;
-  const bool ws = RA == 128 ? wsm != 0 : wsm == 2;
   const char* rgv = getenv("LGX_TN_RING");
-  const bool ring = RA == 256 && !ws && !(rgv && rgv[0] == '0') && (a.M / a.slices) % TR == 0;
+  const bool ringv = !(rgv && rgv[0] == '0') && (a.M / a.slices) % TR == 0;
+  const bool ring = ringv && RA == 256, ring128 = ringv && RA == 128;
+  const bool ws = !ringv && (RA == 128 ? wsm != 0 : wsm == 2);
   g.rt = a.R / RA;
   g.ct = (a.Cc + TT - 1) / TT;
   const int64_t tiles = (int64_t)g.rt * g.ct * a.slices * a.batch;
@@ -849,14 +866,18 @@ extern "C" int lgx_gemm_tn(const lgx_gemm_tn_args* args, void* stream) {
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ws_kernel<128>), hipFuncAttributeMaxDynamicSharedMemorySize,
                           TW<128>::LDS) == hipSuccess &&
       hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ring_kernel<256>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          TRing::LDS) == hipSuccess;
+                          TRing<256>::LDS) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_tn_ring_kernel<128>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          TRing<128>::LDS) == hipSuccess;
   if (!attrs) return lgx_fail(LGX_EHIP, "lgx_gemm_tn: hipFuncSetAttribute (dynamic LDS) failed");
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int64_t per_xcd = (tiles + 7) / 8;
   const int64_t wgs = 8 * std::min<int64_t>(per_xcd, std::max(1, cus / 8));
   if (ring)
-    LGX_LAUNCH(gemm_tn_ring_kernel<256>, dim3((unsigned)wgs), dim3(512), TRing::LDS, reinterpret_cast<hipStream_t>(stream), g);
+    LGX_LAUNCH(gemm_tn_ring_kernel<256>, dim3((unsigned)wgs), dim3(512), TRing<256>::LDS, reinterpret_cast<hipStream_t>(stream), g);
+  else if (ring128)
+    LGX_LAUNCH(gemm_tn_ring_kernel<128>, dim3((unsigned)wgs), dim3(512), TRing<128>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else if (ws && RA == 256)
     LGX_LAUNCH(gemm_tn_ws_kernel<256>, dim3((unsigned)wgs), dim3(512), TW<256>::LDS, reinterpret_cast<hipStream_t>(stream), g);
   else if (ws)

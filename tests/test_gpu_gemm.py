@@ -320,7 +320,7 @@ def test_gemm_tn_column_sums(gpu, M, S, R, Cc, ldb):
                                           (24576, 32, 128, 256, None), (24576, 16, 256, 512, None)])
 def test_gemm_tn_warp_specialised_equals_plain(gpu, monkeypatch, M, S, R, Cc, ldb):
     """The warp-specialised dW kernel (producer waves stage and split, consumer waves only read
-    fragments and issue MFMAs; the default for 128-row tiles) against gemm_tn_x3_kernel (LGX_TN_WS=0): the same products in
+    fragments and issue MFMAs; with LGX_TN_RING=0 the form for 128-row tiles) against gemm_tn_x3_kernel (LGX_TN_WS=0): the same products in
     the same order per output element, so the weight gradients are bitwise equal; the column sums
     (other per-thread row groups) within f32 rounding."""
     dev = "cuda:0"
@@ -328,6 +328,7 @@ def test_gemm_tn_warp_specialised_equals_plain(gpu, monkeypatch, M, S, R, Cc, ld
     ldb = ldb or Cc
     A = torch.randn(2, M, R, device=dev, generator=g)
     B = torch.randn(2, M, ldb, device=dev, generator=g)
+    monkeypatch.setenv("LGX_TN_RING", "0")
     outs = []
     for ws in ("2", "0"):        # (2: the warp-specialised kernel at both tile heights)
         monkeypatch.setenv("LGX_TN_WS", ws)
@@ -374,6 +375,35 @@ def test_gemm_tn_ring_equals_plain(gpu, monkeypatch, M, S, R, Cc, ldb):
         torch.cuda.synchronize()
         outs.append((Cout, cs))
     assert not torch.isnan(outs[0][0]).any()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5 * (M // S) ** 0.5)
+
+
+@pytest.mark.parametrize("M,S,R,Cc,ldb", [(2048, 4, 128, 235, 256), (96, 3, 128, 384, None), (160, 1, 384, 128, None),
+                                          (24576, 32, 128, 256, None), (24576, 16, 128, 256, None)])
+def test_gemm_tn_ring_128_row_tiles_equal_ws(gpu, monkeypatch, M, S, R, Cc, ldb):
+    """The ring form at 128-row tiles (the default: waves of 32 x 64) against the warp-specialised
+    kernel (LGX_TN_RING=0): bitwise weight gradients, column sums within f32 rounding."""
+    dev = "cuda:0"
+    g = torch.Generator(device=dev).manual_seed(M + R + 3)
+    ldb = ldb or Cc
+    A = torch.randn(2, M, R, device=dev, generator=g)
+    B = torch.randn(2, M, ldb, device=dev, generator=g)
+    monkeypatch.setenv("LGX_TN_WS", "1")
+    outs = []
+    for ring in ("1", "0"):
+        monkeypatch.setenv("LGX_TN_RING", ring)
+        Cout = torch.full((2, S, R, Cc), float("nan"), device=dev)
+        cs = torch.full((2, S, R), float("nan"), device=dev)
+        a = abi.LgxGemmTnArgs()
+        a.M, a.R, a.Cc, a.slices, a.batch = M, R, Cc, S, 2
+        a.A, a.lda, a.sa = A.data_ptr(), R, M * R
+        a.B, a.ldb, a.sb = B.data_ptr(), ldb, M * ldb
+        a.C, a.ldc, a.colsum = Cout.data_ptr(), Cc, cs.data_ptr()
+        lgxlib.check(_lib().lgx_gemm_tn(C.byref(a), _stream()), "lgx_gemm_tn")
+        torch.cuda.synchronize()
+        outs.append((Cout, cs))
+    assert not torch.isnan(outs[0][0]).any() and not torch.isnan(outs[0][1]).any()
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.allclose(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-5 * (M // S) ** 0.5)
 
