@@ -22,7 +22,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "--one":
             e.record(); torch.cuda.synchronize()
             res.append(s.elapsed_time(e) / 200 * 1e3)
     ref = ac.actor(obs)
-    print("max |mu - torch| =", float((mu0[0] - ref).abs().max()))
+    print("max |mu - torch| =", float((mu0[0] - ref).abs().max()), "checksum", repr(float(mu0[0].double().sum())),
+          repr(float(mu0[1].double().sum())))
     print(f"{os.environ.get('LGX_LIB_PATH','product')}: per call {min(res):.1f} us (min of 5), {sorted(res)[2]:.1f} median")
     sys.exit(0)
 for v in sys.argv[1:]:
